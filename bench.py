@@ -1,0 +1,212 @@
+#!/usr/bin/env python3
+"""Benchmark: Gibbs tokens sampled/sec at K=512 (BASELINE.json metric).
+
+Workload (one "step" = one full Gibbs sweep over the GPU's shard = sample
+kernel + [RCCL all-reduce of the nw/nwsum delta when N > 1] + apply):
+  config C4 of BASELINE.json (10M docs x 200 tokens, V=100k, K=512, 8 GPUs)
+  sharded AD-LDA style: every GPU holds 1.25M docs x 200 tokens (2.5e8
+  tokens), so N=8 is exactly C4 and N=1 is one C4 shard (weak scaling).
+Synthetic corpus: LDA generative process, drawn on the GPU.
+
+Prints ONE JSON line (rank 0).  value = tokens sampled by all ranks per
+second of the max-over-ranks wall time of the K timed sweeps.
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--config c4|c2|c3]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import platform
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+CONFIGS = {
+    # name: docs per GPU, doc length, V, K, description
+    "c4": dict(docs=1_250_000, doc_len=200, V=100_000, K=512,
+               desc="C4 shard: 1.25M docs x 200 tok per GPU, V=100k, K=512 (N=8 == C4: 10M docs)"),
+    "c2": dict(docs=100_000, doc_len=200, V=50_000, K=128, desc="C2: 100k docs x 200 tok, V=50k, K=128"),
+    "c3": dict(docs=100_000, doc_len=200, V=50_000, K=1024, desc="C3: 100k docs x 200 tok, V=50k, K=1024"),
+}
+HBM_PEAK_GBS = 8000.0   # MI355X spec (MI355X_MICROARCH.md: 8.0 TB/s)
+
+
+def bytes_per_token(K: int) -> int:
+    """SURVEY.md §8d fixed contract: 4K (int32 nw row gather) + 4 (word id)
+    + 4 (z read) + 4 (z write) + 4 (amortised nw/nwsum delta updates)."""
+    return 4 * K + 16
+
+
+def cpu_baseline(corpus, K, alpha_sum, beta, budget_s=15.0, threads=4):
+    """cpu_mallet (oracle/, the Mallet 2.0.7 SparseLDA restatement) timed on a
+    bounded sample of the same workload on this host's cores."""
+    from oracle import oracle as O
+    O.build()
+    ndocs = min(corpus.num_docs, 20_000)
+    sub = corpus.subset(np.arange(ndocs))
+    m = O.MalletModel(K, alpha_sum, beta, corpus.num_types, sub.doc_off, sub.words, seed=1,
+                      num_threads=threads)
+    m.estimate(2)                                    # warm-up sweeps
+    t0 = time.perf_counter()
+    sweeps = 0
+    while True:
+        m.estimate(1)
+        sweeps += 1
+        if time.perf_counter() - t0 >= budget_s or sweeps >= 50:
+            break
+    dt = time.perf_counter() - t0
+    return {
+        "value": sub.num_tokens * sweeps / dt,
+        "unit": "tokens/s",
+        "cores": threads,
+        "kind": "port",
+        "sample": (f"cpu_mallet (Mallet 2.0.7 SparseLDA restatement, oracle/lda_oracle.c), "
+                   f"{threads} threads (= setNumThreads(4), src/cmu_ron/TrainAndPredict.java:164), "
+                   f"first {ndocs} docs ({sub.num_tokens} tokens) of this workload, "
+                   f"{sweeps} timed sweeps after 2 warm-up, host {platform.processor() or platform.machine()}"),
+    }
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", default="c4", choices=sorted(CONFIGS))
+    ap.add_argument("--docs", type=int, default=0, help="override docs per GPU")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-budget", type=float, default=15.0)
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
+    torch.cuda.set_device(local_rank)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+
+    from ldagibbssampling_amd.corpus import synthetic_lda_torch
+    from ldagibbssampling_amd.sampler import GibbsSampler
+
+    cfg = CONFIGS[args.config]
+    K, V, L = cfg["K"], cfg["V"], cfg["doc_len"]
+    docs = args.docs or cfg["docs"]
+    alpha_sum, beta = 0.1 * K, 0.01
+    t_gen = time.perf_counter()
+    corpus = synthetic_lda_torch(docs, V, K, doc_len=L, seed=20261015 + rank,
+                                 device=f"cuda:{local_rank}")
+    t_gen = time.perf_counter() - t_gen
+    n_local = corpus.num_tokens
+    sampler = GibbsSampler(K, V, corpus.doc_off, corpus.words, np.full(K, alpha_sum / K), beta,
+                           seed=1, device=local_rank, token_base=rank * n_local)
+    stream = torch.cuda.current_stream()
+    sampler.set_stream(stream.cuda_stream)
+    delta = sampler.delta_tensor() if world > 1 else None
+
+    def step():
+        sampler.sample()
+        if world > 1:
+            dist.all_reduce(delta)           # AD-LDA: sum of every rank's nw/nwsum delta
+        sampler.apply()
+
+    # initial global counts
+    if world > 1:
+        dist.all_reduce(delta)
+    sampler.apply()
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    kernel_ms = []
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+        kernel_ms.append(None)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    # per-launch kernel duration of the sampler (HIP events on its stream):
+    # a separate, identical pass so that the timed loop carries no host syncs.
+    ks = []
+    for _ in range(3):
+        sampler.sample()
+        ks.append(sampler.last_sample_ms())
+        if world > 1:
+            dist.all_reduce(delta)
+        sampler.apply()
+    torch.cuda.synchronize()
+    kern_ms = float(np.mean(ks))
+
+    t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local_rank}")
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed = float(t.item())
+    total_tokens = n_local * world * args.steps
+    value = total_tokens / elapsed
+    ll = sampler.log_likelihood_parts()
+
+    if rank == 0:
+        bpt = bytes_per_token(K)
+        achieved = n_local * bpt / (kern_ms * 1e-3) / 1e9      # GB/s, algorithmic
+        result = {
+            "metric": "Gibbs tokens sampled/sec at K=512",
+            "value": value,
+            "unit": "tokens/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed * 1e3 / args.steps,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "fp32 weights / int32 counts",
+            "data": "synthetic (LDA generative process, SURVEY.md §8d; phi~Dir(0.01), theta~Dir(0.1))",
+            "config": {
+                "workload": cfg["desc"],
+                "docs_per_gpu": docs,
+                "doc_len": L,
+                "tokens_per_gpu": n_local,
+                "num_types": V,
+                "num_topics": K,
+                "alpha_sum": alpha_sum,
+                "beta": beta,
+                "parallelism": f"dp{world} (AD-LDA doc shards, RCCL all-reduce of int32 delta)",
+            },
+            "roofline": {
+                "bound": "hbm",
+                "achieved": achieved,
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": achieved / HBM_PEAK_GBS,
+                "traffic": None,
+                "kernel": f"k_sample<C={sampler.Kp // 64}> avg {kern_ms:.3f} ms/launch over "
+                          f"{n_local} tokens, B(K)={bpt} B/token",
+            },
+            "ll_per_token_rank0": (ll[0] + ll[1]) / n_local if world == 1 else None,
+            "corpus_gen_s": t_gen,
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            result["cpu_baseline"] = cpu_baseline(corpus, K, alpha_sum, beta, args.cpu_budget)
+        print(json.dumps(result), flush=True)
+    sampler.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,151 @@
+/*
+ * lda_mi355x.h — C ABI of the MI355X-native collapsed-Gibbs LDA sampler.
+ *
+ * This is the drop-in boundary for the reference's only hot path: the
+ * per-token z-resampling loop that qianjinding/LDAGibbsSampling delegates to
+ * Mallet 2.0.7 (pom.xml:107-111) through
+ *     ParallelTopicModel.estimate()            src/cmu_ron/TrainAndPredict.java:166
+ *                                              src/cmu/TrainAndPredict.java:265
+ * and from there WorkerRunnable.sampleTopicsForOneDoc (Mallet, not vendored).
+ * The reference has no FFI of its own; the seam is Mallet's public class API
+ * as called from trainNewModel (src/cmu_ron/TrainAndPredict.java:159-171,
+ * src/cmu/TrainAndPredict.java:258-269).  Each entry point below names the
+ * Mallet call it replaces; INTEGRATION.md shows the JNI binding a Java
+ * maintainer adds (GpuParallelTopicModel extends ParallelTopicModel).
+ *
+ * Conventions
+ *  - Plain pointers and sizes only.  The caller owns every host buffer;
+ *    lda_create copies its inputs into device memory and no pointer is kept
+ *    after a call returns (except lda_delta_buffer's device pointer, which is
+ *    owned by the context).
+ *  - Every call returns an lda_status (0 = OK, < 0 = error class);
+ *    lda_last_error() gives a thread-local message.  No C++ exception crosses
+ *    the ABI.
+ *  - One context = one GPU = one caller thread (not re-entrant per context).
+ *    Multi-GPU: one process (or thread) per GPU, each with a context over its
+ *    own document shard, exchanging the nw/nwsum delta buffer with an
+ *    all-reduce between lda_sample() and lda_apply() (AD-LDA).
+ *  - Counts are int32 (exact).  Sampling weights are fp32, evaluated in the
+ *    fixed order documented in DESIGN.md so that z/nw/nwsum/nd are bit-exact
+ *    against the CPU oracle and independent of GPU count and scheduling.
+ */
+#ifndef LDA_MI355X_H
+#define LDA_MI355X_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef int32_t lda_status;
+#define LDA_OK 0
+#define LDA_ERR_INVALID_ARG (-1)
+#define LDA_ERR_DEVICE (-2)       /* HIP runtime / kernel launch failure */
+#define LDA_ERR_OUT_OF_MEMORY (-3)
+#define LDA_ERR_STATE (-4)        /* call out of order (e.g. sample with a pending delta) */
+#define LDA_ERR_UNSUPPORTED (-5)  /* e.g. K above the compiled maximum */
+
+#define LDA_MAX_TOPICS 1024       /* dense-kernel instantiations: K <= 1024 */
+
+typedef struct lda_ctx lda_ctx;
+
+typedef struct lda_config {
+  int32_t num_topics;     /* K      (ParallelTopicModel(numberOfTopics, ...)) */
+  int32_t num_types;      /* V      (alphabet size; word ids are 0..V-1)       */
+  int64_t num_docs;       /* D      documents in THIS shard                    */
+  const double* alpha;    /* [K] per-topic alpha (alphaSum/K when symmetric)   */
+  double beta;            /* beta   (ParallelTopicModel(.., .., beta))         */
+  uint64_t seed;          /* Philox key (ParallelTopicModel.setRandomSeed)     */
+  int32_t device;         /* HIP device ordinal                                */
+  int32_t reserved0;
+  int64_t token_base;     /* global index of this shard's first token          */
+  int64_t tokens_per_range; /* work-queue granule (0 = default)                */
+} lda_config;
+
+/* Create a sampler over one shard.  doc_off[D+1] (int64, doc_off[0] may be
+ * non-zero: offsets are rebased), words[N] (int32 word ids), z_init[N] or NULL
+ * (NULL = Philox initialisation, the GPU analogue of addInstances' random
+ * topics).  The shard's own counts are left as the PENDING delta: call
+ * lda_apply (after an all-reduce of lda_delta_buffer when sharded) before the
+ * first lda_sample.  Replaces ParallelTopicModel(K, alphaSum, beta) +
+ * addInstances(InstanceList)  [src/cmu_ron/TrainAndPredict.java:160-162]. */
+lda_status lda_create(lda_ctx** out, const lda_config* cfg, const int64_t* doc_off,
+                      const int32_t* words, const int32_t* z_init);
+void lda_destroy(lda_ctx* ctx);
+
+/* Run n full sweeps on a single (unsharded) context: apply any pending delta,
+ * then n x (sample + apply).  Replaces ParallelTopicModel.estimate() with
+ * setNumIterations(n) and optimizeInterval 0 [src/cmu_ron/TrainAndPredict.java:165-166]. */
+lda_status lda_sweep(lda_ctx* ctx, int32_t n);
+
+/* One sampling pass over the shard against the current nw/nwsum snapshot;
+ * changes go to the delta buffer (one sweep of WorkerRunnable.run()). */
+lda_status lda_sample(lda_ctx* ctx);
+/* Device pointer to the pending delta: int32[V*Kp + Kp] (nw delta row-major
+ * with padded row length Kp = lda_padded_topics(), then nwsum delta).  Sum it
+ * across ranks in place (the sumTypeTopicCounts analogue) before lda_apply. */
+lda_status lda_delta_buffer(lda_ctx* ctx, void** dev_ptr, size_t* count);
+/* nw += delta, nwsum += delta, delta = 0, refresh the per-topic tables. */
+lda_status lda_apply(lda_ctx* ctx);
+
+/* The HIP stream every call of this context is ordered on (hipStream_t;
+ * NULL = the context's own stream). */
+lda_status lda_set_stream(lda_ctx* ctx, void* hip_stream);
+lda_status lda_get_stream(lda_ctx* ctx, void** hip_stream);
+lda_status lda_synchronize(lda_ctx* ctx);
+
+/* Sweep counter (the Philox counter word that keys a sampling pass). */
+lda_status lda_get_sweep(lda_ctx* ctx, uint32_t* sweep);
+lda_status lda_set_sweep(lda_ctx* ctx, uint32_t sweep);
+
+int32_t lda_padded_topics(int32_t num_topics);
+lda_status lda_get_shape(lda_ctx* ctx, int32_t* K, int32_t* Kp, int32_t* V, int64_t* D,
+                         int64_t* N);
+
+/* Copy state out (caller-allocated host buffers; NULL skips an output).
+ * z[N]; nw[V*K] row-major (unpadded); nwsum[K]; nd[D*K]; ndsum[D]. */
+lda_status lda_get_z(lda_ctx* ctx, int32_t* z);
+lda_status lda_set_z(lda_ctx* ctx, const int32_t* z); /* re-seeds counts as pending delta */
+lda_status lda_get_counts(lda_ctx* ctx, int32_t* nw, int32_t* nwsum, int32_t* nd,
+                          int32_t* ndsum);
+
+/* Replace alpha[K] / beta (host-side hyperparameter optimisation,
+ * ParallelTopicModel.optimizeAlpha/optimizeBeta). */
+lda_status lda_set_alpha_beta(lda_ctx* ctx, const double* alpha, double beta);
+
+/* ParallelTopicModel.modelLogLikelihood() over this shard's documents:
+ * doc_part = sum_d [sum_k logG(a_k+n_dk)-logG(a_k)] - logG(A+n_d) + logG(A)
+ * (fp64, Dirichlet.logGammaStirling); word_part = the nw/nwsum terms (global,
+ * identical on every rank).  Total = sum over ranks of doc_part + word_part. */
+lda_status lda_log_likelihood_parts(lda_ctx* ctx, double* doc_part, double* word_part);
+lda_status lda_log_likelihood(lda_ctx* ctx, double* out); /* doc_part + word_part */
+
+/* TopicInferencer.getSampledDistribution(instance, n_iter, thin, burn_in)
+ * [src/cmu_ron/TrainAndPredict.java:144] batched over Dh held-out documents
+ * against the frozen model (out-of-vocabulary tokens removed by the caller).
+ * theta[Dh*K] (fp64, rows sum to 1). */
+lda_status lda_infer(lda_ctx* ctx, int64_t Dh, const int64_t* doc_off, const int32_t* words,
+                     int32_t n_iter, int32_t burn_in, int32_t thin, uint64_t seed,
+                     double* theta);
+
+/* Mallet-layout adapter: typeTopicCounts as packed (count << topic_bits) |
+ * topic rows sorted descending, rows[row_off[w] .. row_off[w+1]) with
+ * row_off[V+1]; row length = min(K, typeTotal[w]) exactly as Mallet allocates
+ * it, trailing cells 0.  Pass rows = NULL to get row_off / total / topic_bits
+ * only. */
+lda_status lda_to_mallet_packed(lda_ctx* ctx, int32_t* rows, int64_t* row_off,
+                                int32_t* topic_bits);
+
+/* Kernel-level timing of the last lda_sample (ms, HIP events on the
+ * context's stream). */
+lda_status lda_last_sample_ms(lda_ctx* ctx, float* ms);
+
+const char* lda_last_error(void);
+const char* lda_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* LDA_MI355X_H */

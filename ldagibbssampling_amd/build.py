@@ -1,0 +1,23 @@
+"""Build the in-tree HIP library (hipcc, gfx950) and the CPU oracle (gcc)."""
+from __future__ import annotations
+
+import os
+import subprocess
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+
+
+def build_library(jobs: int = 2) -> str:
+    subprocess.run(["make", "-s", f"-j{jobs}", "-C", os.path.join(HERE, "csrc")], check=True)
+    return os.path.join(HERE, "lib", "liblda_mi355x.so")
+
+
+def build_oracle() -> str:
+    subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle")], check=True)
+    return os.path.join(ROOT, "oracle", "lib", "liblda_oracle.so")
+
+
+if __name__ == "__main__":
+    print(build_library())
+    print(build_oracle())

@@ -1,0 +1,113 @@
+"""ctypes binding of the C ABI in include/lda_mi355x.h (liblda_mi355x.so).
+
+The library is built in-tree (ldagibbssampling_amd/lib/) by build.py /
+__graft_entry__.build().  There is no CPU fallback: if the library is missing
+or cannot be loaded, importing the sampler raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "lib", "liblda_mi355x.so")
+HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "lda_mi355x.h")
+
+LDA_OK = 0
+STATUS_NAMES = {
+    -1: "LDA_ERR_INVALID_ARG",
+    -2: "LDA_ERR_DEVICE",
+    -3: "LDA_ERR_OUT_OF_MEMORY",
+    -4: "LDA_ERR_STATE",
+    -5: "LDA_ERR_UNSUPPORTED",
+}
+MAX_TOPICS = 1024
+
+
+class LdaError(RuntimeError):
+    def __init__(self, status: int, where: str, message: str):
+        self.status = status
+        super().__init__(f"{where}: {STATUS_NAMES.get(status, status)}: {message}")
+
+
+class lda_config(C.Structure):
+    _fields_ = [
+        ("num_topics", C.c_int32),
+        ("num_types", C.c_int32),
+        ("num_docs", C.c_int64),
+        ("alpha", C.POINTER(C.c_double)),
+        ("beta", C.c_double),
+        ("seed", C.c_uint64),
+        ("device", C.c_int32),
+        ("reserved0", C.c_int32),
+        ("token_base", C.c_int64),
+        ("tokens_per_range", C.c_int64),
+    ]
+
+
+_i32p = np.ctypeslib.ndpointer(dtype=np.int32, flags="C_CONTIGUOUS")
+_i64p = np.ctypeslib.ndpointer(dtype=np.int64, flags="C_CONTIGUOUS")
+_f64p = np.ctypeslib.ndpointer(dtype=np.float64, flags="C_CONTIGUOUS")
+_vp = C.c_void_p
+
+# name -> (restype, argtypes); every symbol include/lda_mi355x.h declares.
+SIGNATURES = {
+    "lda_create": (C.c_int32, [C.POINTER(_vp), C.POINTER(lda_config), _i64p, _vp, _vp]),
+    "lda_destroy": (None, [_vp]),
+    "lda_sweep": (C.c_int32, [_vp, C.c_int32]),
+    "lda_sample": (C.c_int32, [_vp]),
+    "lda_delta_buffer": (C.c_int32, [_vp, C.POINTER(_vp), C.POINTER(C.c_size_t)]),
+    "lda_apply": (C.c_int32, [_vp]),
+    "lda_set_stream": (C.c_int32, [_vp, _vp]),
+    "lda_get_stream": (C.c_int32, [_vp, C.POINTER(_vp)]),
+    "lda_synchronize": (C.c_int32, [_vp]),
+    "lda_get_sweep": (C.c_int32, [_vp, C.POINTER(C.c_uint32)]),
+    "lda_set_sweep": (C.c_int32, [_vp, C.c_uint32]),
+    "lda_padded_topics": (C.c_int32, [C.c_int32]),
+    "lda_get_shape": (C.c_int32, [_vp, C.POINTER(C.c_int32), C.POINTER(C.c_int32),
+                                  C.POINTER(C.c_int32), C.POINTER(C.c_int64), C.POINTER(C.c_int64)]),
+    "lda_get_z": (C.c_int32, [_vp, _i32p]),
+    "lda_set_z": (C.c_int32, [_vp, _i32p]),
+    "lda_get_counts": (C.c_int32, [_vp, _vp, _vp, _vp, _vp]),
+    "lda_set_alpha_beta": (C.c_int32, [_vp, _f64p, C.c_double]),
+    "lda_log_likelihood_parts": (C.c_int32, [_vp, C.POINTER(C.c_double), C.POINTER(C.c_double)]),
+    "lda_log_likelihood": (C.c_int32, [_vp, C.POINTER(C.c_double)]),
+    "lda_infer": (C.c_int32, [_vp, C.c_int64, _i64p, _i32p, C.c_int32, C.c_int32, C.c_int32,
+                              C.c_uint64, _f64p]),
+    "lda_to_mallet_packed": (C.c_int32, [_vp, _vp, _i64p, C.POINTER(C.c_int32)]),
+    "lda_last_sample_ms": (C.c_int32, [_vp, C.POINTER(C.c_float)]),
+    "lda_last_error": (C.c_char_p, []),
+    "lda_version": (C.c_char_p, []),
+}
+
+_lib = None
+
+
+def load(path: str = LIB_PATH):
+    """Load liblda_mi355x.so; raises if it is missing (no CPU fallback)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise ImportError(
+            f"{path} not found: build the HIP extension first "
+            "(python -c 'import __graft_entry__ as g; g.build()')")
+    L = C.CDLL(path)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(L, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = L
+    return L
+
+
+def check(status: int, where: str):
+    if status != LDA_OK:
+        msg = load().lda_last_error()
+        raise LdaError(status, where, msg.decode() if msg else "")
+
+
+def padded_topics(K: int) -> int:
+    return int(load().lda_padded_topics(K))

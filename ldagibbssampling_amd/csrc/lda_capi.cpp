@@ -1,0 +1,627 @@
+// lda_capi.cpp — the C ABI (include/lda_mi355x.h) over the gfx950 kernels.
+//
+// One lda_ctx = one document shard on one GPU.  Device layout:
+//   words[N] int32, z[N] int32           token stream, documents contiguous
+//   doc_off[D+1] int64, range_doc[R+1]   documents / work ranges
+//   nw[V*Kp] int32 (row = word type, Kp = K rounded up to 64), nwsum[Kp]
+//   delta[V*Kp + Kp] int32               pending nw / nwsum changes (the
+//                                        buffer an AD-LDA all-reduce sums)
+//   alpha_f/inv/inv_m1[Kp] fp32          per-topic tables of the snapshot
+// Mallet equivalents: nw ~ typeTopicCounts, nwsum ~ tokensPerTopic, z ~
+// TopicAssignment.topicSequence, nd ~ WorkerRunnable.localTopicCounts (never
+// stored: rebuilt from z per document inside the kernel).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/lda_mi355x.h"
+#include "lda_kernels.h"
+
+namespace {
+
+thread_local std::string g_last_error;
+
+lda_status fail(lda_status code, const std::string& msg) {
+  g_last_error = msg;
+  return code;
+}
+
+#define HIP_TRY(expr)                                                                     \
+  do {                                                                                    \
+    hipError_t e_ = (expr);                                                               \
+    if (e_ != hipSuccess)                                                                 \
+      return fail(e_ == hipErrorOutOfMemory ? LDA_ERR_OUT_OF_MEMORY : LDA_ERR_DEVICE,     \
+                  std::string(#expr) + ": " + hipGetErrorString(e_));                     \
+  } while (0)
+
+int pad_topics(int K) { return (K + 63) / 64 * 64; }
+
+double log_gamma_stirling(double z) {  // Dirichlet.logGammaStirling [M]
+  const double HALF_LOG_TWO_PI = 0.91893853320467274178;
+  int shift = 0;
+  while (z < 2) {
+    z += 1.0;
+    ++shift;
+  }
+  double result = HALF_LOG_TWO_PI + (z - 0.5) * std::log(z) - z + 1 / (12 * z) -
+                  1 / (360 * z * z * z) + 1 / (1260 * z * z * z * z * z);
+  while (shift > 0) {
+    --shift;
+    z -= 1.0;
+    result -= std::log(z);
+  }
+  return result;
+}
+
+// Group whole documents into work ranges of about `target` tokens.
+std::vector<int64_t> make_ranges(const std::vector<int64_t>& off, int64_t target) {
+  std::vector<int64_t> r;
+  const int64_t D = (int64_t)off.size() - 1;
+  r.push_back(0);
+  int64_t start_tok = off[0];
+  for (int64_t d = 0; d < D; ++d) {
+    if (off[d + 1] - start_tok >= target) {
+      r.push_back(d + 1);
+      start_tok = off[d + 1];
+    }
+  }
+  if (r.back() != D) r.push_back(D);
+  return r;
+}
+
+template <typename T>
+hipError_t dalloc(T** p, size_t n) {
+  *p = nullptr;
+  if (n == 0) n = 1;
+  return hipMalloc(reinterpret_cast<void**>(p), n * sizeof(T));
+}
+
+}  // namespace
+
+struct lda_ctx {
+  int device = 0;
+  hipStream_t own_stream = nullptr;
+  hipStream_t stream = nullptr;
+  int32_t K = 0, Kp = 0, C = 0, V = 0;
+  int64_t D = 0, N = 0, R = 0;
+  std::vector<double> alpha;
+  double beta = 0.0;
+  uint64_t seed = 0;
+  int64_t token_base = 0;
+  uint32_t sweep = 0;
+  bool pending = true;
+  int cus = 256;
+  int sample_blocks = 0, sample_blocks_frozen = 0;
+  int64_t tokens_per_range = 0;
+  std::vector<int64_t> doc_off_h;
+
+  int32_t* words = nullptr;
+  int32_t* z = nullptr;
+  int64_t* doc_off = nullptr;
+  int64_t* range_doc = nullptr;
+  int32_t* queue = nullptr;
+  int32_t* nw = nullptr;
+  int32_t* nwsum = nullptr;
+  int32_t* delta = nullptr;
+  double* alpha_d = nullptr;
+  float* alpha_f = nullptr;
+  float* inv = nullptr;
+  float* inv_m1 = nullptr;
+  double* partial = nullptr;
+  unsigned long long* nonzero = nullptr;
+  int partial_blocks = 1024;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  bool timed = false;
+
+  ~lda_ctx() {
+    if (device >= 0) (void)hipSetDevice(device);
+    for (void* p : {(void*)words, (void*)z, (void*)doc_off, (void*)range_doc, (void*)queue,
+                    (void*)nw, (void*)nwsum, (void*)delta, (void*)alpha_d, (void*)alpha_f,
+                    (void*)inv, (void*)inv_m1, (void*)partial, (void*)nonzero})
+      if (p) (void)hipFree(p);
+    if (ev0) (void)hipEventDestroy(ev0);
+    if (ev1) (void)hipEventDestroy(ev1);
+    if (own_stream) (void)hipStreamDestroy(own_stream);
+  }
+
+  lda::SampleParams params(bool frozen) const {
+    lda::SampleParams p{};
+    p.words = words;
+    p.z = z;
+    p.doc_off = doc_off;
+    p.range_doc = range_doc;
+    p.num_ranges = R;
+    p.queue = queue;
+    p.nw = nw;
+    p.delta = delta;
+    p.dsum = delta + (int64_t)V * Kp;
+    p.alpha = alpha_f;
+    p.inv = inv;
+    p.inv_m1 = inv_m1;
+    p.beta = (float)beta;
+    p.K = K;
+    p.token_base = token_base;
+    p.k0 = (uint32_t)seed;
+    p.k1 = (uint32_t)(seed >> 32);
+    p.c2 = sweep;
+    p.c3 = lda::STREAM_SAMPLE;
+    (void)frozen;
+    return p;
+  }
+};
+
+static lda_status apply_impl(lda_ctx* c) {
+  HIP_TRY(hipSetDevice(c->device));
+  HIP_TRY(lda::launch_apply(c->nw, c->delta, (int64_t)c->V * c->Kp, c->stream));
+  HIP_TRY(lda::launch_prepare_topics(c->nwsum, c->delta + (int64_t)c->V * c->Kp, c->alpha_d,
+                                     c->beta, (double)c->V * c->beta, c->K, c->Kp, c->alpha_f,
+                                     c->inv, c->inv_m1, c->stream));
+  c->pending = false;
+  return LDA_OK;
+}
+
+static lda_status recount_impl(lda_ctx* c) {
+  // local (word, topic) counts of this shard become the pending delta
+  HIP_TRY(hipMemsetAsync(c->delta, 0, sizeof(int32_t) * ((size_t)c->V * c->Kp + c->Kp), c->stream));
+  HIP_TRY(hipMemsetAsync(c->nw, 0, sizeof(int32_t) * (size_t)c->V * c->Kp, c->stream));
+  HIP_TRY(hipMemsetAsync(c->nwsum, 0, sizeof(int32_t) * c->Kp, c->stream));
+  HIP_TRY(lda::launch_count(c->words, c->z, c->N, c->Kp, c->delta, c->delta + (int64_t)c->V * c->Kp,
+                            c->stream));
+  c->pending = true;
+  return LDA_OK;
+}
+
+extern "C" {
+
+const char* lda_last_error(void) { return g_last_error.c_str(); }
+const char* lda_version(void) { return "lda_mi355x 0.1.0 (gfx950)"; }
+int32_t lda_padded_topics(int32_t num_topics) { return pad_topics(num_topics); }
+
+lda_status lda_create(lda_ctx** out, const lda_config* cfg, const int64_t* doc_off,
+                      const int32_t* words, const int32_t* z_init) {
+  if (!out || !cfg || !doc_off) return fail(LDA_ERR_INVALID_ARG, "null argument");
+  *out = nullptr;
+  if (cfg->num_topics < 1) return fail(LDA_ERR_INVALID_ARG, "num_topics must be >= 1");
+  if (cfg->num_topics > LDA_MAX_TOPICS)
+    return fail(LDA_ERR_UNSUPPORTED, "num_topics above LDA_MAX_TOPICS (1024)");
+  if (cfg->num_types < 1) return fail(LDA_ERR_INVALID_ARG, "num_types must be >= 1");
+  if (cfg->num_docs < 0) return fail(LDA_ERR_INVALID_ARG, "num_docs must be >= 0");
+  if (!cfg->alpha) return fail(LDA_ERR_INVALID_ARG, "alpha is null");
+  if (!(cfg->beta > 0.0)) return fail(LDA_ERR_INVALID_ARG, "beta must be > 0");
+  for (int k = 0; k < cfg->num_topics; ++k)
+    if (!(cfg->alpha[k] > 0.0)) return fail(LDA_ERR_INVALID_ARG, "alpha must be > 0");
+  const int64_t D = cfg->num_docs;
+  std::vector<int64_t> off(D + 1);
+  for (int64_t d = 0; d <= D; ++d) {
+    off[d] = doc_off[d] - doc_off[0];
+    if (d > 0 && off[d] < off[d - 1]) return fail(LDA_ERR_INVALID_ARG, "doc_off not monotone");
+  }
+  const int64_t N = off[D];
+  if (N > 0 && !words) return fail(LDA_ERR_INVALID_ARG, "words is null");
+  for (int64_t i = 0; i < N; ++i)
+    if (words[i] < 0 || words[i] >= cfg->num_types)
+      return fail(LDA_ERR_INVALID_ARG, "word id out of range [0, V)");
+  if (z_init)
+    for (int64_t i = 0; i < N; ++i)
+      if (z_init[i] < 0 || z_init[i] >= cfg->num_topics)
+        return fail(LDA_ERR_INVALID_ARG, "z_init topic out of range [0, K)");
+
+  lda_ctx* c = new (std::nothrow) lda_ctx();
+  if (!c) return fail(LDA_ERR_OUT_OF_MEMORY, "host allocation");
+  c->device = cfg->device;
+  c->K = cfg->num_topics;
+  c->Kp = pad_topics(c->K);
+  c->C = c->Kp / 64;
+  c->V = cfg->num_types;
+  c->D = D;
+  c->N = N;
+  c->alpha.assign(cfg->alpha, cfg->alpha + c->K);
+  c->beta = cfg->beta;
+  c->seed = cfg->seed;
+  c->token_base = cfg->token_base;
+  c->doc_off_h = off;
+
+  auto bail = [&](lda_status s) {
+    delete c;
+    return s;
+  };
+#define CT(expr)                                    \
+  do {                                              \
+    hipError_t e_ = (expr);                         \
+    if (e_ != hipSuccess)                           \
+      return bail(fail(e_ == hipErrorOutOfMemory ? LDA_ERR_OUT_OF_MEMORY : LDA_ERR_DEVICE, \
+                       std::string(#expr) + ": " + hipGetErrorString(e_)));               \
+  } while (0)
+
+  CT(hipSetDevice(c->device));
+  CT(hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking));
+  c->stream = c->own_stream;
+  hipDeviceProp_t prop;
+  CT(hipGetDeviceProperties(&prop, c->device));
+  c->cus = prop.multiProcessorCount;
+  c->sample_blocks = lda::sample_blocks_per_cu(c->C, false) * c->cus;
+  c->sample_blocks_frozen = lda::sample_blocks_per_cu(c->C, true) * c->cus;
+  const int64_t waves = (int64_t)c->sample_blocks * 4;
+  int64_t tpr = cfg->tokens_per_range;
+  if (tpr <= 0) tpr = std::max<int64_t>(256, std::min<int64_t>(65536, N / std::max<int64_t>(1, waves * 8)));
+  c->tokens_per_range = tpr;
+  std::vector<int64_t> ranges = make_ranges(off, tpr);
+  c->R = (int64_t)ranges.size() - 1;
+
+  CT(dalloc(&c->words, N));
+  CT(dalloc(&c->z, N));
+  CT(dalloc(&c->doc_off, D + 1));
+  CT(dalloc(&c->range_doc, ranges.size()));
+  CT(dalloc(&c->queue, 4));
+  CT(dalloc(&c->nw, (size_t)c->V * c->Kp));
+  CT(dalloc(&c->nwsum, c->Kp));
+  CT(dalloc(&c->delta, (size_t)c->V * c->Kp + c->Kp));
+  CT(dalloc(&c->alpha_d, c->K));
+  CT(dalloc(&c->alpha_f, c->Kp));
+  CT(dalloc(&c->inv, c->Kp));
+  CT(dalloc(&c->inv_m1, c->Kp));
+  CT(dalloc(&c->partial, c->partial_blocks));
+  CT(dalloc(&c->nonzero, c->partial_blocks));
+  CT(hipEventCreate(&c->ev0));
+  CT(hipEventCreate(&c->ev1));
+
+  if (N > 0) CT(hipMemcpyAsync(c->words, words, sizeof(int32_t) * N, hipMemcpyHostToDevice, c->stream));
+  CT(hipMemcpyAsync(c->doc_off, off.data(), sizeof(int64_t) * (D + 1), hipMemcpyHostToDevice, c->stream));
+  CT(hipMemcpyAsync(c->range_doc, ranges.data(), sizeof(int64_t) * ranges.size(),
+                    hipMemcpyHostToDevice, c->stream));
+  CT(hipMemcpyAsync(c->alpha_d, c->alpha.data(), sizeof(double) * c->K, hipMemcpyHostToDevice, c->stream));
+  if (z_init) {
+    if (N > 0) CT(hipMemcpyAsync(c->z, z_init, sizeof(int32_t) * N, hipMemcpyHostToDevice, c->stream));
+  } else {
+    CT(lda::launch_init_z(c->z, N, c->K, c->token_base, (uint32_t)c->seed,
+                          (uint32_t)(c->seed >> 32), c->stream));
+  }
+  {
+    lda_status s = recount_impl(c);
+    if (s != LDA_OK) return bail(s);
+  }
+  CT(hipMemsetAsync(c->alpha_f, 0, sizeof(float) * c->Kp, c->stream));
+  CT(hipStreamSynchronize(c->stream));
+#undef CT
+  *out = c;
+  return LDA_OK;
+}
+
+void lda_destroy(lda_ctx* ctx) { delete ctx; }
+
+lda_status lda_set_stream(lda_ctx* c, void* s) {
+  if (!c) return fail(LDA_ERR_INVALID_ARG, "null ctx");
+  c->stream = s ? (hipStream_t)s : c->own_stream;
+  return LDA_OK;
+}
+
+lda_status lda_get_stream(lda_ctx* c, void** s) {
+  if (!c || !s) return fail(LDA_ERR_INVALID_ARG, "null argument");
+  *s = (void*)c->stream;
+  return LDA_OK;
+}
+
+lda_status lda_synchronize(lda_ctx* c) {
+  if (!c) return fail(LDA_ERR_INVALID_ARG, "null ctx");
+  HIP_TRY(hipSetDevice(c->device));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  return LDA_OK;
+}
+
+lda_status lda_get_sweep(lda_ctx* c, uint32_t* s) {
+  if (!c || !s) return fail(LDA_ERR_INVALID_ARG, "null argument");
+  *s = c->sweep;
+  return LDA_OK;
+}
+
+lda_status lda_set_sweep(lda_ctx* c, uint32_t s) {
+  if (!c) return fail(LDA_ERR_INVALID_ARG, "null ctx");
+  c->sweep = s;
+  return LDA_OK;
+}
+
+lda_status lda_get_shape(lda_ctx* c, int32_t* K, int32_t* Kp, int32_t* V, int64_t* D, int64_t* N) {
+  if (!c) return fail(LDA_ERR_INVALID_ARG, "null ctx");
+  if (K) *K = c->K;
+  if (Kp) *Kp = c->Kp;
+  if (V) *V = c->V;
+  if (D) *D = c->D;
+  if (N) *N = c->N;
+  return LDA_OK;
+}
+
+lda_status lda_apply(lda_ctx* c) {
+  if (!c) return fail(LDA_ERR_INVALID_ARG, "null ctx");
+  return apply_impl(c);
+}
+
+lda_status lda_sample(lda_ctx* c) {
+  if (!c) return fail(LDA_ERR_INVALID_ARG, "null ctx");
+  if (c->pending) return fail(LDA_ERR_STATE, "lda_sample with a pending delta: call lda_apply first");
+  HIP_TRY(hipSetDevice(c->device));
+  if (c->N > 0) {
+    HIP_TRY(hipMemsetAsync(c->queue, 0, sizeof(int32_t), c->stream));
+    const lda::SampleParams p = c->params(false);
+    const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>(c->sample_blocks, (c->R + 3) / 4));
+    HIP_TRY(hipEventRecord(c->ev0, c->stream));
+    HIP_TRY(lda::launch_sample(c->C, false, p, blocks, c->stream));
+    HIP_TRY(hipEventRecord(c->ev1, c->stream));
+    c->timed = true;
+  }
+  c->sweep++;
+  c->pending = true;
+  return LDA_OK;
+}
+
+lda_status lda_last_sample_ms(lda_ctx* c, float* ms) {
+  if (!c || !ms) return fail(LDA_ERR_INVALID_ARG, "null argument");
+  *ms = 0.0f;
+  if (!c->timed) return LDA_OK;
+  HIP_TRY(hipEventSynchronize(c->ev1));
+  HIP_TRY(hipEventElapsedTime(ms, c->ev0, c->ev1));
+  return LDA_OK;
+}
+
+lda_status lda_delta_buffer(lda_ctx* c, void** dev_ptr, size_t* count) {
+  if (!c || !dev_ptr || !count) return fail(LDA_ERR_INVALID_ARG, "null argument");
+  *dev_ptr = c->delta;
+  *count = (size_t)c->V * c->Kp + c->Kp;
+  return LDA_OK;
+}
+
+lda_status lda_sweep(lda_ctx* c, int32_t n) {
+  if (!c) return fail(LDA_ERR_INVALID_ARG, "null ctx");
+  if (n < 0) return fail(LDA_ERR_INVALID_ARG, "n must be >= 0");
+  if (c->pending) {
+    lda_status s = apply_impl(c);
+    if (s) return s;
+  }
+  for (int32_t i = 0; i < n; ++i) {
+    lda_status s = lda_sample(c);
+    if (s) return s;
+    s = apply_impl(c);
+    if (s) return s;
+  }
+  return LDA_OK;
+}
+
+lda_status lda_get_z(lda_ctx* c, int32_t* z) {
+  if (!c || !z) return fail(LDA_ERR_INVALID_ARG, "null argument");
+  HIP_TRY(hipSetDevice(c->device));
+  if (c->N > 0) HIP_TRY(hipMemcpyAsync(z, c->z, sizeof(int32_t) * c->N, hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  return LDA_OK;
+}
+
+lda_status lda_set_z(lda_ctx* c, const int32_t* z) {
+  if (!c || !z) return fail(LDA_ERR_INVALID_ARG, "null argument");
+  for (int64_t i = 0; i < c->N; ++i)
+    if (z[i] < 0 || z[i] >= c->K) return fail(LDA_ERR_INVALID_ARG, "topic out of range [0, K)");
+  HIP_TRY(hipSetDevice(c->device));
+  if (c->N > 0) HIP_TRY(hipMemcpyAsync(c->z, z, sizeof(int32_t) * c->N, hipMemcpyHostToDevice, c->stream));
+  lda_status s = recount_impl(c);
+  if (s) return s;
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  return LDA_OK;
+}
+
+lda_status lda_get_counts(lda_ctx* c, int32_t* nw, int32_t* nwsum, int32_t* nd, int32_t* ndsum) {
+  if (!c) return fail(LDA_ERR_INVALID_ARG, "null ctx");
+  HIP_TRY(hipSetDevice(c->device));
+  if (nw) {
+    HIP_TRY(hipMemcpy2DAsync(nw, sizeof(int32_t) * c->K, c->nw, sizeof(int32_t) * c->Kp,
+                             sizeof(int32_t) * c->K, c->V, hipMemcpyDeviceToHost, c->stream));
+  }
+  if (nwsum) HIP_TRY(hipMemcpyAsync(nwsum, c->nwsum, sizeof(int32_t) * c->K, hipMemcpyDeviceToHost, c->stream));
+  if (nd && c->D > 0) {
+    int32_t* tmp = nullptr;
+    HIP_TRY(dalloc(&tmp, (size_t)c->D * c->K));
+    hipError_t e = lda::launch_doc_topics(c->z, c->doc_off, c->D, c->K, c->Kp, tmp, 0, c->stream);
+    if (e == hipSuccess)
+      e = hipMemcpyAsync(nd, tmp, sizeof(int32_t) * (size_t)c->D * c->K, hipMemcpyDeviceToHost, c->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    (void)hipFree(tmp);
+    HIP_TRY(e);
+  }
+  if (ndsum)
+    for (int64_t d = 0; d < c->D; ++d) ndsum[d] = (int32_t)(c->doc_off_h[d + 1] - c->doc_off_h[d]);
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  return LDA_OK;
+}
+
+lda_status lda_set_alpha_beta(lda_ctx* c, const double* alpha, double beta) {
+  if (!c || !alpha) return fail(LDA_ERR_INVALID_ARG, "null argument");
+  if (!(beta > 0.0)) return fail(LDA_ERR_INVALID_ARG, "beta must be > 0");
+  for (int k = 0; k < c->K; ++k)
+    if (!(alpha[k] > 0.0)) return fail(LDA_ERR_INVALID_ARG, "alpha must be > 0");
+  HIP_TRY(hipSetDevice(c->device));
+  c->alpha.assign(alpha, alpha + c->K);
+  c->beta = beta;
+  HIP_TRY(hipMemcpyAsync(c->alpha_d, c->alpha.data(), sizeof(double) * c->K, hipMemcpyHostToDevice, c->stream));
+  // refresh the fp32 tables (the nwsum delta part is zero unless pending)
+  if (!c->pending) {
+    HIP_TRY(lda::launch_prepare_topics(c->nwsum, c->delta + (int64_t)c->V * c->Kp, c->alpha_d,
+                                       c->beta, (double)c->V * c->beta, c->K, c->Kp, c->alpha_f,
+                                       c->inv, c->inv_m1, c->stream));
+  }
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  return LDA_OK;
+}
+
+lda_status lda_log_likelihood_parts(lda_ctx* c, double* doc_part, double* word_part) {
+  if (!c) return fail(LDA_ERR_INVALID_ARG, "null ctx");
+  if (c->pending) return fail(LDA_ERR_STATE, "log likelihood with a pending delta: call lda_apply first");
+  HIP_TRY(hipSetDevice(c->device));
+  double alpha_sum = 0.0;
+  for (double a : c->alpha) alpha_sum += a;
+  const int nb = c->partial_blocks;
+  std::vector<double> part(nb);
+  std::vector<unsigned long long> nz(nb);
+  double docs = 0.0;
+  if (c->D > 0) {
+    HIP_TRY(lda::launch_ll_docs(c->z, c->doc_off, c->D, c->alpha_d, alpha_sum, c->K, c->Kp,
+                                c->partial, nb, c->stream));
+    HIP_TRY(hipMemcpyAsync(part.data(), c->partial, sizeof(double) * nb, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    for (int b = 0; b < nb; ++b) docs += part[b];
+  }
+  docs += (double)c->D * log_gamma_stirling(alpha_sum);
+  HIP_TRY(lda::launch_ll_words(c->nw, c->V, c->K, c->Kp, c->beta, c->partial, c->nonzero, nb, c->stream));
+  HIP_TRY(hipMemcpyAsync(part.data(), c->partial, sizeof(double) * nb, hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipMemcpyAsync(nz.data(), c->nonzero, sizeof(unsigned long long) * nb, hipMemcpyDeviceToHost, c->stream));
+  std::vector<int32_t> nws(c->K);
+  HIP_TRY(hipMemcpyAsync(nws.data(), c->nwsum, sizeof(int32_t) * c->K, hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  double words_ll = 0.0;
+  unsigned long long nonzero = 0;
+  for (int b = 0; b < nb; ++b) {
+    words_ll += part[b];
+    nonzero += nz[b];
+  }
+  for (int k = 0; k < c->K; ++k) words_ll -= log_gamma_stirling(c->beta * c->V + nws[k]);
+  words_ll += log_gamma_stirling(c->beta * c->V) * c->K;
+  words_ll -= log_gamma_stirling(c->beta) * (double)nonzero;
+  if (doc_part) *doc_part = docs;
+  if (word_part) *word_part = words_ll;
+  return LDA_OK;
+}
+
+lda_status lda_log_likelihood(lda_ctx* c, double* out) {
+  if (!out) return fail(LDA_ERR_INVALID_ARG, "null argument");
+  double a = 0.0, b = 0.0;
+  lda_status s = lda_log_likelihood_parts(c, &a, &b);
+  if (s) return s;
+  *out = a + b;
+  return LDA_OK;
+}
+
+lda_status lda_infer(lda_ctx* c, int64_t Dh, const int64_t* doc_off, const int32_t* words,
+                     int32_t n_iter, int32_t burn_in, int32_t thin, uint64_t seed, double* theta) {
+  if (!c || !doc_off || !theta) return fail(LDA_ERR_INVALID_ARG, "null argument");
+  if (Dh < 0 || n_iter < 0 || burn_in < 0 || thin < 1) return fail(LDA_ERR_INVALID_ARG, "bad sizes");
+  if (c->pending) return fail(LDA_ERR_STATE, "inference with a pending delta: call lda_apply first");
+  std::vector<int64_t> off(Dh + 1);
+  for (int64_t d = 0; d <= Dh; ++d) {
+    off[d] = doc_off[d] - doc_off[0];
+    if (d > 0 && off[d] < off[d - 1]) return fail(LDA_ERR_INVALID_ARG, "doc_off not monotone");
+  }
+  const int64_t N = off[Dh];
+  for (int64_t i = 0; i < N; ++i)
+    if (words[i] < 0 || words[i] >= c->V) return fail(LDA_ERR_INVALID_ARG, "word id out of range (OOV must be removed)");
+  HIP_TRY(hipSetDevice(c->device));
+  int32_t *dw = nullptr, *dz = nullptr, *acc = nullptr, *q = nullptr;
+  int64_t *doff = nullptr, *drange = nullptr;
+  std::vector<int64_t> ranges = make_ranges(off, std::max<int64_t>(256, std::min<int64_t>(c->tokens_per_range, N / std::max<int64_t>(1, (int64_t)c->sample_blocks_frozen * 32))));
+  const int64_t R = (int64_t)ranges.size() - 1;
+  hipError_t e = hipSuccess;
+  auto chk = [&](hipError_t x) {
+    if (e == hipSuccess) e = x;
+  };
+  chk(dalloc(&dw, N));
+  chk(dalloc(&dz, N));
+  chk(dalloc(&acc, (size_t)std::max<int64_t>(Dh, 1) * c->K));
+  chk(dalloc(&q, 4));
+  chk(dalloc(&doff, Dh + 1));
+  chk(dalloc(&drange, ranges.size()));
+  if (e == hipSuccess && N > 0) chk(hipMemcpyAsync(dw, words, sizeof(int32_t) * N, hipMemcpyHostToDevice, c->stream));
+  if (e == hipSuccess) chk(hipMemcpyAsync(doff, off.data(), sizeof(int64_t) * (Dh + 1), hipMemcpyHostToDevice, c->stream));
+  if (e == hipSuccess) chk(hipMemcpyAsync(drange, ranges.data(), sizeof(int64_t) * ranges.size(), hipMemcpyHostToDevice, c->stream));
+  if (e == hipSuccess) chk(hipMemsetAsync(acc, 0, sizeof(int32_t) * (size_t)std::max<int64_t>(Dh, 1) * c->K, c->stream));
+  if (e == hipSuccess) chk(lda::launch_infer_init(dw, dz, N, c->nw, c->K, c->Kp, c->stream));
+  int32_t nsamples = 0;
+  lda::SampleParams p = c->params(true);
+  p.words = dw;
+  p.z = dz;
+  p.doc_off = doff;
+  p.range_doc = drange;
+  p.num_ranges = R;
+  p.queue = q;
+  p.delta = nullptr;
+  p.dsum = nullptr;
+  p.token_base = 0;
+  p.k0 = (uint32_t)seed;
+  p.k1 = (uint32_t)(seed >> 32);
+  p.c3 = lda::STREAM_INFER;
+  const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>(c->sample_blocks_frozen, (R + 3) / 4));
+  for (int32_t it = 1; it <= n_iter && e == hipSuccess && N > 0; ++it) {
+    p.c2 = (uint32_t)(it - 1);
+    chk(hipMemsetAsync(q, 0, sizeof(int32_t), c->stream));
+    if (e == hipSuccess) chk(lda::launch_sample(c->C, true, p, blocks, c->stream));
+    if (it > burn_in && (it - burn_in) % thin == 0) {
+      ++nsamples;
+      if (e == hipSuccess) chk(lda::launch_doc_topics(dz, doff, Dh, c->K, c->Kp, acc, 1, c->stream));
+    }
+  }
+  if (nsamples == 0) {
+    nsamples = 1;
+    if (e == hipSuccess) chk(lda::launch_doc_topics(dz, doff, Dh, c->K, c->Kp, acc, 1, c->stream));
+  }
+  std::vector<int32_t> acc_h((size_t)Dh * c->K);
+  if (e == hipSuccess && Dh > 0)
+    chk(hipMemcpyAsync(acc_h.data(), acc, sizeof(int32_t) * (size_t)Dh * c->K, hipMemcpyDeviceToHost, c->stream));
+  if (e == hipSuccess) chk(hipStreamSynchronize(c->stream));
+  for (void* ptr : {(void*)dw, (void*)dz, (void*)acc, (void*)q, (void*)doff, (void*)drange})
+    if (ptr) (void)hipFree(ptr);
+  HIP_TRY(e);
+  for (int64_t d = 0; d < Dh; ++d) {
+    double sum = 0.0;
+    for (int k = 0; k < c->K; ++k) {
+      const double v = (double)nsamples * c->alpha[k] + (double)acc_h[(size_t)d * c->K + k];
+      theta[(size_t)d * c->K + k] = v;
+      sum += v;
+    }
+    for (int k = 0; k < c->K; ++k) theta[(size_t)d * c->K + k] /= sum;
+  }
+  return LDA_OK;
+}
+
+lda_status lda_to_mallet_packed(lda_ctx* c, int32_t* rows, int64_t* row_off, int32_t* topic_bits) {
+  if (!c || !row_off) return fail(LDA_ERR_INVALID_ARG, "null argument");
+  if (c->pending) return fail(LDA_ERR_STATE, "pending delta: call lda_apply first");
+  // ParallelTopicModel(numberOfTopics, ...): topicMask / topicBits [M]
+  int32_t mask;
+  if ((c->K & (c->K - 1)) == 0) {
+    mask = c->K - 1;
+  } else {
+    int hb = 1;
+    while (hb * 2 <= c->K) hb *= 2;
+    mask = hb * 2 - 1;
+  }
+  const int32_t bits = __builtin_popcount((unsigned)mask);
+  if (topic_bits) *topic_bits = bits;
+  std::vector<int32_t> nw((size_t)c->V * c->K);
+  lda_status s = lda_get_counts(c, nw.data(), nullptr, nullptr, nullptr);
+  if (s) return s;
+  // row length = min(K, typeTotal) exactly as addInstances allocates it
+  row_off[0] = 0;
+  for (int w = 0; w < c->V; ++w) {
+    int64_t total = 0;
+    for (int k = 0; k < c->K; ++k) total += nw[(size_t)w * c->K + k];
+    row_off[w + 1] = row_off[w] + std::min<int64_t>(c->K, total);
+  }
+  if (!rows) return LDA_OK;
+  std::vector<int32_t> cell;
+  for (int w = 0; w < c->V; ++w) {
+    cell.clear();
+    for (int k = 0; k < c->K; ++k) {
+      const int32_t n = nw[(size_t)w * c->K + k];
+      if (n > 0) {
+        if ((int64_t)n >= (1LL << (31 - bits)))
+          return fail(LDA_ERR_UNSUPPORTED, "count does not fit Mallet's packed cell");
+        cell.push_back((n << bits) + k);
+      }
+    }
+    std::sort(cell.begin(), cell.end(), [](int32_t a, int32_t b) { return a > b; });
+    int64_t o = row_off[w];
+    const int64_t len = row_off[w + 1] - row_off[w];
+    for (int64_t i = 0; i < len; ++i) rows[o + i] = i < (int64_t)cell.size() ? cell[i] : 0;
+  }
+  return LDA_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,63 @@
+// lda_kernels.h — internal interface between the C-ABI runtime
+// (lda_capi.cpp) and the gfx950 kernels (lda_kernels.hip).  Not installed.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+namespace lda {
+
+// Philox counter word 3: which stream a draw belongs to.
+constexpr uint32_t STREAM_SAMPLE = 0u;
+constexpr uint32_t STREAM_INIT = 1u;
+constexpr uint32_t STREAM_INFER = 2u;
+
+// Row-prefetch depth of the sampler per C = Kp/64 (tokens in flight per wave).
+#define SAMPLE_P1 4
+#define SAMPLE_P2 4
+#define SAMPLE_P4 4
+#define SAMPLE_P8 4
+#define SAMPLE_P16 2
+
+struct SampleParams {
+  const int32_t* words;     // [N] token stream (doc-contiguous)
+  int32_t* z;               // [N] topic of each token (read old, write new)
+  const int64_t* doc_off;   // [D+1]
+  const int64_t* range_doc; // [R+1] work ranges as doc boundaries
+  int64_t num_ranges;
+  int32_t* queue;           // range counter, zeroed before each launch
+  const int32_t* nw;        // [V*Kp] snapshot
+  int32_t* delta;           // [V*Kp] pending nw delta
+  int32_t* dsum;            // [Kp]   pending nwsum delta
+  const float* alpha;       // [Kp]
+  const float* inv;         // [Kp]   1/(nwsum + V*beta)
+  const float* inv_m1;      // [Kp]   1/(nwsum - 1 + V*beta)
+  float beta;
+  int32_t K;
+  int64_t token_base;       // Philox counter offset (global token index)
+  uint32_t k0, k1;          // Philox key (seed)
+  uint32_t c2, c3;          // Philox counter words 2 (sweep) and 3 (stream)
+};
+
+hipError_t launch_sample(int C, bool frozen, const SampleParams& p, int blocks, hipStream_t st);
+int sample_blocks_per_cu(int C, bool frozen);
+hipError_t launch_init_z(int32_t* z, int64_t n, int32_t K, int64_t token_base, uint32_t k0,
+                         uint32_t k1, hipStream_t st);
+hipError_t launch_count(const int32_t* words, const int32_t* z, int64_t n, int32_t Kp,
+                        int32_t* delta, int32_t* dsum, hipStream_t st);
+hipError_t launch_apply(int32_t* nw, int32_t* delta, int64_t n, hipStream_t st);
+hipError_t launch_prepare_topics(int32_t* nwsum, int32_t* dsum, const double* alpha, double beta,
+                                 double vbeta, int32_t K, int32_t Kp, float* alpha_f, float* inv,
+                                 float* inv_m1, hipStream_t st);
+hipError_t launch_doc_topics(const int32_t* z, const int64_t* doc_off, int64_t D, int32_t K,
+                             int32_t Kp, int32_t* out, int accumulate, hipStream_t st);
+hipError_t launch_ll_docs(const int32_t* z, const int64_t* doc_off, int64_t D, const double* alpha,
+                          double alpha_sum, int32_t K, int32_t Kp, double* partial, int blocks,
+                          hipStream_t st);
+hipError_t launch_ll_words(const int32_t* nw, int64_t V, int32_t K, int32_t Kp, double beta,
+                           double* partial, unsigned long long* nonzero, int blocks,
+                           hipStream_t st);
+hipError_t launch_infer_init(const int32_t* words, int32_t* z, int64_t n, const int32_t* nw,
+                             int32_t K, int32_t Kp, hipStream_t st);
+
+}  // namespace lda

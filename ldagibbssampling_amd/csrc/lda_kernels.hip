@@ -1,0 +1,619 @@
+// lda_kernels.hip — gfx950 (MI355X / CDNA4) kernels of the collapsed-Gibbs
+// LDA sampler.  Replaces the per-token loop of Mallet 2.0.7's
+// WorkerRunnable.sampleTopicsForOneDoc, reached from ParallelTopicModel.
+// estimate() at src/cmu_ron/TrainAndPredict.java:166 and
+// src/cmu/TrainAndPredict.java:265 of the reference.
+//
+// Sampling semantics: AD-LDA with a per-sweep
+// snapshot.  nw/nwsum are read-only during a pass (the token's own old
+// assignment is subtracted on the fly), nd is live inside a document, and all
+// count changes go to an int32 delta buffer that lda_apply folds in after the
+// pass (after an RCCL all-reduce when the corpus is sharded over GPUs).
+// Integer adds commute, so z/nw/nwsum are independent of scheduling, of the
+// number of GPUs, and bit-identical to the CPU oracle (oracle/lda_oracle.c).
+//
+// Exact fp32 evaluation order of one draw (mirrored by oracle exact_draw):
+//   lane l owns topics [l*C, l*C+C), C = Kp/64.
+//   b_k  = (float(nw_wk - [k==zo]) + beta) * (k==zo ? inv_m1_k : inv_k)
+//   a_k  = float(nd_k) + alpha_k
+//   S_j  = fma(a_j, b_j, S_{j-1}), S_{-1} = 0   (serial inside the lane)
+//   T    = wave_incl_scan(S_{C-1})              (DPP order, see below)
+//   thr  = u * T_63,  u = (x0 >> 8) * 2^-24, x0 = Philox4x32-10 word 0
+//   l*   = first lane <= last_lane with T_l > thr, else last_lane
+//   j*   = #{j : T_{l*-1} + S_j <= thr} (S is monotone) or, if that is C,
+//          the last valid topic of lane l*
+//   z    = l*·C + j*
+//
+// Compiled with -ffp-contract=off: the only fused multiply-adds are the
+// explicit __builtin_fmaf below.
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "lda_kernels.h"
+
+namespace lda {
+
+// ---------------------------------------------------------------- Philox
+#define PHILOX_M0 0xD2511F53u
+#define PHILOX_M1 0xCD9E8D57u
+#define PHILOX_W0 0x9E3779B9u
+#define PHILOX_W1 0xBB67AE85u
+
+__device__ __forceinline__ uint32_t philox_x0(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3,
+                                              uint32_t k0, uint32_t k1) {
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    if (r > 0) {
+      k0 += PHILOX_W0;
+      k1 += PHILOX_W1;
+    }
+    const uint32_t hi0 = __umulhi(PHILOX_M0, c0), lo0 = PHILOX_M0 * c0;
+    const uint32_t hi1 = __umulhi(PHILOX_M1, c2), lo1 = PHILOX_M1 * c2;
+    const uint32_t n0 = hi1 ^ c1 ^ k0;
+    const uint32_t n2 = hi0 ^ c3 ^ k1;
+    c0 = n0;
+    c1 = lo1;
+    c2 = n2;
+    c3 = lo0;
+  }
+  return c0;
+}
+
+__device__ __forceinline__ uint32_t draw_u32(uint64_t gtok, uint32_t c2, uint32_t c3, uint32_t k0,
+                                             uint32_t k1) {
+  return philox_x0((uint32_t)gtok, (uint32_t)(gtok >> 32), c2, c3, k0, k1);
+}
+
+__device__ __forceinline__ float u01(uint32_t x) { return (float)(x >> 8) * 0x1p-24f; }
+
+// ------------------------------------------------------------ wave helpers
+template <int CTRL, int ROW_MASK, bool BOUND>
+__device__ __forceinline__ float dpp_mov(float v) {
+  return __builtin_bit_cast(
+      float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, ROW_MASK, 0xf, BOUND));
+}
+
+// Inclusive wavefront scan: row_shr:1,2,4,8 inside 16-lane rows (sources
+// outside the row read 0), row_bcast:15 into rows 1 and 3, row_bcast:31 into
+// rows 2 and 3.  Restated lane by lane in oracle/lda_oracle.c:wave_scan_emulate.
+__device__ __forceinline__ float wave_incl_scan(float x) {
+  x = dpp_mov<0x111, 0xf, true>(x) + x;
+  x = dpp_mov<0x112, 0xf, true>(x) + x;
+  x = dpp_mov<0x114, 0xf, true>(x) + x;
+  x = dpp_mov<0x118, 0xf, true>(x) + x;
+  x = x + dpp_mov<0x142, 0xa, false>(x);
+  x = x + dpp_mov<0x143, 0xc, false>(x);
+  return x;
+}
+
+__device__ __forceinline__ int readlane_i(int v, int l) { return __builtin_amdgcn_readlane(v, l); }
+__device__ __forceinline__ float readlane_f(float v, int l) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), l));
+}
+__device__ __forceinline__ int uniform_i(int v) { return __builtin_amdgcn_readfirstlane(v); }
+
+template <int C>
+__device__ __forceinline__ void load_row(int32_t (&r)[C], const int32_t* __restrict__ p) {
+  if constexpr (C >= 4) {
+#pragma unroll
+    for (int q = 0; q < C / 4; ++q) {
+      const int4 v = reinterpret_cast<const int4*>(p)[q];
+      r[4 * q + 0] = v.x;
+      r[4 * q + 1] = v.y;
+      r[4 * q + 2] = v.z;
+      r[4 * q + 3] = v.w;
+    }
+  } else if constexpr (C == 2) {
+    const int2 v = *reinterpret_cast<const int2*>(p);
+    r[0] = v.x;
+    r[1] = v.y;
+  } else {
+    r[0] = p[0];
+  }
+}
+
+// ------------------------------------------------------------- the sampler
+// One wavefront walks one work range (a run of whole documents) at a time,
+// pulling ranges from a device queue.  The wave keeps a 64-token chunk of the
+// token stream in registers (lane i <-> token i of the chunk: word, old z,
+// Philox uniform, new z), the next chunk's words/z one chunk ahead, and the
+// nw rows of the next P tokens in flight (the snapshot makes row loads
+// independent of the draws, so they pipeline across tokens and documents).
+template <int C, int P, bool FROZEN>
+__global__ __launch_bounds__(256) void k_sample(SampleParams p) {
+  extern __shared__ __attribute__((aligned(16))) int32_t smem[];
+  constexpr int KP = C * 64;
+  const int lane = threadIdx.x & 63;
+  const int wid = threadIdx.x >> 6;
+  int32_t* hist = smem + wid * KP;  // per-wave doc-topic histogram scratch
+  int32_t* bsum = smem + 4 * KP;    // per-block nwsum delta
+
+  for (int i = threadIdx.x; i < 5 * KP; i += 256) smem[i] = 0;
+  __syncthreads();
+
+  float alpha_r[C], inv_r[C], invm1_r[C];
+#pragma unroll
+  for (int j = 0; j < C; ++j) {
+    alpha_r[j] = p.alpha[lane * C + j];
+    inv_r[j] = p.inv[lane * C + j];
+    invm1_r[j] = FROZEN ? 0.0f : p.inv_m1[lane * C + j];
+  }
+  const float beta = p.beta;
+  const int last_lane = (p.K - 1) / C;
+  const int last_j = (lane < last_lane) ? C - 1 : (p.K - 1) % C;
+  const int32_t* __restrict__ nw = p.nw;
+
+  while (true) {
+    int r = 0;
+    if (lane == 0) r = atomicAdd(p.queue, 1);
+    r = uniform_i(__shfl(r, 0));
+    if (r >= p.num_ranges) break;
+    const int64_t d0 = p.range_doc[r], d1 = p.range_doc[r + 1];
+    const int64_t t0 = p.doc_off[d0], t1 = p.doc_off[d1];
+    if (t1 <= t0) continue;
+
+    // --- chunk registers
+    int64_t cbase = t0;
+    int cw = 0, cz = 0, czn = 0, cwn = 0;
+    if (t0 + lane < t1) {
+      cw = p.words[t0 + lane];
+      cz = p.z[t0 + lane];
+    }
+    if (t0 + 64 + lane < t1) {
+      cwn = p.words[t0 + 64 + lane];
+      czn = p.z[t0 + 64 + lane];
+    }
+    int cn = cz;
+    float cu = u01(draw_u32((uint64_t)(p.token_base + t0 + lane), p.c2, p.c3, p.k0, p.k1));
+
+    // --- first document of the range
+    int64_t doc = d0;
+    while (p.doc_off[doc + 1] <= t0) ++doc;
+    int64_t doc_end = p.doc_off[doc + 1];
+    float ndv[C];
+    {
+      for (int64_t i = t0 + lane; i < doc_end; i += 64) atomicAdd(&hist[p.z[i]], 1);
+#pragma unroll
+      for (int j = 0; j < C; ++j) {
+        ndv[j] = (float)hist[lane * C + j];
+        hist[lane * C + j] = 0;
+      }
+    }
+
+    // --- prime the row pipeline
+    int32_t rows[P][C];
+#pragma unroll
+    for (int s = 0; s < P; ++s) {
+      const int64_t tp = t0 + s;
+      const int wp = readlane_i(cw, s);
+      const int64_t wrow = (tp < t1) ? (int64_t)wp : 0;
+      load_row<C>(rows[s], nw + wrow * KP + lane * C);
+    }
+
+    for (int64_t tb = t0; tb < t1; tb += P) {
+#pragma unroll
+      for (int s = 0; s < P; ++s) {
+        const int64_t t = tb + s;
+        if (t >= t1) break;
+        int idx = (int)(t - cbase);
+        if (idx == 64) {
+          // chunk switch: publish the finished chunk's new z, shift
+          p.z[cbase + lane] = cn;
+          cbase += 64;
+          idx = 0;
+          cw = cwn;
+          cz = czn;
+          cn = cz;
+          cu = u01(draw_u32((uint64_t)(p.token_base + cbase + lane), p.c2, p.c3, p.k0, p.k1));
+          if (cbase + 64 + lane < t1) {
+            cwn = p.words[cbase + 64 + lane];
+            czn = p.z[cbase + 64 + lane];
+          }
+        }
+        if (t == doc_end) {
+          ++doc;
+          while (p.doc_off[doc + 1] <= t) ++doc;
+          doc_end = p.doc_off[doc + 1];
+          for (int64_t i = t + lane; i < doc_end; i += 64) atomicAdd(&hist[p.z[i]], 1);
+#pragma unroll
+          for (int j = 0; j < C; ++j) {
+            ndv[j] = (float)hist[lane * C + j];
+            hist[lane * C + j] = 0;
+          }
+        }
+
+        const int w = readlane_i(cw, idx);
+        const int zo = readlane_i(cz, idx);
+        const float u = readlane_f(cu, idx);
+        const int lo = zo / C, jo = zo % C;
+        const bool own_old = (lane == lo);
+
+        // remove the token from its document
+#pragma unroll
+        for (int j = 0; j < C; ++j)
+          if (j == jo) ndv[j] = own_old ? ndv[j] - 1.0f : ndv[j];
+
+        // weights and the lane-serial prefix
+        float S[C];
+        float acc = 0.0f;
+#pragma unroll
+        for (int j = 0; j < C; ++j) {
+          int32_t c = rows[s][j];
+          float iv = inv_r[j];
+          if (!FROZEN) {
+            const bool me = own_old && (j == jo);
+            c = me ? c - 1 : c;
+            iv = me ? invm1_r[j] : iv;
+          }
+          const float b = ((float)c + beta) * iv;
+          const float a = ndv[j] + alpha_r[j];
+          acc = __builtin_fmaf(a, b, acc);
+          S[j] = acc;
+        }
+
+        // wavefront scan and the draw
+        const float T = wave_incl_scan(acc);
+        const float total = readlane_f(T, 63);
+        const float thr = u * total;
+        const uint64_t m = __ballot((T > thr) && (lane <= last_lane));
+        const int lstar = m ? (int)__builtin_ctzll(m) : last_lane;
+        const float E = lstar > 0 ? readlane_f(T, lstar - 1) : 0.0f;
+        int cnt = 0;
+#pragma unroll
+        for (int j = 0; j < C; ++j) cnt += (E + S[j] <= thr) ? 1 : 0;
+        const int jsel = cnt < C ? cnt : last_j;
+        const int jn = readlane_i(jsel, lstar);
+        const int kn = lstar * C + jn;
+
+        // add the token back under its new topic
+        const bool own_new = (lane == lstar);
+#pragma unroll
+        for (int j = 0; j < C; ++j)
+          if (j == jn) ndv[j] = own_new ? ndv[j] + 1.0f : ndv[j];
+        cn = (lane == idx) ? kn : cn;
+        if (!FROZEN && kn != zo) {
+          if (lane < 2) {
+            const int k = lane == 0 ? zo : kn;
+            const int v = lane == 0 ? -1 : 1;
+            atomicAdd(&p.delta[(int64_t)w * KP + k], v);
+            atomicAdd(&bsum[k], v);
+          }
+        }
+
+        // keep the pipeline full: row of token t+P
+        const int64_t tp = t + P;
+        if (tp < t1) {
+          const int pidx = (int)(tp - cbase);
+          const int wp = pidx < 64 ? readlane_i(cw, pidx) : readlane_i(cwn, pidx - 64);
+          load_row<C>(rows[s], nw + (int64_t)wp * KP + lane * C);
+        }
+      }
+    }
+    if (cbase + lane < t1) p.z[cbase + lane] = cn;
+  }
+
+  if (!FROZEN) {
+    __syncthreads();
+    for (int i = threadIdx.x; i < KP; i += 256) {
+      const int v = bsum[i];
+      if (v != 0) atomicAdd(&p.dsum[i], v);
+    }
+  }
+}
+
+// ----------------------------------------------------------- count kernels
+__global__ __launch_bounds__(256) void k_init_z(int32_t* __restrict__ z, int64_t n, int32_t K,
+                                                int64_t token_base, uint32_t k0, uint32_t k1) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    const uint32_t x = draw_u32((uint64_t)(token_base + i), 0u, STREAM_INIT, k0, k1);
+    z[i] = (int32_t)(((uint64_t)x * (uint64_t)K) >> 32);
+  }
+}
+
+// Local histogram of (word, topic) and topic totals into the delta buffer.
+__global__ __launch_bounds__(256) void k_count(const int32_t* __restrict__ words,
+                                               const int32_t* __restrict__ z, int64_t n,
+                                               int32_t Kp, int32_t* __restrict__ delta,
+                                               int32_t* __restrict__ dsum) {
+  extern __shared__ __attribute__((aligned(16))) int32_t hsum[];
+  for (int i = threadIdx.x; i < Kp; i += 256) hsum[i] = 0;
+  __syncthreads();
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    const int k = z[i];
+    atomicAdd(&delta[(int64_t)words[i] * Kp + k], 1);
+    atomicAdd(&hsum[k], 1);
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < Kp; i += 256)
+    if (hsum[i]) atomicAdd(&dsum[i], hsum[i]);
+}
+
+// nw += delta; delta = 0 over the V*Kp region (Kp is a multiple of 64, so
+// the region is a multiple of 4 int32 and int4-aligned).
+__global__ __launch_bounds__(256) void k_apply(int4* __restrict__ nw, int4* __restrict__ delta,
+                                               int64_t n4) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += (int64_t)gridDim.x * 256) {
+    int4 a = nw[i];
+    const int4 d = delta[i];
+    if (d.x | d.y | d.z | d.w) {
+      a.x += d.x;
+      a.y += d.y;
+      a.z += d.z;
+      a.w += d.w;
+      nw[i] = a;
+      delta[i] = make_int4(0, 0, 0, 0);
+    }
+  }
+}
+
+// nwsum += dsum; dsum = 0; per-topic fp32 tables (one block, Kp <= 1024).
+__global__ void k_prepare_topics(int32_t* __restrict__ nwsum, int32_t* __restrict__ dsum,
+                                 const double* __restrict__ alpha, double beta, double vbeta,
+                                 int32_t K, int32_t Kp, float* __restrict__ alpha_f,
+                                 float* __restrict__ inv, float* __restrict__ inv_m1) {
+  const int k = threadIdx.x;
+  if (k >= Kp) return;
+  const int32_t s = nwsum[k] + dsum[k];
+  nwsum[k] = s;
+  dsum[k] = 0;
+  const float vb = (float)vbeta;
+  if (k < K) {
+    alpha_f[k] = (float)alpha[k];
+    inv[k] = 1.0f / ((float)s + vb);
+    inv_m1[k] = 1.0f / ((float)(s - 1) + vb);
+  } else {
+    alpha_f[k] = 0.0f;
+    inv[k] = 0.0f;
+    inv_m1[k] = 0.0f;
+  }
+  (void)beta;
+}
+
+// Dense nd rows: one wavefront per document.
+__global__ __launch_bounds__(256) void k_doc_topics(const int32_t* __restrict__ z,
+                                                    const int64_t* __restrict__ doc_off, int64_t D,
+                                                    int32_t K, int32_t Kp, int32_t* __restrict__ out,
+                                                    int accumulate) {
+  extern __shared__ __attribute__((aligned(16))) int32_t h[];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  int32_t* hist = h + wid * Kp;
+  for (int i = lane; i < Kp; i += 64) hist[i] = 0;
+  for (int64_t d = (int64_t)blockIdx.x * 4 + wid; d < D; d += (int64_t)gridDim.x * 4) {
+    for (int64_t i = doc_off[d] + lane; i < doc_off[d + 1]; i += 64) atomicAdd(&hist[z[i]], 1);
+    for (int k = lane; k < K; k += 64) {
+      const int32_t c = hist[k];
+      if (accumulate)
+        out[d * K + k] += c;
+      else
+        out[d * K + k] = c;
+    }
+    for (int k = lane; k < Kp; k += 64) hist[k] = 0;
+  }
+}
+
+// Mallet's Dirichlet.logGammaStirling in fp64.
+__device__ double log_gamma_stirling(double z) {
+  const double HALF_LOG_TWO_PI = 0.91893853320467274178;
+  int shift = 0;
+  while (z < 2) {
+    z += 1.0;
+    ++shift;
+  }
+  double result = HALF_LOG_TWO_PI + (z - 0.5) * log(z) - z + 1 / (12 * z) -
+                  1 / (360 * z * z * z) + 1 / (1260 * z * z * z * z * z);
+  while (shift > 0) {
+    --shift;
+    z -= 1.0;
+    result -= log(z);
+  }
+  return result;
+}
+
+__device__ __forceinline__ double wave_sum_d(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+
+// Document part of modelLogLikelihood: one wave per doc, per-block partials.
+__global__ __launch_bounds__(256) void k_ll_docs(const int32_t* __restrict__ z,
+                                                 const int64_t* __restrict__ doc_off, int64_t D,
+                                                 const double* __restrict__ alpha, double alpha_sum,
+                                                 int32_t K, int32_t Kp, double* __restrict__ partial) {
+  extern __shared__ __attribute__((aligned(16))) int32_t h[];
+  __shared__ double wsum[4];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  int32_t* hist = h + wid * Kp;
+  for (int i = lane; i < Kp; i += 64) hist[i] = 0;
+  double acc = 0.0;
+  for (int64_t d = (int64_t)blockIdx.x * 4 + wid; d < D; d += (int64_t)gridDim.x * 4) {
+    for (int64_t i = doc_off[d] + lane; i < doc_off[d + 1]; i += 64) atomicAdd(&hist[z[i]], 1);
+    for (int k = lane; k < K; k += 64) {
+      const int32_t c = hist[k];
+      if (c > 0) acc += log_gamma_stirling(alpha[k] + c) - log_gamma_stirling(alpha[k]);
+      hist[k] = 0;
+    }
+    if (lane == 0) acc -= log_gamma_stirling(alpha_sum + (double)(doc_off[d + 1] - doc_off[d]));
+  }
+  acc = wave_sum_d(acc);
+  if (lane == 0) wsum[wid] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) partial[blockIdx.x] = ((wsum[0] + wsum[1]) + wsum[2]) + wsum[3];
+}
+
+// Word part: sum over nonzero nw cells of logGammaStirling(beta + count).
+__global__ __launch_bounds__(256) void k_ll_words(const int32_t* __restrict__ nw, int64_t V,
+                                                  int32_t K, int32_t Kp, double beta,
+                                                  double* __restrict__ partial,
+                                                  unsigned long long* __restrict__ nonzero) {
+  __shared__ double wsum[4];
+  __shared__ unsigned long long wnz[4];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  double acc = 0.0;
+  unsigned long long nz = 0;
+  const int64_t n = V * Kp;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    const int k = (int)(i % Kp);
+    const int32_t c = nw[i];
+    if (k < K && c > 0) {
+      acc += log_gamma_stirling(beta + c);
+      ++nz;
+    }
+  }
+  acc = wave_sum_d(acc);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) nz += __shfl_xor(nz, o);
+  if (lane == 0) {
+    wsum[wid] = acc;
+    wnz[wid] = nz;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    partial[blockIdx.x] = ((wsum[0] + wsum[1]) + wsum[2]) + wsum[3];
+    nonzero[blockIdx.x] = wnz[0] + wnz[1] + wnz[2] + wnz[3];
+  }
+}
+
+// TopicInferencer init: most frequent topic of the word (ties -> larger id).
+__global__ __launch_bounds__(256) void k_infer_init(const int32_t* __restrict__ words,
+                                                    int32_t* __restrict__ z, int64_t n,
+                                                    const int32_t* __restrict__ nw, int32_t K,
+                                                    int32_t Kp) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  for (int64_t i = (int64_t)blockIdx.x * 4 + wid; i < n; i += (int64_t)gridDim.x * 4) {
+    const int32_t* row = nw + (int64_t)words[i] * Kp;
+    int best_c = -1, best_k = 0;
+    for (int k = lane; k < K; k += 64) {
+      const int c = row[k];
+      if (c >= best_c) {
+        best_c = c;
+        best_k = k;
+      }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const int oc = __shfl_xor(best_c, o), ok = __shfl_xor(best_k, o);
+      if (oc > best_c || (oc == best_c && ok > best_k)) {
+        best_c = oc;
+        best_k = ok;
+      }
+    }
+    if (lane == 0) z[i] = best_k;
+  }
+}
+
+// ------------------------------------------------------------- launchers
+template <int C, int P, bool FROZEN>
+static hipError_t launch_sample_t(const SampleParams& p, int blocks, hipStream_t st) {
+  const size_t lds = 5 * 64 * C * sizeof(int32_t);
+  hipLaunchKernelGGL((k_sample<C, P, FROZEN>), dim3(blocks), dim3(256), lds, st, p);
+  return hipGetLastError();
+}
+
+template <int C, int P, bool FROZEN>
+static int occupancy_t() {
+  int nb = 0;
+  const size_t lds = 5 * 64 * C * sizeof(int32_t);
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_sample<C, P, FROZEN>, 256, lds) !=
+      hipSuccess)
+    return 1;
+  return nb > 0 ? nb : 1;
+}
+
+#define LDA_DISPATCH_C(C_, FN, ...)                               \
+  switch (C_) {                                                   \
+    case 1: return FN<1, SAMPLE_P1, FROZEN>(__VA_ARGS__);         \
+    case 2: return FN<2, SAMPLE_P2, FROZEN>(__VA_ARGS__);         \
+    case 4: return FN<4, SAMPLE_P4, FROZEN>(__VA_ARGS__);         \
+    case 8: return FN<8, SAMPLE_P8, FROZEN>(__VA_ARGS__);         \
+    case 16: return FN<16, SAMPLE_P16, FROZEN>(__VA_ARGS__);      \
+    default: break;                                               \
+  }
+
+template <bool FROZEN>
+static hipError_t launch_sample_c(int C, const SampleParams& p, int blocks, hipStream_t st) {
+  LDA_DISPATCH_C(C, launch_sample_t, p, blocks, st)
+  return hipErrorInvalidValue;
+}
+template <bool FROZEN>
+static int occupancy_c(int C) {
+  LDA_DISPATCH_C(C, occupancy_t)
+  return 1;
+}
+
+hipError_t launch_sample(int C, bool frozen, const SampleParams& p, int blocks, hipStream_t st) {
+  return frozen ? launch_sample_c<true>(C, p, blocks, st) : launch_sample_c<false>(C, p, blocks, st);
+}
+int sample_blocks_per_cu(int C, bool frozen) {
+  return frozen ? occupancy_c<true>(C) : occupancy_c<false>(C);
+}
+
+hipError_t launch_init_z(int32_t* z, int64_t n, int32_t K, int64_t token_base, uint32_t k0,
+                         uint32_t k1, hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  const int blocks = (int)std::min<int64_t>((n + 255) / 256, 8192);
+  hipLaunchKernelGGL(k_init_z, dim3(blocks), dim3(256), 0, st, z, n, K, token_base, k0, k1);
+  return hipGetLastError();
+}
+
+hipError_t launch_count(const int32_t* words, const int32_t* z, int64_t n, int32_t Kp,
+                        int32_t* delta, int32_t* dsum, hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  const int blocks = (int)std::min<int64_t>((n + 255) / 256, 4096);
+  hipLaunchKernelGGL(k_count, dim3(blocks), dim3(256), Kp * sizeof(int32_t), st, words, z, n, Kp,
+                     delta, dsum);
+  return hipGetLastError();
+}
+
+hipError_t launch_apply(int32_t* nw, int32_t* delta, int64_t n, hipStream_t st) {
+  const int64_t n4 = n / 4;
+  if (n4 <= 0) return hipSuccess;
+  const int blocks = (int)std::min<int64_t>((n4 + 255) / 256, 8192);
+  hipLaunchKernelGGL(k_apply, dim3(blocks), dim3(256), 0, st, reinterpret_cast<int4*>(nw),
+                     reinterpret_cast<int4*>(delta), n4);
+  return hipGetLastError();
+}
+
+hipError_t launch_prepare_topics(int32_t* nwsum, int32_t* dsum, const double* alpha, double beta,
+                                 double vbeta, int32_t K, int32_t Kp, float* alpha_f, float* inv,
+                                 float* inv_m1, hipStream_t st) {
+  hipLaunchKernelGGL(k_prepare_topics, dim3(1), dim3(Kp), 0, st, nwsum, dsum, alpha, beta, vbeta, K,
+                     Kp, alpha_f, inv, inv_m1);
+  return hipGetLastError();
+}
+
+hipError_t launch_doc_topics(const int32_t* z, const int64_t* doc_off, int64_t D, int32_t K,
+                             int32_t Kp, int32_t* out, int accumulate, hipStream_t st) {
+  if (D <= 0) return hipSuccess;
+  const int blocks = (int)std::min<int64_t>((D + 3) / 4, 4096);
+  hipLaunchKernelGGL(k_doc_topics, dim3(blocks), dim3(256), 4 * Kp * sizeof(int32_t), st, z,
+                     doc_off, D, K, Kp, out, accumulate);
+  return hipGetLastError();
+}
+
+hipError_t launch_ll_docs(const int32_t* z, const int64_t* doc_off, int64_t D, const double* alpha,
+                          double alpha_sum, int32_t K, int32_t Kp, double* partial, int blocks,
+                          hipStream_t st) {
+  hipLaunchKernelGGL(k_ll_docs, dim3(blocks), dim3(256), 4 * Kp * sizeof(int32_t), st, z, doc_off, D,
+                     alpha, alpha_sum, K, Kp, partial);
+  return hipGetLastError();
+}
+
+hipError_t launch_ll_words(const int32_t* nw, int64_t V, int32_t K, int32_t Kp, double beta,
+                           double* partial, unsigned long long* nonzero, int blocks,
+                           hipStream_t st) {
+  hipLaunchKernelGGL(k_ll_words, dim3(blocks), dim3(256), 0, st, nw, V, K, Kp, beta, partial,
+                     nonzero);
+  return hipGetLastError();
+}
+
+hipError_t launch_infer_init(const int32_t* words, int32_t* z, int64_t n, const int32_t* nw,
+                             int32_t K, int32_t Kp, hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  const int blocks = (int)std::min<int64_t>((n + 3) / 4, 8192);
+  hipLaunchKernelGGL(k_infer_init, dim3(blocks), dim3(256), 0, st, words, z, n, nw, K, Kp);
+  return hipGetLastError();
+}
+
+}  // namespace lda

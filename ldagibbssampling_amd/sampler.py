@@ -1,0 +1,193 @@
+"""GibbsSampler: one document shard on one MI355X, driven through the C ABI.
+
+This is the thin host object over ``lda_ctx`` (include/lda_mi355x.h).  It is
+what ParallelTopicModel.estimate() (topic_model.py) and the AD-LDA driver
+(distributed.py) run; it has no CPU path — every call goes to
+liblda_mi355x.so and raises LdaError on failure.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from . import capi
+
+
+class _DeviceArray:
+    """Exposes a device pointer through __cuda_array_interface__ (zero-copy
+    torch.as_tensor view of the delta buffer for torch.distributed)."""
+
+    def __init__(self, ptr: int, count: int, typestr: str = "<i4"):
+        self.__cuda_array_interface__ = {
+            "shape": (count,),
+            "typestr": typestr,
+            "data": (ptr, False),
+            "version": 3,
+            "strides": None,
+        }
+
+
+class GibbsSampler:
+    def __init__(self, num_topics: int, num_types: int, doc_off, words, alpha, beta: float,
+                 seed: int = 0, z_init=None, device: int = 0, token_base: int = 0,
+                 tokens_per_range: int = 0):
+        L = capi.load()
+        self.K = int(num_topics)
+        self.V = int(num_types)
+        doc_off = np.ascontiguousarray(doc_off, dtype=np.int64)
+        words = np.ascontiguousarray(words, dtype=np.int32)
+        self.D = len(doc_off) - 1
+        self.N = int(doc_off[-1] - doc_off[0])
+        alpha = np.ascontiguousarray(np.broadcast_to(np.asarray(alpha, dtype=np.float64), (self.K,)))
+        self._alpha = alpha
+        cfg = capi.lda_config()
+        cfg.num_topics = self.K
+        cfg.num_types = self.V
+        cfg.num_docs = self.D
+        cfg.alpha = alpha.ctypes.data_as(C.POINTER(C.c_double))
+        cfg.beta = float(beta)
+        cfg.seed = int(seed) & (2**64 - 1)
+        cfg.device = int(device)
+        cfg.token_base = int(token_base)
+        cfg.tokens_per_range = int(tokens_per_range)
+        zp = None
+        if z_init is not None:
+            self._z_init = np.ascontiguousarray(z_init, dtype=np.int32)
+            zp = self._z_init.ctypes.data
+        h = C.c_void_p()
+        capi.check(L.lda_create(C.byref(h), C.byref(cfg), doc_off,
+                                words.ctypes.data if self.N else None, zp), "lda_create")
+        self._h = h
+        self._L = L
+        self.device = int(device)
+        kp = C.c_int32()
+        capi.check(L.lda_get_shape(h, None, C.byref(kp), None, None, None), "lda_get_shape")
+        self.Kp = kp.value
+        self.beta = float(beta)
+
+    # ---------------------------------------------------------------- life
+    def close(self):
+        h = getattr(self, "_h", None)
+        if h:
+            self._L.lda_destroy(h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    # --------------------------------------------------------------- sweeps
+    def sweep(self, n: int = 1):
+        capi.check(self._L.lda_sweep(self._h, int(n)), "lda_sweep")
+
+    def sample(self):
+        capi.check(self._L.lda_sample(self._h), "lda_sample")
+
+    def apply(self):
+        capi.check(self._L.lda_apply(self._h), "lda_apply")
+
+    def delta_buffer(self):
+        ptr, cnt = C.c_void_p(), C.c_size_t()
+        capi.check(self._L.lda_delta_buffer(self._h, C.byref(ptr), C.byref(cnt)), "lda_delta_buffer")
+        return int(ptr.value), int(cnt.value)
+
+    def delta_tensor(self):
+        """Zero-copy torch int32 view of the pending delta (device memory)."""
+        import torch
+
+        ptr, cnt = self.delta_buffer()
+        t = torch.as_tensor(_DeviceArray(ptr, cnt), device=f"cuda:{self.device}")
+        assert t.data_ptr() == ptr and t.dtype == torch.int32
+        return t
+
+    def set_stream(self, stream_handle: int | None):
+        capi.check(self._L.lda_set_stream(self._h, stream_handle), "lda_set_stream")
+
+    def synchronize(self):
+        capi.check(self._L.lda_synchronize(self._h), "lda_synchronize")
+
+    @property
+    def sweep_index(self) -> int:
+        s = C.c_uint32()
+        capi.check(self._L.lda_get_sweep(self._h, C.byref(s)), "lda_get_sweep")
+        return s.value
+
+    @sweep_index.setter
+    def sweep_index(self, v: int):
+        capi.check(self._L.lda_set_sweep(self._h, int(v)), "lda_set_sweep")
+
+    def last_sample_ms(self) -> float:
+        ms = C.c_float()
+        capi.check(self._L.lda_last_sample_ms(self._h, C.byref(ms)), "lda_last_sample_ms")
+        return float(ms.value)
+
+    # ---------------------------------------------------------------- state
+    def z(self) -> np.ndarray:
+        out = np.empty(self.N, dtype=np.int32)
+        capi.check(self._L.lda_get_z(self._h, out), "lda_get_z")
+        return out
+
+    def set_z(self, z):
+        z = np.ascontiguousarray(z, dtype=np.int32)
+        capi.check(self._L.lda_set_z(self._h, z), "lda_set_z")
+
+    def counts(self, with_nd: bool = False):
+        nw = np.empty((self.V, self.K), dtype=np.int32)
+        nwsum = np.empty(self.K, dtype=np.int32)
+        nd = np.empty((self.D, self.K), dtype=np.int32) if with_nd else None
+        ndsum = np.empty(self.D, dtype=np.int32)
+        capi.check(self._L.lda_get_counts(self._h, nw.ctypes.data, nwsum.ctypes.data,
+                                          nd.ctypes.data if with_nd else None,
+                                          ndsum.ctypes.data), "lda_get_counts")
+        return nw, nwsum, nd, ndsum
+
+    def set_alpha_beta(self, alpha, beta: float):
+        a = np.ascontiguousarray(np.broadcast_to(np.asarray(alpha, dtype=np.float64), (self.K,)))
+        capi.check(self._L.lda_set_alpha_beta(self._h, a, float(beta)), "lda_set_alpha_beta")
+        self._alpha = a
+        self.beta = float(beta)
+
+    @property
+    def alpha(self) -> np.ndarray:
+        return self._alpha.copy()
+
+    def log_likelihood_parts(self):
+        a, b = C.c_double(), C.c_double()
+        capi.check(self._L.lda_log_likelihood_parts(self._h, C.byref(a), C.byref(b)),
+                   "lda_log_likelihood_parts")
+        return a.value, b.value
+
+    def log_likelihood(self) -> float:
+        out = C.c_double()
+        capi.check(self._L.lda_log_likelihood(self._h, C.byref(out)), "lda_log_likelihood")
+        return out.value
+
+    def infer(self, doc_off, words, n_iter: int = 100, burn_in: int = 10, thin: int = 10,
+              seed: int = 0) -> np.ndarray:
+        doc_off = np.ascontiguousarray(doc_off, dtype=np.int64)
+        words = np.ascontiguousarray(words, dtype=np.int32)
+        Dh = len(doc_off) - 1
+        theta = np.zeros((Dh, self.K), dtype=np.float64)
+        capi.check(self._L.lda_infer(self._h, Dh, doc_off, words, int(n_iter), int(burn_in),
+                                     int(thin), int(seed) & (2**64 - 1), theta), "lda_infer")
+        return theta
+
+    def mallet_packed(self):
+        """typeTopicCounts in Mallet's packed layout: (rows, row_off, topic_bits)."""
+        row_off = np.zeros(self.V + 1, dtype=np.int64)
+        bits = C.c_int32()
+        capi.check(self._L.lda_to_mallet_packed(self._h, None, row_off, C.byref(bits)),
+                   "lda_to_mallet_packed")
+        rows = np.zeros(int(row_off[-1]), dtype=np.int32)
+        capi.check(self._L.lda_to_mallet_packed(self._h, rows.ctypes.data if len(rows) else None,
+                                                row_off, C.byref(bits)), "lda_to_mallet_packed")
+        return rows, row_off, bits.value

@@ -1,0 +1,1050 @@
+/*
+ * lda_oracle.c — CPU restatements of the collapsed-Gibbs LDA hot path.
+ *
+ * TEST INFRASTRUCTURE ONLY (see lda_oracle.h for the contract and the parity
+ * status: the Mallet restatement is "parity unpinned" against Mallet 2.0.7,
+ * which cannot be built or run in this image; cpu_exact is the bit-exact
+ * oracle for the HIP sampler and is pinned by the committed golden fixtures).
+ *
+ * Compile with -ffp-contract=off: every fp32 fused multiply-add below is an
+ * explicit fmaf(), exactly where the HIP kernel issues v_fma_f32, and no other
+ * operation may be contracted.
+ */
+#include "lda_oracle.h"
+
+#include <math.h>
+#include <pthread.h>
+#include <stdlib.h>
+#include <string.h>
+
+/* ======================================================================== */
+/* Philox4x32-10 — Salmon, Moraes, Dror, Shaw, "Parallel random numbers: as  */
+/* easy as 1, 2, 3", SC'11; constants and round structure as in Random123's */
+/* philox.h.  Pinned by tests/test_oracle.py against the published KATs.    */
+/* ======================================================================== */
+#define PHILOX_M0 0xD2511F53u
+#define PHILOX_M1 0xCD9E8D57u
+#define PHILOX_W0 0x9E3779B9u
+#define PHILOX_W1 0xBB67AE85u
+
+void orc_philox4x32_10(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]) {
+  uint32_t c0 = ctr[0], c1 = ctr[1], c2 = ctr[2], c3 = ctr[3];
+  uint32_t k0 = key[0], k1 = key[1];
+  for (int r = 0; r < 10; ++r) {
+    if (r > 0) {
+      k0 += PHILOX_W0;
+      k1 += PHILOX_W1;
+    }
+    uint64_t p0 = (uint64_t)PHILOX_M0 * c0;
+    uint64_t p1 = (uint64_t)PHILOX_M1 * c2;
+    uint32_t hi0 = (uint32_t)(p0 >> 32), lo0 = (uint32_t)p0;
+    uint32_t hi1 = (uint32_t)(p1 >> 32), lo1 = (uint32_t)p1;
+    uint32_t n0 = hi1 ^ c1 ^ k0;
+    uint32_t n1 = lo1;
+    uint32_t n2 = hi0 ^ c3 ^ k1;
+    uint32_t n3 = lo0;
+    c0 = n0; c1 = n1; c2 = n2; c3 = n3;
+  }
+  out[0] = c0; out[1] = c1; out[2] = c2; out[3] = c3;
+}
+
+uint32_t orc_draw(uint64_t seed, uint64_t gtok, uint32_t c2, uint32_t c3) {
+  uint32_t ctr[4] = {(uint32_t)gtok, (uint32_t)(gtok >> 32), c2, c3};
+  uint32_t key[2] = {(uint32_t)seed, (uint32_t)(seed >> 32)};
+  uint32_t out[4];
+  orc_philox4x32_10(ctr, key, out);
+  return out[0];
+}
+
+float orc_u01(uint32_t x) { return (float)(x >> 8) * 0x1p-24f; }
+
+/* Philox stream ids (counter word 3). */
+#define STREAM_SAMPLE 0u
+#define STREAM_INIT 1u
+#define STREAM_INFER 2u
+
+/* ======================================================================== */
+/* java.util.Random: 48-bit LCG (JDK spec), base of cc.mallet.util.Randoms.  */
+/* ======================================================================== */
+#define JR_MULT 0x5DEECE66DULL
+#define JR_MASK ((1ULL << 48) - 1)
+
+void orc_jrandom_seed(orc_jrandom* r, int64_t seed) { r->s = ((uint64_t)seed ^ JR_MULT) & JR_MASK; }
+
+static inline int32_t jr_next(orc_jrandom* r, int bits) {
+  r->s = (r->s * JR_MULT + 0xBULL) & JR_MASK;
+  return (int32_t)(int64_t)(r->s >> (48 - bits));
+}
+
+int32_t orc_jrandom_next_int(orc_jrandom* r) { return jr_next(r, 32); }
+
+int32_t orc_jrandom_next_int_n(orc_jrandom* r, int32_t n) {
+  if ((n & -n) == n) return (int32_t)(((int64_t)n * (int64_t)jr_next(r, 31)) >> 31);
+  int32_t bits, val;
+  do {
+    bits = jr_next(r, 31);
+    val = bits % n;
+  } while (bits - val + (n - 1) < 0);
+  return val;
+}
+
+double orc_jrandom_next_double(orc_jrandom* r) {
+  int64_t hi = (int64_t)jr_next(r, 26);
+  int64_t lo = (int64_t)jr_next(r, 27);
+  return (double)((hi << 27) + lo) * 0x1p-53;
+}
+
+/* ======================================================================== */
+/* cc.mallet.types.Dirichlet.logGammaStirling [M]                            */
+/* ======================================================================== */
+double orc_log_gamma_stirling(double z) {
+  const double HALF_LOG_TWO_PI = log(2.0 * M_PI) / 2.0;
+  int shift = 0;
+  while (z < 2) {
+    z++;
+    shift++;
+  }
+  double result = HALF_LOG_TWO_PI + (z - 0.5) * log(z) - z + 1 / (12 * z) - 1 / (360 * z * z * z) +
+                  1 / (1260 * z * z * z * z * z);
+  while (shift > 0) {
+    shift--;
+    z--;
+    result -= log(z);
+  }
+  return result;
+}
+
+/* ======================================================================== */
+/* cpu_exact                                                                */
+/* ======================================================================== */
+struct orc_exact {
+  int32_t K, Kp, C, V;
+  int64_t D, N;
+  int64_t* doc_off;
+  int32_t* words;
+  int32_t* z;
+  int32_t* nw;    /* V*Kp snapshot */
+  int32_t* nwsum; /* Kp */
+  int32_t* delta; /* V*Kp + Kp */
+  double* alpha;  /* K */
+  double beta;
+  float* alpha_f; /* Kp (0 in the padding) */
+  float beta_f, vbeta_f;
+  float* inv;    /* Kp: 1/(nwsum + V*beta), 0 in the padding */
+  float* inv_m1; /* Kp: 1/(nwsum - 1 + V*beta) */
+  uint64_t seed;
+  int64_t token_base;
+  uint32_t sweep;
+};
+
+static void exact_prepare_topics(orc_exact* s) {
+  for (int k = 0; k < s->Kp; ++k) {
+    if (k < s->K) {
+      s->alpha_f[k] = (float)s->alpha[k];
+      s->inv[k] = 1.0f / ((float)s->nwsum[k] + s->vbeta_f);
+      s->inv_m1[k] = 1.0f / ((float)(s->nwsum[k] - 1) + s->vbeta_f);
+    } else {
+      s->alpha_f[k] = 0.0f;
+      s->inv[k] = 0.0f;
+      s->inv_m1[k] = 0.0f;
+    }
+  }
+}
+
+orc_exact* orc_exact_create(int32_t K, int32_t V, int64_t D, const int64_t* doc_off,
+                            const int32_t* words, const int32_t* z_init, const double* alpha,
+                            double beta, uint64_t seed, int64_t token_base) {
+  orc_exact* s = (orc_exact*)calloc(1, sizeof(orc_exact));
+  s->K = K;
+  s->Kp = (K + 63) / 64 * 64;
+  s->C = s->Kp / 64;
+  s->V = V;
+  s->D = D;
+  s->N = doc_off[D] - doc_off[0];
+  s->doc_off = (int64_t*)malloc(sizeof(int64_t) * (D + 1));
+  for (int64_t d = 0; d <= D; ++d) s->doc_off[d] = doc_off[d] - doc_off[0];
+  s->words = (int32_t*)malloc(sizeof(int32_t) * (s->N ? s->N : 1));
+  s->z = (int32_t*)malloc(sizeof(int32_t) * (s->N ? s->N : 1));
+  memcpy(s->words, words, sizeof(int32_t) * s->N);
+  s->nw = (int32_t*)calloc((size_t)V * s->Kp, sizeof(int32_t));
+  s->nwsum = (int32_t*)calloc(s->Kp, sizeof(int32_t));
+  s->delta = (int32_t*)calloc((size_t)V * s->Kp + s->Kp, sizeof(int32_t));
+  s->alpha = (double*)malloc(sizeof(double) * K);
+  memcpy(s->alpha, alpha, sizeof(double) * K);
+  s->beta = beta;
+  s->alpha_f = (float*)calloc(s->Kp, sizeof(float));
+  s->inv = (float*)calloc(s->Kp, sizeof(float));
+  s->inv_m1 = (float*)calloc(s->Kp, sizeof(float));
+  s->beta_f = (float)beta;
+  s->vbeta_f = (float)((double)V * beta);
+  s->seed = seed;
+  s->token_base = token_base;
+  s->sweep = 0;
+  for (int64_t i = 0; i < s->N; ++i) {
+    if (z_init) {
+      s->z[i] = z_init[i];
+    } else {
+      uint32_t x = orc_draw(seed, (uint64_t)(token_base + i), 0u, STREAM_INIT);
+      s->z[i] = (int32_t)(((uint64_t)x * (uint64_t)K) >> 32);
+    }
+  }
+  /* local counts become the pending delta; the first apply (after an
+   * all-reduce when sharded) turns them into the global snapshot. */
+  int32_t* dsum = s->delta + (size_t)V * s->Kp;
+  for (int64_t i = 0; i < s->N; ++i) {
+    s->delta[(size_t)s->words[i] * s->Kp + s->z[i]] += 1;
+    dsum[s->z[i]] += 1;
+  }
+  exact_prepare_topics(s);
+  return s;
+}
+
+void orc_exact_destroy(orc_exact* s) {
+  if (!s) return;
+  free(s->doc_off); free(s->words); free(s->z); free(s->nw); free(s->nwsum); free(s->delta);
+  free(s->alpha); free(s->alpha_f); free(s->inv); free(s->inv_m1);
+  free(s);
+}
+
+int32_t orc_exact_kpad(const orc_exact* s) { return s->Kp; }
+int32_t* orc_exact_delta(orc_exact* s) { return s->delta; }
+void orc_exact_set_sweep(orc_exact* s, uint32_t sweep) { s->sweep = sweep; }
+uint32_t orc_exact_get_sweep(const orc_exact* s) { return s->sweep; }
+
+void orc_exact_apply(orc_exact* s) {
+  size_t nv = (size_t)s->V * s->Kp;
+  for (size_t i = 0; i < nv; ++i) {
+    s->nw[i] += s->delta[i];
+    s->delta[i] = 0;
+  }
+  for (int k = 0; k < s->Kp; ++k) {
+    s->nwsum[k] += s->delta[nv + k];
+    s->delta[nv + k] = 0;
+  }
+  exact_prepare_topics(s);
+}
+
+void orc_exact_set_alpha_beta(orc_exact* s, const double* alpha, double beta) {
+  memcpy(s->alpha, alpha, sizeof(double) * s->K);
+  s->beta = beta;
+  s->beta_f = (float)beta;
+  s->vbeta_f = (float)((double)s->V * beta);
+  exact_prepare_topics(s);
+}
+
+/* The wavefront inclusive scan of the kernel (DPP): row_shr 1,2,4,8 inside
+ * 16-lane rows (out-of-row sources read 0), then row_bcast:15 into rows 1 and
+ * 3, then row_bcast:31 into rows 2 and 3.  ldagibbssampling_amd/csrc/
+ * lda_kernels.hip: wave_incl_scan(). */
+static void wave_scan_emulate(float x[64]) {
+  float y[64];
+  for (int d = 1; d <= 8; d <<= 1) {
+    for (int l = 0; l < 64; ++l) y[l] = ((l & 15) >= d) ? x[l - d] : 0.0f;
+    for (int l = 0; l < 64; ++l) x[l] = y[l] + x[l];
+  }
+  for (int l = 0; l < 64; ++l) {
+    int row = l >> 4;
+    y[l] = (row == 1 || row == 3) ? x[16 * row - 1] : 0.0f;
+  }
+  for (int l = 0; l < 64; ++l) x[l] = x[l] + y[l];
+  for (int l = 0; l < 64; ++l) y[l] = (l >= 32) ? x[31] : 0.0f;
+  for (int l = 0; l < 64; ++l) x[l] = x[l] + y[l];
+}
+
+/* One categorical draw over the Kp padded topics.  nwrow = the snapshot row
+ * of the token's word; nd = live doc counts with the token already removed;
+ * zo = the token's old topic (-1: frozen, no self-correction). */
+static int exact_draw(const orc_exact* s, const int32_t* nwrow, const int32_t* nd, int zo,
+                      float u, float* S /* scratch Kp */) {
+  const int C = s->C, K = s->K;
+  float t[64];
+  for (int l = 0; l < 64; ++l) {
+    float acc = 0.0f;
+    for (int j = 0; j < C; ++j) {
+      int k = l * C + j;
+      int32_t c = nwrow[k];
+      float iv = s->inv[k];
+      if (k == zo) {
+        c -= 1;
+        iv = s->inv_m1[k];
+      }
+      float b = ((float)c + s->beta_f) * iv;
+      float a = (float)nd[k] + s->alpha_f[k];
+      acc = fmaf(a, b, acc);
+      S[k] = acc;
+    }
+    t[l] = acc;
+  }
+  wave_scan_emulate(t);
+  float total = t[63];
+  float thr = u * total;
+  const int last_lane = (K - 1) / C;
+  int lstar = last_lane;
+  for (int l = 0; l <= last_lane; ++l) {
+    if (t[l] > thr) {
+      lstar = l;
+      break;
+    }
+  }
+  float E = lstar > 0 ? t[lstar - 1] : 0.0f;
+  int cnt = 0;
+  for (int j = 0; j < C; ++j) cnt += (E + S[lstar * C + j] <= thr) ? 1 : 0;
+  int jsel;
+  if (cnt < C) {
+    jsel = cnt;
+  } else {
+    jsel = (lstar < last_lane) ? C - 1 : (K - 1) % C;
+  }
+  return lstar * C + jsel;
+}
+
+/* Sample the docs [d0, d1) of a token stream against the snapshot. */
+static void exact_sample_docs(const orc_exact* s, const int64_t* doc_off, const int32_t* words,
+                              int32_t* z, int64_t d0, int64_t d1, int frozen, uint32_t c2,
+                              uint32_t c3, int64_t token_base, int32_t* delta) {
+  int32_t* nd = (int32_t*)calloc(s->Kp, sizeof(int32_t));
+  float* S = (float*)malloc(sizeof(float) * s->Kp);
+  int32_t* dsum = delta ? delta + (size_t)s->V * s->Kp : NULL;
+  for (int64_t d = d0; d < d1; ++d) {
+    memset(nd, 0, sizeof(int32_t) * s->Kp);
+    for (int64_t i = doc_off[d]; i < doc_off[d + 1]; ++i) nd[z[i]]++;
+    for (int64_t i = doc_off[d]; i < doc_off[d + 1]; ++i) {
+      int w = words[i];
+      int zo = z[i];
+      float u = orc_u01(orc_draw(s->seed, (uint64_t)(token_base + i), c2, c3));
+      nd[zo]--;
+      int kn = exact_draw(s, s->nw + (size_t)w * s->Kp, nd, frozen ? -1 : zo, u, S);
+      nd[kn]++;
+      z[i] = kn;
+      if (!frozen && kn != zo) {
+        delta[(size_t)w * s->Kp + zo] -= 1;
+        delta[(size_t)w * s->Kp + kn] += 1;
+        dsum[zo] -= 1;
+        dsum[kn] += 1;
+      }
+    }
+  }
+  free(nd);
+  free(S);
+}
+
+void orc_exact_sample(orc_exact* s, int frozen) {
+  exact_sample_docs(s, s->doc_off, s->words, s->z, 0, s->D, frozen, s->sweep, STREAM_SAMPLE,
+                    s->token_base, frozen ? NULL : s->delta);
+  s->sweep++;
+}
+
+void orc_exact_get_z(const orc_exact* s, int32_t* z) { memcpy(z, s->z, sizeof(int32_t) * s->N); }
+
+void orc_exact_get_counts(const orc_exact* s, int32_t* nw, int32_t* nwsum, int32_t* nd,
+                          int32_t* ndsum) {
+  if (nw)
+    for (int w = 0; w < s->V; ++w)
+      for (int k = 0; k < s->K; ++k) nw[(size_t)w * s->K + k] = s->nw[(size_t)w * s->Kp + k];
+  if (nwsum)
+    for (int k = 0; k < s->K; ++k) nwsum[k] = s->nwsum[k];
+  if (nd) {
+    memset(nd, 0, sizeof(int32_t) * (size_t)s->D * s->K);
+    for (int64_t d = 0; d < s->D; ++d)
+      for (int64_t i = s->doc_off[d]; i < s->doc_off[d + 1]; ++i) nd[(size_t)d * s->K + s->z[i]]++;
+  }
+  if (ndsum)
+    for (int64_t d = 0; d < s->D; ++d) ndsum[d] = (int32_t)(s->doc_off[d + 1] - s->doc_off[d]);
+}
+
+/* ParallelTopicModel.modelLogLikelihood() [M], restated over dense counts. */
+static double mallet_ll_dense(int K, int V, int Kstride, const double* alpha, double beta,
+                              int64_t D, const int64_t* doc_off, const int32_t* z,
+                              const int32_t* nw, const int32_t* nwsum) {
+  double alpha_sum = 0.0;
+  for (int k = 0; k < K; ++k) alpha_sum += alpha[k];
+  double ll = 0.0;
+  double* topic_lg = (double*)malloc(sizeof(double) * K);
+  int32_t* counts = (int32_t*)calloc(K, sizeof(int32_t));
+  for (int k = 0; k < K; ++k) topic_lg[k] = orc_log_gamma_stirling(alpha[k]);
+  for (int64_t d = 0; d < D; ++d) {
+    for (int64_t i = doc_off[d]; i < doc_off[d + 1]; ++i) counts[z[i]]++;
+    for (int k = 0; k < K; ++k)
+      if (counts[k] > 0) ll += orc_log_gamma_stirling(alpha[k] + counts[k]) - topic_lg[k];
+    ll -= orc_log_gamma_stirling(alpha_sum + (double)(doc_off[d + 1] - doc_off[d]));
+    memset(counts, 0, sizeof(int32_t) * K);
+  }
+  ll += (double)D * orc_log_gamma_stirling(alpha_sum);
+  int64_t nonzero = 0;
+  for (int w = 0; w < V; ++w)
+    for (int k = 0; k < K; ++k) {
+      int32_t c = nw[(size_t)w * Kstride + k];
+      if (c > 0) {
+        nonzero++;
+        ll += orc_log_gamma_stirling(beta + c);
+      }
+    }
+  for (int k = 0; k < K; ++k) ll -= orc_log_gamma_stirling(beta * V + nwsum[k]);
+  ll += orc_log_gamma_stirling(beta * V) * K;
+  ll -= orc_log_gamma_stirling(beta) * (double)nonzero;
+  free(topic_lg);
+  free(counts);
+  return ll;
+}
+
+double orc_exact_log_likelihood(const orc_exact* s) {
+  return mallet_ll_dense(s->K, s->V, s->Kp, s->alpha, s->beta, s->D, s->doc_off, s->z, s->nw,
+                         s->nwsum);
+}
+
+void orc_exact_infer(const orc_exact* s, int64_t Dh, const int64_t* doc_off, const int32_t* words,
+                     int32_t n_iter, int32_t burn_in, int32_t thin, uint64_t seed, double* theta) {
+  int64_t N = doc_off[Dh] - doc_off[0];
+  int64_t* off = (int64_t*)malloc(sizeof(int64_t) * (Dh + 1));
+  for (int64_t d = 0; d <= Dh; ++d) off[d] = doc_off[d] - doc_off[0];
+  const int32_t* w = words;
+  int32_t* z = (int32_t*)malloc(sizeof(int32_t) * (N ? N : 1));
+  /* TopicInferencer init: the most frequent topic of the word in the model
+   * (packed rows are sorted by (count << bits | topic), so ties go to the
+   * larger topic id). */
+  for (int64_t i = 0; i < N; ++i) {
+    const int32_t* row = s->nw + (size_t)w[i] * s->Kp;
+    int best = 0;
+    for (int k = 1; k < s->K; ++k)
+      if (row[k] >= row[best]) best = k;
+    z[i] = best;
+  }
+  int64_t* acc = (int64_t*)calloc((size_t)Dh * s->K, sizeof(int64_t));
+  int32_t nsamples = 0;
+  orc_exact tmp = *s;
+  tmp.seed = seed;
+  for (int32_t it = 1; it <= n_iter; ++it) {
+    exact_sample_docs(&tmp, off, w, z, 0, Dh, 1, (uint32_t)(it - 1), STREAM_INFER, 0, NULL);
+    if (it > burn_in && (it - burn_in) % thin == 0) {
+      nsamples++;
+      for (int64_t d = 0; d < Dh; ++d)
+        for (int64_t i = off[d]; i < off[d + 1]; ++i) acc[(size_t)d * s->K + z[i]]++;
+    }
+  }
+  if (nsamples == 0) {
+    nsamples = 1;
+    for (int64_t d = 0; d < Dh; ++d)
+      for (int64_t i = off[d]; i < off[d + 1]; ++i) acc[(size_t)d * s->K + z[i]]++;
+  }
+  for (int64_t d = 0; d < Dh; ++d) {
+    double sum = 0.0;
+    for (int k = 0; k < s->K; ++k) {
+      double v = (double)nsamples * s->alpha[k] + (double)acc[(size_t)d * s->K + k];
+      theta[(size_t)d * s->K + k] = v;
+      sum += v;
+    }
+    for (int k = 0; k < s->K; ++k) theta[(size_t)d * s->K + k] /= sum;
+  }
+  free(acc);
+  free(z);
+  free(off);
+}
+
+double orc_doc_completion_loglik(int32_t K, int32_t V, const int32_t* nw, const int32_t* nwsum,
+                                 double beta, int64_t Dh, const double* theta,
+                                 const int64_t* doc_off, const int32_t* words) {
+  double ll = 0.0;
+  double vbeta = beta * V;
+  for (int64_t d = 0; d < Dh; ++d) {
+    const double* th = theta + (size_t)d * K;
+    for (int64_t i = doc_off[d]; i < doc_off[d + 1]; ++i) {
+      int w = words[i];
+      double p = 0.0;
+      for (int k = 0; k < K; ++k) p += th[k] * ((double)nw[(size_t)w * K + k] + beta) / ((double)nwsum[k] + vbeta);
+      ll += log(p);
+    }
+  }
+  return ll;
+}
+
+/* ======================================================================== */
+/* cpu_mallet — Mallet 2.0.7 ParallelTopicModel / WorkerRunnable [M]        */
+/* ======================================================================== */
+typedef struct {
+  int32_t** ttc;  /* typeTopicCounts[V][len[w]] packed (count<<bits)|topic */
+  int32_t* tpt;   /* tokensPerTopic[K] */
+  double* cached; /* cachedCoefficients[K] */
+  double smoothing_only_mass;
+  orc_jrandom rng;
+  int64_t start_doc, num_docs;
+  int32_t *local_counts, *local_index;
+  double* term_scores;
+} mallet_worker;
+
+struct orc_mallet {
+  int32_t K, V, T;
+  int32_t topic_mask, topic_bits;
+  double alpha_sum, beta, beta_sum;
+  double* alpha;
+  int64_t D, N;
+  int64_t* doc_off;
+  int32_t* words;
+  int32_t* z;
+  int32_t* type_totals;
+  int32_t* row_len;
+  int32_t** ttc; /* global typeTopicCounts */
+  int32_t* tpt;  /* global tokensPerTopic */
+  mallet_worker* workers;
+  int64_t seed;
+};
+
+static int32_t** ttc_alloc(const orc_mallet* m) {
+  int32_t** t = (int32_t**)malloc(sizeof(int32_t*) * m->V);
+  for (int w = 0; w < m->V; ++w) t[w] = (int32_t*)calloc(m->row_len[w] ? m->row_len[w] : 1, sizeof(int32_t));
+  return t;
+}
+static void ttc_free(const orc_mallet* m, int32_t** t) {
+  for (int w = 0; w < m->V; ++w) free(t[w]);
+  free(t);
+}
+
+/* buildInitialTypeTopicCounts / WorkerRunnable.buildLocalTypeTopicCounts:
+ * add one (type, topic) occurrence to a packed row, keeping it sorted. */
+static void ttc_add_one(const orc_mallet* m, int32_t* row, int len, int topic) {
+  int index = 0;
+  int current_topic = row[index] & m->topic_mask;
+  while (row[index] > 0 && current_topic != topic) {
+    index++;
+    if (index == len) return; /* Mallet logs "overflow"; cannot happen: len >= distinct topics */
+    current_topic = row[index] & m->topic_mask;
+  }
+  int current_value = row[index] >> m->topic_bits;
+  if (current_value == 0) {
+    row[index] = (1 << m->topic_bits) + topic;
+  } else {
+    row[index] = ((current_value + 1) << m->topic_bits) + topic;
+    while (index > 0 && row[index] > row[index - 1]) {
+      int32_t tmp = row[index];
+      row[index] = row[index - 1];
+      row[index - 1] = tmp;
+      index--;
+    }
+  }
+}
+
+static void build_counts(const orc_mallet* m, int32_t** ttc, int32_t* tpt, int64_t d0, int64_t d1) {
+  memset(tpt, 0, sizeof(int32_t) * m->K);
+  for (int w = 0; w < m->V; ++w) {
+    int32_t* row = ttc[w];
+    for (int p = 0; p < m->row_len[w] && row[p] > 0; ++p) row[p] = 0;
+  }
+  for (int64_t d = d0; d < d1; ++d)
+    for (int64_t i = m->doc_off[d]; i < m->doc_off[d + 1]; ++i) {
+      int topic = m->z[i];
+      tpt[topic]++;
+      ttc_add_one(m, ttc[m->words[i]], m->row_len[m->words[i]], topic);
+    }
+}
+
+orc_mallet* orc_mallet_create(int32_t K, double alpha_sum, double beta, int32_t V, int64_t D,
+                              const int64_t* doc_off, const int32_t* words, int64_t seed,
+                              int32_t num_threads) {
+  orc_mallet* m = (orc_mallet*)calloc(1, sizeof(orc_mallet));
+  m->K = K;
+  m->V = V;
+  m->T = num_threads < 1 ? 1 : num_threads;
+  /* ParallelTopicModel(int numberOfTopics, double alphaSum, double beta) */
+  if ((K & (K - 1)) == 0) {
+    m->topic_mask = K - 1;
+  } else {
+    int hb = 1;
+    while (hb * 2 <= K) hb *= 2;
+    m->topic_mask = hb * 2 - 1;
+  }
+  m->topic_bits = __builtin_popcount((unsigned)m->topic_mask);
+  m->alpha_sum = alpha_sum;
+  m->beta = beta;
+  m->alpha = (double*)malloc(sizeof(double) * K);
+  for (int k = 0; k < K; ++k) m->alpha[k] = alpha_sum / K;
+  m->D = D;
+  m->N = doc_off[D] - doc_off[0];
+  m->doc_off = (int64_t*)malloc(sizeof(int64_t) * (D + 1));
+  for (int64_t d = 0; d <= D; ++d) m->doc_off[d] = doc_off[d] - doc_off[0];
+  m->words = (int32_t*)malloc(sizeof(int32_t) * (m->N ? m->N : 1));
+  memcpy(m->words, words, sizeof(int32_t) * m->N);
+  m->z = (int32_t*)malloc(sizeof(int32_t) * (m->N ? m->N : 1));
+  m->seed = seed;
+  /* addInstances: betaSum, typeTotals, row lengths min(K, typeTotal) */
+  m->beta_sum = beta * V;
+  m->type_totals = (int32_t*)calloc(V, sizeof(int32_t));
+  for (int64_t i = 0; i < m->N; ++i) m->type_totals[m->words[i]]++;
+  m->row_len = (int32_t*)malloc(sizeof(int32_t) * V);
+  for (int w = 0; w < V; ++w) m->row_len[w] = m->type_totals[w] < K ? m->type_totals[w] : K;
+  m->ttc = ttc_alloc(m);
+  m->tpt = (int32_t*)calloc(K, sizeof(int32_t));
+  /* topics[position] = random.nextInt(numTopics), doc by doc */
+  orc_jrandom r;
+  orc_jrandom_seed(&r, seed);
+  for (int64_t i = 0; i < m->N; ++i) m->z[i] = orc_jrandom_next_int_n(&r, K);
+  build_counts(m, m->ttc, m->tpt, 0, D);
+  /* estimate(): runnables with contiguous doc blocks; last takes the rest */
+  m->workers = (mallet_worker*)calloc(m->T, sizeof(mallet_worker));
+  int64_t per = D / m->T, offset = 0;
+  for (int t = 0; t < m->T; ++t) {
+    mallet_worker* wk = &m->workers[t];
+    wk->start_doc = offset;
+    wk->num_docs = (t == m->T - 1) ? D - offset : per;
+    offset += wk->num_docs;
+    if (m->T > 1) {
+      wk->ttc = ttc_alloc(m);
+      for (int w = 0; w < V; ++w) memcpy(wk->ttc[w], m->ttc[w], sizeof(int32_t) * m->row_len[w]);
+      wk->tpt = (int32_t*)malloc(sizeof(int32_t) * K);
+      memcpy(wk->tpt, m->tpt, sizeof(int32_t) * K);
+    } else {
+      wk->ttc = m->ttc;
+      wk->tpt = m->tpt;
+    }
+    wk->cached = (double*)calloc(K, sizeof(double));
+    wk->local_counts = (int32_t*)calloc(K, sizeof(int32_t));
+    wk->local_index = (int32_t*)calloc(K, sizeof(int32_t));
+    wk->term_scores = (double*)calloc(K, sizeof(double));
+    orc_jrandom_seed(&wk->rng, seed);
+  }
+  return m;
+}
+
+void orc_mallet_destroy(orc_mallet* m) {
+  if (!m) return;
+  for (int t = 0; t < m->T; ++t) {
+    mallet_worker* wk = &m->workers[t];
+    if (m->T > 1) {
+      ttc_free(m, wk->ttc);
+      free(wk->tpt);
+    }
+    free(wk->cached); free(wk->local_counts); free(wk->local_index); free(wk->term_scores);
+  }
+  free(m->workers);
+  ttc_free(m, m->ttc);
+  free(m->tpt); free(m->alpha); free(m->doc_off); free(m->words); free(m->z);
+  free(m->type_totals); free(m->row_len);
+  free(m);
+}
+
+/* WorkerRunnable.sampleTopicsForOneDoc [M] */
+static void mallet_sample_doc(const orc_mallet* m, mallet_worker* wk, int64_t d) {
+  const int K = m->K;
+  const int32_t mask = m->topic_mask, bits = m->topic_bits;
+  const double beta = m->beta, beta_sum = m->beta_sum;
+  const double* alpha = m->alpha;
+  int32_t* tpt = wk->tpt;
+  double* cached = wk->cached;
+  int32_t* lc = wk->local_counts;
+  int32_t* li = wk->local_index;
+  double* scores = wk->term_scores;
+  int32_t* topics = m->z + m->doc_off[d];
+  const int32_t* tokens = m->words + m->doc_off[d];
+  int64_t len = m->doc_off[d + 1] - m->doc_off[d];
+
+  memset(lc, 0, sizeof(int32_t) * K);
+  for (int64_t p = 0; p < len; ++p) lc[topics[p]]++;
+  int dense = 0;
+  for (int k = 0; k < K; ++k)
+    if (lc[k] != 0) li[dense++] = k;
+  int nonzero = dense;
+  double topic_beta_mass = 0.0;
+  for (dense = 0; dense < nonzero; ++dense) {
+    int k = li[dense];
+    int n = lc[k];
+    topic_beta_mass += beta * n / (tpt[k] + beta_sum);
+    cached[k] = (alpha[k] + n) / (tpt[k] + beta_sum);
+  }
+  for (int64_t p = 0; p < len; ++p) {
+    int type = tokens[p];
+    int old_topic = topics[p];
+    int32_t* row = wk->ttc[type];
+    int row_len = m->row_len[type];
+    /* remove this token from all counts */
+    wk->smoothing_only_mass -= alpha[old_topic] * beta / (tpt[old_topic] + beta_sum);
+    topic_beta_mass -= beta * lc[old_topic] / (tpt[old_topic] + beta_sum);
+    lc[old_topic]--;
+    if (lc[old_topic] == 0) {
+      dense = 0;
+      while (li[dense] != old_topic) dense++;
+      while (dense < nonzero) {
+        if (dense < K - 1) li[dense] = li[dense + 1];
+        dense++;
+      }
+      nonzero--;
+    }
+    tpt[old_topic]--;
+    wk->smoothing_only_mass += alpha[old_topic] * beta / (tpt[old_topic] + beta_sum);
+    topic_beta_mass += beta * lc[old_topic] / (tpt[old_topic] + beta_sum);
+    cached[old_topic] = (alpha[old_topic] + lc[old_topic]) / (tpt[old_topic] + beta_sum);
+
+    /* walk the packed row: decrement the old topic, score the rest */
+    int index = 0;
+    int already_decremented = 0;
+    double topic_term_mass = 0.0;
+    while (index < row_len && row[index] > 0) {
+      int current_topic = row[index] & mask;
+      int current_value = row[index] >> bits;
+      if (!already_decremented && current_topic == old_topic) {
+        current_value--;
+        if (current_value == 0)
+          row[index] = 0;
+        else
+          row[index] = (current_value << bits) + old_topic;
+        int sub = index;
+        while (sub < row_len - 1 && row[sub] < row[sub + 1]) {
+          int32_t tmp = row[sub];
+          row[sub] = row[sub + 1];
+          row[sub + 1] = tmp;
+          sub++;
+        }
+        already_decremented = 1;
+      } else {
+        double score = cached[current_topic] * current_value;
+        topic_term_mass += score;
+        scores[index] = score;
+        index++;
+      }
+    }
+    double sample = orc_jrandom_next_double(&wk->rng) *
+                    (wk->smoothing_only_mass + topic_beta_mass + topic_term_mass);
+    int new_topic = -1;
+    if (sample < topic_term_mass) {
+      int i = -1;
+      while (sample > 0) {
+        i++;
+        sample -= scores[i];
+      }
+      new_topic = row[i] & mask;
+      int current_value = row[i] >> bits;
+      row[i] = ((current_value + 1) << bits) + new_topic;
+      while (i > 0 && row[i] > row[i - 1]) {
+        int32_t tmp = row[i];
+        row[i] = row[i - 1];
+        row[i - 1] = tmp;
+        i--;
+      }
+    } else {
+      sample -= topic_term_mass;
+      if (sample < topic_beta_mass) {
+        sample /= beta;
+        for (dense = 0; dense < nonzero; ++dense) {
+          int k = li[dense];
+          sample -= lc[k] / (tpt[k] + beta_sum);
+          if (sample <= 0.0) {
+            new_topic = k;
+            break;
+          }
+        }
+      } else {
+        sample -= topic_beta_mass;
+        sample /= beta;
+        new_topic = 0;
+        sample -= alpha[new_topic] / (tpt[new_topic] + beta_sum);
+        while (sample > 0.0 && new_topic < K - 1) {
+          new_topic++;
+          sample -= alpha[new_topic] / (tpt[new_topic] + beta_sum);
+        }
+      }
+      if (new_topic == -1) new_topic = K - 1; /* "sampling error" fallback */
+      index = 0;
+      while (row[index] > 0 && (row[index] & mask) != new_topic) {
+        index++;
+        if (index == row_len) break;
+      }
+      if (index < row_len) {
+        if (row[index] == 0) {
+          row[index] = (1 << bits) + new_topic;
+        } else {
+          int current_value = row[index] >> bits;
+          row[index] = ((current_value + 1) << bits) + new_topic;
+          while (index > 0 && row[index] > row[index - 1]) {
+            int32_t tmp = row[index];
+            row[index] = row[index - 1];
+            row[index - 1] = tmp;
+            index--;
+          }
+        }
+      }
+    }
+    topics[p] = new_topic;
+    wk->smoothing_only_mass -= alpha[new_topic] * beta / (tpt[new_topic] + beta_sum);
+    topic_beta_mass -= beta * lc[new_topic] / (tpt[new_topic] + beta_sum);
+    lc[new_topic]++;
+    if (lc[new_topic] == 1) {
+      dense = nonzero;
+      while (dense > 0 && li[dense - 1] > new_topic) {
+        li[dense] = li[dense - 1];
+        dense--;
+      }
+      li[dense] = new_topic;
+      nonzero++;
+    }
+    tpt[new_topic]++;
+    cached[new_topic] = (alpha[new_topic] + lc[new_topic]) / (tpt[new_topic] + beta_sum);
+    wk->smoothing_only_mass += alpha[new_topic] * beta / (tpt[new_topic] + beta_sum);
+    topic_beta_mass += beta * lc[new_topic] / (tpt[new_topic] + beta_sum);
+  }
+  for (dense = 0; dense < nonzero; ++dense) {
+    int k = li[dense];
+    cached[k] = alpha[k] / (tpt[k] + beta_sum);
+  }
+}
+
+typedef struct {
+  orc_mallet* m;
+  int t;
+} mallet_job;
+
+/* WorkerRunnable.run() [M] */
+static void* mallet_worker_run(void* arg) {
+  mallet_job* job = (mallet_job*)arg;
+  orc_mallet* m = job->m;
+  mallet_worker* wk = &m->workers[job->t];
+  wk->smoothing_only_mass = 0.0;
+  for (int k = 0; k < m->K; ++k) {
+    wk->smoothing_only_mass += m->alpha[k] * m->beta / (wk->tpt[k] + m->beta_sum);
+    wk->cached[k] = m->alpha[k] / (wk->tpt[k] + m->beta_sum);
+  }
+  for (int64_t d = wk->start_doc; d < m->D && d < wk->start_doc + wk->num_docs; ++d)
+    mallet_sample_doc(m, wk, d);
+  if (m->T > 1) build_counts(m, wk->ttc, wk->tpt, wk->start_doc, wk->start_doc + wk->num_docs);
+  return NULL;
+}
+
+/* ParallelTopicModel.sumTypeTopicCounts + copy-back to every runnable [M] */
+static void mallet_sum_type_topic_counts(orc_mallet* m) {
+  memset(m->tpt, 0, sizeof(int32_t) * m->K);
+  for (int w = 0; w < m->V; ++w) {
+    int32_t* row = m->ttc[w];
+    for (int p = 0; p < m->row_len[w] && row[p] > 0; ++p) row[p] = 0;
+  }
+  for (int t = 0; t < m->T; ++t) {
+    mallet_worker* wk = &m->workers[t];
+    for (int k = 0; k < m->K; ++k) m->tpt[k] += wk->tpt[k];
+    for (int w = 0; w < m->V; ++w) {
+      int32_t* src = wk->ttc[w];
+      int32_t* dst = m->ttc[w];
+      int len = m->row_len[w];
+      for (int si = 0; si < len && src[si] > 0; ++si) {
+        int topic = src[si] & m->topic_mask;
+        int count = src[si] >> m->topic_bits;
+        int ti = 0;
+        int current_topic = dst[ti] & m->topic_mask;
+        while (dst[ti] > 0 && current_topic != topic) {
+          ti++;
+          current_topic = dst[ti] & m->topic_mask;
+        }
+        int current_count = dst[ti] >> m->topic_bits;
+        dst[ti] = ((current_count + count) << m->topic_bits) + topic;
+        while (ti > 0 && dst[ti] > dst[ti - 1]) {
+          int32_t tmp = dst[ti];
+          dst[ti] = dst[ti - 1];
+          dst[ti - 1] = tmp;
+          ti--;
+        }
+      }
+    }
+  }
+  for (int t = 0; t < m->T; ++t) {
+    mallet_worker* wk = &m->workers[t];
+    memcpy(wk->tpt, m->tpt, sizeof(int32_t) * m->K);
+    for (int w = 0; w < m->V; ++w) {
+      int32_t* dst = wk->ttc[w];
+      int32_t* src = m->ttc[w];
+      for (int p = 0; p < m->row_len[w]; ++p) {
+        if (src[p] != 0)
+          dst[p] = src[p];
+        else if (dst[p] != 0)
+          dst[p] = 0;
+        else
+          break;
+      }
+    }
+  }
+}
+
+void orc_mallet_estimate(orc_mallet* m, int32_t n_iter) {
+  mallet_job* jobs = (mallet_job*)malloc(sizeof(mallet_job) * m->T);
+  pthread_t* th = (pthread_t*)malloc(sizeof(pthread_t) * m->T);
+  for (int it = 1; it <= n_iter; ++it) {
+    if (m->T > 1) {
+      for (int t = 0; t < m->T; ++t) {
+        jobs[t].m = m;
+        jobs[t].t = t;
+        pthread_create(&th[t], NULL, mallet_worker_run, &jobs[t]);
+      }
+      for (int t = 0; t < m->T; ++t) pthread_join(th[t], NULL);
+      mallet_sum_type_topic_counts(m);
+    } else {
+      jobs[0].m = m;
+      jobs[0].t = 0;
+      mallet_worker_run(&jobs[0]);
+    }
+  }
+  free(jobs);
+  free(th);
+}
+
+static void mallet_dense_counts(const orc_mallet* m, int32_t* nw, int32_t* nwsum) {
+  if (nw) {
+    memset(nw, 0, sizeof(int32_t) * (size_t)m->V * m->K);
+    for (int w = 0; w < m->V; ++w)
+      for (int p = 0; p < m->row_len[w] && m->ttc[w][p] > 0; ++p)
+        nw[(size_t)w * m->K + (m->ttc[w][p] & m->topic_mask)] = m->ttc[w][p] >> m->topic_bits;
+  }
+  if (nwsum) memcpy(nwsum, m->tpt, sizeof(int32_t) * m->K);
+}
+
+double orc_mallet_log_likelihood(const orc_mallet* m) {
+  int32_t* nw = (int32_t*)malloc(sizeof(int32_t) * (size_t)m->V * m->K);
+  mallet_dense_counts(m, nw, NULL);
+  double ll = mallet_ll_dense(m->K, m->V, m->K, m->alpha, m->beta, m->D, m->doc_off, m->z, nw, m->tpt);
+  free(nw);
+  return ll;
+}
+
+void orc_mallet_get_z(const orc_mallet* m, int32_t* z) { memcpy(z, m->z, sizeof(int32_t) * m->N); }
+
+void orc_mallet_get_counts(const orc_mallet* m, int32_t* nw, int32_t* nwsum) {
+  mallet_dense_counts(m, nw, nwsum);
+}
+
+/* TopicInferencer.getSampledDistribution [M] (sparse, fp64, frozen counts). */
+void orc_mallet_infer(const orc_mallet* m, int64_t Dh, const int64_t* doc_off, const int32_t* words,
+                      int32_t n_iter, int32_t burn_in, int32_t thin, int64_t seed, double* theta) {
+  const int K = m->K;
+  const int32_t mask = m->topic_mask;
+  const double beta = m->beta, beta_sum = m->beta_sum;
+  const double* alpha = m->alpha;
+  const int32_t* tpt = m->tpt;
+  int32_t** ttc = m->ttc;
+  double* cached = (double*)malloc(sizeof(double) * K);
+  double* scores = (double*)malloc(sizeof(double) * K);
+  int32_t* lc = (int32_t*)malloc(sizeof(int32_t) * K);
+  int32_t* li = (int32_t*)malloc(sizeof(int32_t) * K);
+  double smoothing_only_mass = 0.0;
+  for (int k = 0; k < K; ++k) {
+    smoothing_only_mass += alpha[k] * beta / (tpt[k] + beta_sum);
+    cached[k] = alpha[k] / (tpt[k] + beta_sum);
+  }
+  orc_jrandom rng;
+  orc_jrandom_seed(&rng, seed);
+  for (int64_t d = 0; d < Dh; ++d) {
+    const int32_t* tokens = words + (doc_off[d] - doc_off[0]);
+    int64_t len = doc_off[d + 1] - doc_off[d];
+    int32_t* topics = (int32_t*)calloc(len ? len : 1, sizeof(int32_t));
+    memset(lc, 0, sizeof(int32_t) * K);
+    for (int64_t p = 0; p < len; ++p) {
+      int type = tokens[p];
+      if (type < m->V && m->row_len[type] != 0) {
+        topics[p] = ttc[type][0] & mask;
+        lc[topics[p]]++;
+      }
+    }
+    int dense = 0;
+    for (int k = 0; k < K; ++k)
+      if (lc[k] != 0) li[dense++] = k;
+    int nonzero = dense;
+    double topic_beta_mass = 0.0;
+    for (dense = 0; dense < nonzero; ++dense) {
+      int k = li[dense];
+      topic_beta_mass += beta * lc[k] / (tpt[k] + beta_sum);
+      cached[k] = (alpha[k] + lc[k]) / (tpt[k] + beta_sum);
+    }
+    double* result = theta + (size_t)d * K;
+    for (int k = 0; k < K; ++k) result[k] = 0.0;
+    double sum = 0.0;
+    for (int it = 1; it <= n_iter; ++it) {
+      for (int64_t p = 0; p < len; ++p) {
+        int type = tokens[p];
+        if (type >= m->V || m->row_len[type] == 0) continue;
+        int old_topic = topics[p];
+        const int32_t* row = ttc[type];
+        int row_len = m->row_len[type];
+        topic_beta_mass -= beta * lc[old_topic] / (tpt[old_topic] + beta_sum);
+        lc[old_topic]--;
+        if (lc[old_topic] == 0) {
+          dense = 0;
+          while (li[dense] != old_topic) dense++;
+          while (dense < nonzero) {
+            if (dense < K - 1) li[dense] = li[dense + 1];
+            dense++;
+          }
+          nonzero--;
+        }
+        topic_beta_mass += beta * lc[old_topic] / (tpt[old_topic] + beta_sum);
+        cached[old_topic] = (alpha[old_topic] + lc[old_topic]) / (tpt[old_topic] + beta_sum);
+        int index = 0;
+        double topic_term_mass = 0.0;
+        while (index < row_len && row[index] > 0) {
+          int current_topic = row[index] & mask;
+          int current_value = row[index] >> m->topic_bits;
+          double score = cached[current_topic] * current_value;
+          topic_term_mass += score;
+          scores[index] = score;
+          index++;
+        }
+        double sample = orc_jrandom_next_double(&rng) * (smoothing_only_mass + topic_beta_mass + topic_term_mass);
+        int new_topic = -1;
+        if (sample < topic_term_mass) {
+          int i = -1;
+          while (sample > 0) {
+            i++;
+            sample -= scores[i];
+          }
+          new_topic = row[i] & mask;
+        } else {
+          sample -= topic_term_mass;
+          if (sample < topic_beta_mass) {
+            sample /= beta;
+            for (dense = 0; dense < nonzero; ++dense) {
+              int k = li[dense];
+              sample -= lc[k] / (tpt[k] + beta_sum);
+              if (sample <= 0.0) {
+                new_topic = k;
+                break;
+              }
+            }
+          } else {
+            sample -= topic_beta_mass;
+            sample /= beta;
+            new_topic = 0;
+            sample -= alpha[new_topic] / (tpt[new_topic] + beta_sum);
+            while (sample > 0.0 && new_topic < K - 1) {
+              new_topic++;
+              sample -= alpha[new_topic] / (tpt[new_topic] + beta_sum);
+            }
+          }
+        }
+        if (new_topic == -1) new_topic = K - 1;
+        topics[p] = new_topic;
+        topic_beta_mass -= beta * lc[new_topic] / (tpt[new_topic] + beta_sum);
+        lc[new_topic]++;
+        if (lc[new_topic] == 1) {
+          dense = nonzero;
+          while (dense > 0 && li[dense - 1] > new_topic) {
+            li[dense] = li[dense - 1];
+            dense--;
+          }
+          li[dense] = new_topic;
+          nonzero++;
+        }
+        cached[new_topic] = (alpha[new_topic] + lc[new_topic]) / (tpt[new_topic] + beta_sum);
+        topic_beta_mass += beta * lc[new_topic] / (tpt[new_topic] + beta_sum);
+      }
+      if (it > burn_in && (it - burn_in) % thin == 0) {
+        for (int k = 0; k < K; ++k) {
+          result[k] += alpha[k] + lc[k];
+          sum += alpha[k] + lc[k];
+        }
+      }
+    }
+    for (dense = 0; dense < nonzero; ++dense) {
+      int k = li[dense];
+      cached[k] = alpha[k] / (tpt[k] + beta_sum);
+    }
+    if (sum == 0.0) {
+      for (int k = 0; k < K; ++k) {
+        result[k] = alpha[k] + lc[k];
+        sum += result[k];
+      }
+    }
+    for (int k = 0; k < K; ++k) result[k] /= sum;
+    free(topics);
+  }
+  free(cached); free(scores); free(lc); free(li);
+}

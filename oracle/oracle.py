@@ -1,0 +1,269 @@
+"""ctypes binding of the CPU oracle (oracle/lda_oracle.c).
+
+TEST INFRASTRUCTURE ONLY: imported by tests/, __graft_entry__.smoke() and the
+cpu_baseline leg of bench.py — never by the product package.  See
+oracle/lda_oracle.h for what each restatement follows and for its parity
+status (cpu_exact: bit-exact definition of the GPU sampler, pinned by
+tests/golden/; cpu_mallet: Mallet 2.0.7 restatement, parity unpinned against
+Mallet itself because Mallet cannot be built or run in this image).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB_PATH = os.path.join(_HERE, "lib", "liblda_oracle.so")
+_lib = None
+
+_i32p = np.ctypeslib.ndpointer(dtype=np.int32, flags="C_CONTIGUOUS")
+_i64p = np.ctypeslib.ndpointer(dtype=np.int64, flags="C_CONTIGUOUS")
+_f64p = np.ctypeslib.ndpointer(dtype=np.float64, flags="C_CONTIGUOUS")
+
+
+def build() -> str:
+    """Compile the oracle with its Makefile (gcc)."""
+    subprocess.run(["make", "-s", "-C", _HERE], check=True)
+    return _LIB_PATH
+
+
+def lib():
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(_LIB_PATH):
+        build()
+    L = C.CDLL(_LIB_PATH)
+    L.orc_philox4x32_10.argtypes = [C.POINTER(C.c_uint32), C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]
+    L.orc_draw.restype = C.c_uint32
+    L.orc_draw.argtypes = [C.c_uint64, C.c_uint64, C.c_uint32, C.c_uint32]
+    L.orc_u01.restype = C.c_float
+    L.orc_u01.argtypes = [C.c_uint32]
+    L.orc_jrandom_seed.argtypes = [C.c_void_p, C.c_int64]
+    L.orc_jrandom_next_int.restype = C.c_int32
+    L.orc_jrandom_next_int.argtypes = [C.c_void_p]
+    L.orc_jrandom_next_int_n.restype = C.c_int32
+    L.orc_jrandom_next_int_n.argtypes = [C.c_void_p, C.c_int32]
+    L.orc_jrandom_next_double.restype = C.c_double
+    L.orc_jrandom_next_double.argtypes = [C.c_void_p]
+    L.orc_log_gamma_stirling.restype = C.c_double
+    L.orc_log_gamma_stirling.argtypes = [C.c_double]
+
+    L.orc_exact_create.restype = C.c_void_p
+    L.orc_exact_create.argtypes = [C.c_int32, C.c_int32, C.c_int64, _i64p, _i32p, C.c_void_p,
+                                   _f64p, C.c_double, C.c_uint64, C.c_int64]
+    L.orc_exact_destroy.argtypes = [C.c_void_p]
+    L.orc_exact_kpad.restype = C.c_int32
+    L.orc_exact_kpad.argtypes = [C.c_void_p]
+    L.orc_exact_sample.argtypes = [C.c_void_p, C.c_int]
+    L.orc_exact_delta.restype = C.POINTER(C.c_int32)
+    L.orc_exact_delta.argtypes = [C.c_void_p]
+    L.orc_exact_apply.argtypes = [C.c_void_p]
+    L.orc_exact_set_alpha_beta.argtypes = [C.c_void_p, _f64p, C.c_double]
+    L.orc_exact_set_sweep.argtypes = [C.c_void_p, C.c_uint32]
+    L.orc_exact_get_sweep.restype = C.c_uint32
+    L.orc_exact_get_sweep.argtypes = [C.c_void_p]
+    L.orc_exact_get_z.argtypes = [C.c_void_p, _i32p]
+    L.orc_exact_get_counts.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
+    L.orc_exact_log_likelihood.restype = C.c_double
+    L.orc_exact_log_likelihood.argtypes = [C.c_void_p]
+    L.orc_exact_infer.argtypes = [C.c_void_p, C.c_int64, _i64p, _i32p, C.c_int32, C.c_int32,
+                                  C.c_int32, C.c_uint64, _f64p]
+
+    L.orc_mallet_create.restype = C.c_void_p
+    L.orc_mallet_create.argtypes = [C.c_int32, C.c_double, C.c_double, C.c_int32, C.c_int64,
+                                    _i64p, _i32p, C.c_int64, C.c_int32]
+    L.orc_mallet_destroy.argtypes = [C.c_void_p]
+    L.orc_mallet_estimate.argtypes = [C.c_void_p, C.c_int32]
+    L.orc_mallet_log_likelihood.restype = C.c_double
+    L.orc_mallet_log_likelihood.argtypes = [C.c_void_p]
+    L.orc_mallet_get_z.argtypes = [C.c_void_p, _i32p]
+    L.orc_mallet_get_counts.argtypes = [C.c_void_p, _i32p, _i32p]
+    L.orc_mallet_infer.argtypes = [C.c_void_p, C.c_int64, _i64p, _i32p, C.c_int32, C.c_int32,
+                                   C.c_int32, C.c_int64, _f64p]
+    L.orc_doc_completion_loglik.restype = C.c_double
+    L.orc_doc_completion_loglik.argtypes = [C.c_int32, C.c_int32, _i32p, _i32p, C.c_double,
+                                            C.c_int64, _f64p, _i64p, _i32p]
+    _lib = L
+    return L
+
+
+# ---------------------------------------------------------------- primitives
+def philox4x32_10(ctr, key):
+    L = lib()
+    c = (C.c_uint32 * 4)(*ctr)
+    k = (C.c_uint32 * 2)(*key)
+    o = (C.c_uint32 * 4)()
+    L.orc_philox4x32_10(c, k, o)
+    return [int(x) for x in o]
+
+
+def draw(seed: int, gtok: int, c2: int, c3: int) -> int:
+    return int(lib().orc_draw(seed, gtok, c2, c3))
+
+
+def u01(x: int) -> float:
+    return float(lib().orc_u01(x))
+
+
+def log_gamma_stirling(z: float) -> float:
+    return float(lib().orc_log_gamma_stirling(z))
+
+
+class JavaRandom:
+    """java.util.Random (the base of cc.mallet.util.Randoms)."""
+
+    def __init__(self, seed: int):
+        self._state = (C.c_uint64 * 1)()
+        lib().orc_jrandom_seed(self._state, seed)
+
+    def nextInt(self, n: int | None = None) -> int:
+        if n is None:
+            return int(lib().orc_jrandom_next_int(self._state))
+        return int(lib().orc_jrandom_next_int_n(self._state, n))
+
+    def nextDouble(self) -> float:
+        return float(lib().orc_jrandom_next_double(self._state))
+
+
+# ---------------------------------------------------------------- cpu_exact
+class ExactSampler:
+    """cpu_exact: the bit-exact definition of the GPU sampler (one shard)."""
+
+    def __init__(self, K, V, doc_off, words, alpha, beta, seed, z_init=None, token_base=0):
+        self.K, self.V = int(K), int(V)
+        self.doc_off = np.ascontiguousarray(doc_off, dtype=np.int64)
+        self.words = np.ascontiguousarray(words, dtype=np.int32)
+        self.D = len(self.doc_off) - 1
+        self.N = int(self.doc_off[-1] - self.doc_off[0])
+        alpha = np.ascontiguousarray(np.broadcast_to(np.asarray(alpha, dtype=np.float64), (self.K,)))
+        zi = None
+        if z_init is not None:
+            self._zi = np.ascontiguousarray(z_init, dtype=np.int32)
+            zi = self._zi.ctypes.data
+        self._h = lib().orc_exact_create(self.K, self.V, self.D, self.doc_off, self.words, zi,
+                                         alpha, float(beta), int(seed) & (2**64 - 1), int(token_base))
+        self.Kp = int(lib().orc_exact_kpad(self._h))
+        self._pending = True      # create leaves the shard's counts as the pending delta
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h:
+            lib().orc_exact_destroy(h)
+            self._h = None
+
+    def delta(self) -> np.ndarray:
+        """View of the pending delta buffer (nw delta [V*Kp] then nwsum delta [Kp])."""
+        p = lib().orc_exact_delta(self._h)
+        n = self.V * self.Kp + self.Kp
+        return np.ctypeslib.as_array(p, shape=(n,))
+
+    def sample(self, frozen=False):
+        if self._pending:
+            raise RuntimeError("sample with a pending delta: apply first (as lda_sample)")
+        lib().orc_exact_sample(self._h, 1 if frozen else 0)
+        self._pending = not frozen
+
+    def apply(self):
+        lib().orc_exact_apply(self._h)
+        self._pending = False
+
+    def sweep(self, n=1):
+        """Same contract as lda_sweep: apply a pending delta, then n x (sample + apply)."""
+        if self._pending:
+            self.apply()
+        for _ in range(n):
+            self.sample()
+            self.apply()
+
+    @property
+    def sweep_index(self) -> int:
+        return int(lib().orc_exact_get_sweep(self._h))
+
+    def set_alpha_beta(self, alpha, beta):
+        a = np.ascontiguousarray(np.broadcast_to(np.asarray(alpha, dtype=np.float64), (self.K,)))
+        lib().orc_exact_set_alpha_beta(self._h, a, float(beta))
+
+    def z(self) -> np.ndarray:
+        out = np.empty(self.N, dtype=np.int32)
+        lib().orc_exact_get_z(self._h, out)
+        return out
+
+    def counts(self, with_nd=False):
+        nw = np.empty((self.V, self.K), dtype=np.int32)
+        nwsum = np.empty(self.K, dtype=np.int32)
+        nd = np.empty((self.D, self.K), dtype=np.int32) if with_nd else None
+        ndsum = np.empty(self.D, dtype=np.int32)
+        lib().orc_exact_get_counts(self._h, nw.ctypes.data, nwsum.ctypes.data,
+                                   nd.ctypes.data if with_nd else None, ndsum.ctypes.data)
+        return nw, nwsum, nd, ndsum
+
+    def log_likelihood(self) -> float:
+        return float(lib().orc_exact_log_likelihood(self._h))
+
+    def infer(self, doc_off, words, n_iter=100, burn_in=10, thin=10, seed=0):
+        doc_off = np.ascontiguousarray(doc_off, dtype=np.int64)
+        words = np.ascontiguousarray(words, dtype=np.int32)
+        Dh = len(doc_off) - 1
+        theta = np.zeros((Dh, self.K), dtype=np.float64)
+        lib().orc_exact_infer(self._h, Dh, doc_off, words, n_iter, burn_in, thin, int(seed), theta)
+        return theta
+
+
+# ---------------------------------------------------------------- cpu_mallet
+class MalletModel:
+    """cpu_mallet: Mallet 2.0.7 ParallelTopicModel restatement (parity unpinned)."""
+
+    def __init__(self, K, alpha_sum, beta, V, doc_off, words, seed, num_threads=1):
+        self.K, self.V = int(K), int(V)
+        self.doc_off = np.ascontiguousarray(doc_off, dtype=np.int64)
+        self.words = np.ascontiguousarray(words, dtype=np.int32)
+        self.D = len(self.doc_off) - 1
+        self.N = int(self.doc_off[-1] - self.doc_off[0])
+        self.alpha_sum, self.beta = float(alpha_sum), float(beta)
+        self._h = lib().orc_mallet_create(self.K, self.alpha_sum, self.beta, self.V, self.D,
+                                          self.doc_off, self.words, int(seed), int(num_threads))
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h:
+            lib().orc_mallet_destroy(h)
+            self._h = None
+
+    def estimate(self, n_iter):
+        lib().orc_mallet_estimate(self._h, int(n_iter))
+
+    def log_likelihood(self) -> float:
+        return float(lib().orc_mallet_log_likelihood(self._h))
+
+    def z(self):
+        out = np.empty(self.N, dtype=np.int32)
+        lib().orc_mallet_get_z(self._h, out)
+        return out
+
+    def counts(self):
+        nw = np.empty((self.V, self.K), dtype=np.int32)
+        nwsum = np.empty(self.K, dtype=np.int32)
+        lib().orc_mallet_get_counts(self._h, nw, nwsum)
+        return nw, nwsum
+
+    def infer(self, doc_off, words, n_iter=100, burn_in=10, thin=10, seed=0):
+        doc_off = np.ascontiguousarray(doc_off, dtype=np.int64)
+        words = np.ascontiguousarray(words, dtype=np.int32)
+        Dh = len(doc_off) - 1
+        theta = np.zeros((Dh, self.K), dtype=np.float64)
+        lib().orc_mallet_infer(self._h, Dh, doc_off, words, n_iter, burn_in, thin, int(seed), theta)
+        return theta
+
+
+def doc_completion_loglik(K, V, nw, nwsum, beta, theta, doc_off, words) -> float:
+    nw = np.ascontiguousarray(nw, dtype=np.int32)
+    nwsum = np.ascontiguousarray(nwsum, dtype=np.int32)
+    theta = np.ascontiguousarray(theta, dtype=np.float64)
+    doc_off = np.ascontiguousarray(doc_off, dtype=np.int64)
+    words = np.ascontiguousarray(words, dtype=np.int32)
+    return float(lib().orc_doc_completion_loglik(K, V, nw, nwsum, float(beta), len(doc_off) - 1,
+                                                 theta, doc_off, words))
