@@ -94,6 +94,15 @@ def load(path: str = LIB_PATH):
         raise ImportError(
             f"{path} not found: build the HIP extension first "
             "(python -c 'import __graft_entry__ as g; g.build()')")
+    # One HIP runtime per process: PyTorch-ROCm ships its own libamdhip64
+    # (soname libamdhip64.so.7, loaded by path through its $ORIGIN rpath).
+    # Importing torch first makes our NEEDED libamdhip64.so.7 resolve to that
+    # already-loaded copy; loading /opt/rocm's copy first would leave torch's
+    # runtime without devices ("No HIP GPUs are available").
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     L = C.CDLL(path)
     for name, (res, args) in SIGNATURES.items():
         fn = getattr(L, name)
