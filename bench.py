@@ -43,6 +43,21 @@ def bytes_per_token(K: int) -> int:
     return 4 * K + 16
 
 
+def pmc_traffic(K: int, tokens_per_launch: int, kernel_prefix: str):
+    """HBM bytes per sampler launch from the newest committed rocprofv3 PMC
+    summary (profiles/rNN/traffic_k{K}.json, written from separate
+    FETCH_SIZE / WRITE_SIZE passes over this same command by
+    tools/profile_round*.sh).  None when no summary matches this workload."""
+    import glob
+    paths = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", f"traffic_k{K}.json")))
+    for path in reversed(paths):
+        with open(path) as f:
+            t = json.load(f)
+        if t.get("tokens_per_launch") == tokens_per_launch and t.get("kernel", "").startswith(kernel_prefix):
+            return t["hbm_bytes_per_launch"] / 1e9, os.path.relpath(path, ROOT)
+    return None, None
+
+
 def cpu_baseline(corpus, K, alpha_sum, beta, budget_s=15.0, threads=4):
     """cpu_mallet (oracle/, the Mallet 2.0.7 SparseLDA restatement) timed on a
     bounded sample of the same workload on this host's cores."""
@@ -97,6 +112,7 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
 
     from ldagibbssampling_amd.corpus import synthetic_lda_torch
+    from ldagibbssampling_amd.distributed import ADLDATrainer
     from ldagibbssampling_amd.sampler import GibbsSampler
 
     cfg = CONFIGS[args.config]
@@ -112,29 +128,22 @@ def main():
                            seed=1, device=local_rank, token_base=rank * n_local)
     stream = torch.cuda.current_stream()
     sampler.set_stream(stream.cuda_stream)
-    delta = sampler.delta_tensor() if world > 1 else None
+    # AD-LDA: sample; all-reduce (SUM) of every rank's int32 nw/nwsum delta; apply
+    trainer = ADLDATrainer(sampler, sync_before_reduce=False)
+    trainer.init_counts()
 
     def step():
-        sampler.sample()
-        if world > 1:
-            dist.all_reduce(delta)           # AD-LDA: sum of every rank's nw/nwsum delta
-        sampler.apply()
+        trainer.sweep(1)
 
-    # initial global counts
-    if world > 1:
-        dist.all_reduce(delta)
-    sampler.apply()
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    kernel_ms = []
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
-        kernel_ms.append(None)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -144,11 +153,8 @@ def main():
     # a separate, identical pass so that the timed loop carries no host syncs.
     ks = []
     for _ in range(3):
-        sampler.sample()
+        step()
         ks.append(sampler.last_sample_ms())
-        if world > 1:
-            dist.all_reduce(delta)
-        sampler.apply()
     torch.cuda.synchronize()
     kern_ms = float(np.mean(ks))
 
@@ -158,11 +164,12 @@ def main():
     elapsed = float(t.item())
     total_tokens = n_local * world * args.steps
     value = total_tokens / elapsed
-    ll = sampler.log_likelihood_parts()
+    ll = trainer.log_likelihood()
 
     if rank == 0:
         bpt = bytes_per_token(K)
         achieved = n_local * bpt / (kern_ms * 1e-3) / 1e9      # GB/s, algorithmic
+        traffic_gb, traffic_src = pmc_traffic(K, n_local, "k_sample<")
         result = {
             "metric": "Gibbs tokens sampled/sec at K=512",
             "value": value,
@@ -193,11 +200,14 @@ def main():
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBS,
-                "traffic": None,
+                "traffic": traffic_gb,
+                "traffic_unit": "GB per launch (rocprofv3 PMC, gfx950-corrected)",
+                "traffic_source": traffic_src,
+                "algorithmic_gb_per_launch": n_local * bpt / 1e9,
                 "kernel": f"k_sample<C={sampler.Kp // 64}> avg {kern_ms:.3f} ms/launch over "
                           f"{n_local} tokens, B(K)={bpt} B/token",
             },
-            "ll_per_token_rank0": (ll[0] + ll[1]) / n_local if world == 1 else None,
+            "ll_per_token": ll / (n_local * world),
             "corpus_gen_s": t_gen,
         }
         if world == 1 and not args.no_cpu_baseline:

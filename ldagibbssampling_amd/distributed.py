@@ -1,0 +1,102 @@
+"""AD-LDA across GPUs: one process per GPU, documents sharded, nw replicated.
+
+The reference's only parallelism is Mallet's document-parallel worker
+threads (setNumThreads(4) at src/cmu_ron/TrainAndPredict.java:164 and
+src/cmu/TrainAndPredict.java:262): contiguous doc blocks per thread, and after
+every sweep the per-thread counts are summed into the global typeTopicCounts
+/ tokensPerTopic and copied back (ParallelTopicModel.sumTypeTopicCounts).
+Here that exchange is ONE collective per sweep: an in-place SUM all-reduce of
+the int32 delta buffer [V*Kp nw delta | Kp nwsum delta] over the process group
+(RCCL over xGMI for the "nccl" backend; gloo for CPU tests).  Integer sums
+commute and every draw is keyed by the GLOBAL token index, so the result is
+bit-identical for any number of ranks (tests/test_distributed.py).
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+import numpy as np
+
+
+@dataclass
+class Shard:
+    rank: int
+    world: int
+    doc_begin: int
+    doc_end: int
+    doc_off: np.ndarray   # int64 [docs+1], absolute offsets into the corpus stream
+    words: np.ndarray     # int32 [tokens]
+    token_base: int       # global index of the shard's first token
+
+
+def shard_corpus(doc_off, words, world: int, rank: int) -> Shard:
+    """Contiguous document ranges balanced by token count (the GPU analogue of
+    Mallet's docsPerThread blocks, balanced on tokens instead of documents)."""
+    doc_off = np.asarray(doc_off, dtype=np.int64)
+    D = len(doc_off) - 1
+    total = int(doc_off[-1] - doc_off[0])
+    targets = [doc_off[0] + (total * r) // world for r in range(world + 1)]
+    cuts = [0] + [int(np.searchsorted(doc_off, t, side="left")) for t in targets[1:-1]] + [D]
+    cuts = [min(max(c, 0), D) for c in cuts]
+    for i in range(1, len(cuts)):
+        cuts[i] = max(cuts[i], cuts[i - 1])
+    a, b = cuts[rank], cuts[rank + 1]
+    off = doc_off[a:b + 1]
+    return Shard(rank, world, a, b, off, np.asarray(words[off[0]:off[-1]], dtype=np.int32),
+                 int(off[0] - doc_off[0]))
+
+
+class ADLDATrainer:
+    """Drives one rank's sampler engine through AD-LDA sweeps.
+
+    engine: sample(), apply(), delta_tensor() -> torch int32 tensor aliasing
+    the engine's pending delta, synchronize(), log_likelihood_parts().
+    GibbsSampler (GPU) is the product engine; tests inject a CPU one.
+    """
+
+    def __init__(self, engine, group=None, sync_before_reduce: bool = True):
+        """sync_before_reduce=False when the engine already launches on the
+        stream the collective runs behind (GibbsSampler.set_stream(torch's
+        current stream)): then no host synchronisation per sweep is needed."""
+        import torch.distributed as dist
+
+        self.engine = engine
+        self.sync_before_reduce = sync_before_reduce
+        self.group = group
+        self.dist = dist
+        self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        self._delta = engine.delta_tensor() if self.world > 1 else None
+        self._initialised = False
+
+    def _reduce(self):
+        if self.world > 1:
+            if self.sync_before_reduce:
+                self.engine.synchronize()
+            self.dist.all_reduce(self._delta, op=self.dist.ReduceOp.SUM, group=self.group)
+
+    def init_counts(self):
+        """Global nw/nwsum from every rank's local counts (addInstances)."""
+        self._reduce()
+        self.engine.apply()
+        self._initialised = True
+
+    def sweep(self, n: int = 1):
+        if not self._initialised:
+            self.init_counts()
+        for _ in range(n):
+            self.engine.sample()
+            self._reduce()
+            self.engine.apply()
+
+    def log_likelihood(self) -> float:
+        """modelLogLikelihood of the whole corpus: doc parts summed over ranks,
+        the word part (global counts) taken once."""
+        import torch
+
+        doc, word = self.engine.log_likelihood_parts()
+        if self.world > 1:
+            dev = self._delta.device if self.dist.get_backend(self.group) == "nccl" else "cpu"
+            t = torch.tensor([doc], dtype=torch.float64, device=dev)
+            self.dist.all_reduce(t, op=self.dist.ReduceOp.SUM, group=self.group)
+            doc = float(t.item())
+        return doc + word

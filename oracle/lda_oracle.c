@@ -352,10 +352,13 @@ void orc_exact_get_counts(const orc_exact* s, int32_t* nw, int32_t* nwsum, int32
     for (int64_t d = 0; d < s->D; ++d) ndsum[d] = (int32_t)(s->doc_off[d + 1] - s->doc_off[d]);
 }
 
-/* ParallelTopicModel.modelLogLikelihood() [M], restated over dense counts. */
-static double mallet_ll_dense(int K, int V, int Kstride, const double* alpha, double beta,
-                              int64_t D, const int64_t* doc_off, const int32_t* z,
-                              const int32_t* nw, const int32_t* nwsum) {
+/* ParallelTopicModel.modelLogLikelihood() [M], restated over dense counts,
+ * split into the document part (this shard's docs, incl. D*logG(alphaSum))
+ * and the word part (global counts). */
+static void mallet_ll_dense_parts(int K, int V, int Kstride, const double* alpha, double beta,
+                                  int64_t D, const int64_t* doc_off, const int32_t* z,
+                                  const int32_t* nw, const int32_t* nwsum, double* doc_part,
+                                  double* word_part) {
   double alpha_sum = 0.0;
   for (int k = 0; k < K; ++k) alpha_sum += alpha[k];
   double ll = 0.0;
@@ -370,6 +373,8 @@ static double mallet_ll_dense(int K, int V, int Kstride, const double* alpha, do
     memset(counts, 0, sizeof(int32_t) * K);
   }
   ll += (double)D * orc_log_gamma_stirling(alpha_sum);
+  *doc_part = ll;
+  ll = 0.0;
   int64_t nonzero = 0;
   for (int w = 0; w < V; ++w)
     for (int k = 0; k < K; ++k) {
@@ -382,9 +387,22 @@ static double mallet_ll_dense(int K, int V, int Kstride, const double* alpha, do
   for (int k = 0; k < K; ++k) ll -= orc_log_gamma_stirling(beta * V + nwsum[k]);
   ll += orc_log_gamma_stirling(beta * V) * K;
   ll -= orc_log_gamma_stirling(beta) * (double)nonzero;
+  *word_part = ll;
   free(topic_lg);
   free(counts);
-  return ll;
+}
+
+static double mallet_ll_dense(int K, int V, int Kstride, const double* alpha, double beta,
+                              int64_t D, const int64_t* doc_off, const int32_t* z,
+                              const int32_t* nw, const int32_t* nwsum) {
+  double a, b;
+  mallet_ll_dense_parts(K, V, Kstride, alpha, beta, D, doc_off, z, nw, nwsum, &a, &b);
+  return a + b;
+}
+
+void orc_exact_log_likelihood_parts(const orc_exact* s, double* doc_part, double* word_part) {
+  mallet_ll_dense_parts(s->K, s->V, s->Kp, s->alpha, s->beta, s->D, s->doc_off, s->z, s->nw,
+                        s->nwsum, doc_part, word_part);
 }
 
 double orc_exact_log_likelihood(const orc_exact* s) {

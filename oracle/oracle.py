@@ -70,6 +70,8 @@ def lib():
     L.orc_exact_get_counts.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
     L.orc_exact_log_likelihood.restype = C.c_double
     L.orc_exact_log_likelihood.argtypes = [C.c_void_p]
+    L.orc_exact_log_likelihood_parts.argtypes = [C.c_void_p, C.POINTER(C.c_double),
+                                                 C.POINTER(C.c_double)]
     L.orc_exact_infer.argtypes = [C.c_void_p, C.c_int64, _i64p, _i32p, C.c_int32, C.c_int32,
                                   C.c_int32, C.c_uint64, _f64p]
 
@@ -203,6 +205,11 @@ class ExactSampler:
 
     def log_likelihood(self) -> float:
         return float(lib().orc_exact_log_likelihood(self._h))
+
+    def log_likelihood_parts(self):
+        a, b = C.c_double(), C.c_double()
+        lib().orc_exact_log_likelihood_parts(self._h, C.byref(a), C.byref(b))
+        return a.value, b.value
 
     def infer(self, doc_off, words, n_iter=100, burn_in=10, thin=10, seed=0):
         doc_off = np.ascontiguousarray(doc_off, dtype=np.int64)

@@ -1,0 +1,103 @@
+"""Multi-rank AD-LDA on CPU (gloo, world_size 2 and 3): the product driver
+(ldagibbssampling_amd.distributed) with the cpu_exact oracle injected as the
+engine must reproduce the single-process run bit for bit."""
+import os
+import sys
+import tempfile
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+K, SEED, SWEEPS = 32, 17, 3
+
+
+class OracleEngine:
+    """cpu_exact behind the engine interface ADLDATrainer drives (tests only)."""
+
+    def __init__(self, sampler):
+        self.s = sampler
+
+    def sample(self):
+        self.s.sample()
+
+    def apply(self):
+        self.s.apply()
+
+    def synchronize(self):
+        pass
+
+    def delta_tensor(self):
+        return torch.from_numpy(self.s.delta())
+
+    def log_likelihood_parts(self):
+        return self.s.log_likelihood_parts()
+
+
+def _corpus():
+    from ldagibbssampling_amd.corpus import synthetic_lda
+    return synthetic_lda(num_docs=70, num_types=300, num_topics=K, doc_len=None, mean_len=40,
+                         min_len=0, max_len=150, seed=13)
+
+
+def _worker(rank, world, port, outdir):
+    sys.path.insert(0, ROOT)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from oracle import oracle as O
+    from ldagibbssampling_amd.distributed import ADLDATrainer, shard_corpus
+    c = _corpus()
+    sh = shard_corpus(c.doc_off, c.words, world, rank)
+    o = O.ExactSampler(K, c.num_types, sh.doc_off, sh.words, 0.1, 0.01, SEED, token_base=sh.token_base)
+    tr = ADLDATrainer(OracleEngine(o))
+    tr.sweep(SWEEPS)
+    ll = tr.log_likelihood()
+    nw, nwsum, _, _ = o.counts()
+    np.savez(os.path.join(outdir, f"r{rank}.npz"), z=o.z(), nw=nw, nwsum=nwsum, ll=ll,
+             docs=np.array([sh.doc_begin, sh.doc_end]))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def _free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_gloo_adlda_matches_single(oracle, world):
+    with tempfile.TemporaryDirectory() as d:
+        mp.start_processes(_worker, args=(world, _free_port(), d), nprocs=world, start_method="spawn")
+        res = [np.load(os.path.join(d, f"r{r}.npz")) for r in range(world)]
+    c = _corpus()
+    single = oracle.ExactSampler(K, c.num_types, c.doc_off, c.words, 0.1, 0.01, SEED)
+    single.sweep(SWEEPS)
+    np.testing.assert_array_equal(np.concatenate([r["z"] for r in res]), single.z())
+    nw, nwsum, _, _ = single.counts()
+    for r in res:
+        np.testing.assert_array_equal(r["nw"], nw)       # every replica identical
+        np.testing.assert_array_equal(r["nwsum"], nwsum)
+        assert abs(float(r["ll"]) - single.log_likelihood()) < 1e-9 * abs(single.log_likelihood())
+    spans = [tuple(r["docs"]) for r in res]
+    assert spans[0][0] == 0 and spans[-1][1] == c.num_docs
+    assert all(a[1] == b[0] for a, b in zip(spans, spans[1:]))
+
+
+def test_shard_balanced_by_tokens():
+    from ldagibbssampling_amd.distributed import shard_corpus
+    c = _corpus()
+    world = 4
+    shards = [shard_corpus(c.doc_off, c.words, world, r) for r in range(world)]
+    assert shards[0].doc_begin == 0 and shards[-1].doc_end == c.num_docs
+    toks = [len(s.words) for s in shards]
+    assert sum(toks) == c.num_tokens
+    assert max(toks) - min(toks) <= 200                    # within ~one doc
+    assert [s.token_base for s in shards] == list(np.cumsum([0] + toks[:-1]))

@@ -1,0 +1,65 @@
+"""Two ranks on one MI355X (gloo over device tensors): the product engine
+(GibbsSampler) + ADLDATrainer must equal the single-process GPU run and the
+oracle bit for bit.  (RCCL needs one GPU per rank; the 8-GPU RCCL path is
+exercised by bench.py under torch.distributed.run.)"""
+import os
+import sys
+import tempfile
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+K, SEED, SWEEPS = 128, 23, 4
+
+
+def _corpus():
+    from ldagibbssampling_amd.corpus import synthetic_lda
+    return synthetic_lda(num_docs=160, num_types=900, num_topics=K, doc_len=None, mean_len=70,
+                         min_len=0, max_len=300, seed=31)
+
+
+def _worker(rank, world, port, outdir):
+    sys.path.insert(0, ROOT)
+    import torch
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from ldagibbssampling_amd.distributed import ADLDATrainer, shard_corpus
+    from ldagibbssampling_amd.sampler import GibbsSampler
+    c = _corpus()
+    sh = shard_corpus(c.doc_off, c.words, world, rank)
+    g = GibbsSampler(K, c.num_types, sh.doc_off, sh.words, 0.1, 0.01, seed=SEED,
+                     token_base=sh.token_base)
+    tr = ADLDATrainer(g)
+    tr.sweep(SWEEPS)
+    ll = tr.log_likelihood()
+    nw, nwsum, _, _ = g.counts()
+    np.savez(os.path.join(outdir, f"r{rank}.npz"), z=g.z(), nw=nw, nwsum=nwsum, ll=ll)
+    g.close()
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_two_ranks_one_gpu(oracle):
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    world = 2
+    with tempfile.TemporaryDirectory() as d:
+        mp.start_processes(_worker, args=(world, port, d), nprocs=world, start_method="spawn")
+        res = [np.load(os.path.join(d, f"r{r}.npz")) for r in range(world)]
+    c = _corpus()
+    o = oracle.ExactSampler(K, c.num_types, c.doc_off, c.words, 0.1, 0.01, SEED)
+    o.sweep(SWEEPS)
+    np.testing.assert_array_equal(np.concatenate([r["z"] for r in res]), o.z())
+    nw, nwsum, _, _ = o.counts()
+    for r in res:
+        np.testing.assert_array_equal(r["nw"], nw)
+        np.testing.assert_array_equal(r["nwsum"], nwsum)
+        assert abs(float(r["ll"]) - o.log_likelihood()) < 1e-9 * abs(o.log_likelihood())

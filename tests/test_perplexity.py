@@ -1,0 +1,58 @@
+"""Held-out perplexity: the GPU sampler vs the Mallet 2.0.7 restatement
+(cpu_mallet), 1000 sweeps, seeds {1, 2, 3}, optimizeInterval = 0 on both.
+
+Estimator (the same for both trained states): document completion.  10% of
+the documents are held out; each held-out document's first floor(L/2) tokens
+are observed, theta is inferred against the frozen model with the GPU
+TopicInferencer analogue (lda_infer: 100 iterations, burn-in 10, thinning 10
+— the reference's getSampledDistribution(inst, 100, 10, 10),
+src/cmu_ron/TrainAndPredict.java:144), and the other half is scored:
+perplexity = exp(-sum log sum_k theta_dk phi_kw / N_scored).
+The Mallet state is evaluated by loading its z into a GPU context.
+
+Tolerance: |mean_gpu - mean_mallet| <= 1% of mean_mallet (BASELINE.json
+north_star).  Parity with Mallet itself is unpinned (Mallet cannot run in
+this image); cpu_mallet is its restatement.
+"""
+import numpy as np
+import pytest
+
+pytestmark = [pytest.mark.gpu, pytest.mark.slow]
+
+
+def _perplexity(sampler, held_obs, held_sc, oracle):
+    theta = sampler.infer(held_obs.doc_off, held_obs.words, n_iter=100, burn_in=10, thin=10, seed=7)
+    nw, nwsum, _, _ = sampler.counts()
+    ll = oracle.doc_completion_loglik(sampler.K, sampler.V, nw, nwsum, sampler.beta, theta,
+                                      held_sc.doc_off, held_sc.words)
+    return float(np.exp(-ll / held_sc.num_tokens))
+
+
+@pytest.mark.parametrize("K,alpha_sum,beta", [(20, 10.0, 0.01), (100, 10.0, 0.01)])
+def test_heldout_perplexity_within_1pct(oracle, K, alpha_sum, beta):
+    from ldagibbssampling_amd.corpus import synthetic_lda, document_completion_split
+    from ldagibbssampling_amd.sampler import GibbsSampler
+    c = synthetic_lda(num_docs=2200, num_types=3000, num_topics=K, doc_len=None, mean_len=80,
+                      min_len=10, max_len=300, seed=20261015, k_true=min(K, 50))
+    rng = np.random.default_rng(0)
+    perm = rng.permutation(c.num_docs)
+    n_held = c.num_docs // 10
+    train = c.subset(np.sort(perm[n_held:]))
+    held_obs, held_sc = document_completion_split(c.subset(np.sort(perm[:n_held])))
+    alpha = np.full(K, alpha_sum / K)
+    pg, pm = [], []
+    for seed in (1, 2, 3):
+        g = GibbsSampler(K, c.num_types, train.doc_off, train.words, alpha, beta, seed=seed)
+        g.sweep(1000)
+        pg.append(_perplexity(g, held_obs, held_sc, oracle))
+        m = oracle.MalletModel(K, alpha_sum, beta, c.num_types, train.doc_off, train.words,
+                               seed=seed, num_threads=4)
+        m.estimate(1000)
+        gm = GibbsSampler(K, c.num_types, train.doc_off, train.words, alpha, beta, seed=seed,
+                          z_init=m.z())
+        gm.sweep(0)
+        pm.append(_perplexity(gm, held_obs, held_sc, oracle))
+    mg, mm = float(np.mean(pg)), float(np.mean(pm))
+    print(f"K={K}: gpu {pg} mean {mg:.3f} | cpu_mallet {pm} mean {mm:.3f} | "
+          f"rel diff {(mg - mm) / mm:+.4%}")
+    assert abs(mg - mm) <= 0.01 * mm

@@ -1,0 +1,82 @@
+#!/usr/bin/env python3
+"""Condense rocprofv3 CSV output into small per-kernel summaries.
+
+  summarize_prof.py <prof_dir> <out.json>
+
+Reads every *_kernel_stats.csv, *_kernel_trace.csv and
+*_counter_collection.csv under prof_dir and writes, per kernel name:
+  - dispatch count, average / min / max duration (kernel trace),
+  - per counter: number of dispatches and the average value per dispatch.
+HBM traffic per dispatch (MI355X_MICROARCH.md §HBM, gfx950 corrections):
+  FETCH_SIZE and WRITE_SIZE are in KiB; FETCH_SIZE reads half the bytes of a
+  16 B/lane coalesced stream, so hbm_bytes = (2*FETCH_SIZE + WRITE_SIZE)*1024
+  for kernels whose reads are 16 B/lane (the sampler's row gather).
+"""
+import csv
+import glob
+import json
+import os
+import sys
+from collections import defaultdict
+
+
+def short(name: str) -> str:
+    name = name.strip('"')
+    if "k_sample" in name:
+        # keep the template arguments
+        i = name.find("k_sample")
+        return name[i:].split("(")[0]
+    for key in ("k_apply", "k_prepare_topics", "k_count", "k_init_z", "k_doc_topics",
+                "k_ll_docs", "k_ll_words", "k_infer_init"):
+        if key in name:
+            return key
+    return name.split("(")[0][:80]
+
+
+def main(prof_dir, out_path):
+    out = {"kernels": {}, "counters": {}}
+    for path in glob.glob(os.path.join(prof_dir, "**", "*_kernel_trace.csv"), recursive=True):
+        agg = defaultdict(list)
+        with open(path) as f:
+            for row in csv.DictReader(f):
+                dur = int(row["End_Timestamp"]) - int(row["Start_Timestamp"])
+                agg[short(row["Kernel_Name"])].append(dur)
+        for k, v in agg.items():
+            v.sort()
+            out["kernels"][k] = {
+                "calls": len(v),
+                "avg_ns": sum(v) / len(v),
+                "min_ns": v[0],
+                "max_ns": v[-1],
+                "median_ns": v[len(v) // 2],
+            }
+    for path in glob.glob(os.path.join(prof_dir, "**", "*_kernel_stats.csv"), recursive=True):
+        with open(path) as f:
+            out["kernel_stats_csv"] = list(csv.DictReader(f))[:40]
+    for path in glob.glob(os.path.join(prof_dir, "**", "*_counter_collection.csv"), recursive=True):
+        agg = defaultdict(lambda: defaultdict(list))
+        with open(path) as f:
+            for row in csv.DictReader(f):
+                agg[short(row["Kernel_Name"])][row["Counter_Name"]].append(
+                    (int(row.get("Dispatch_Id", 0) or 0), float(row["Counter_Value"])))
+        for k, ctrs in agg.items():
+            d = out["counters"].setdefault(k, {})
+            for c, vals in ctrs.items():
+                per_dispatch = defaultdict(float)
+                for disp, v in vals:
+                    per_dispatch[disp] += v
+                xs = list(per_dispatch.values())
+                d[c] = {"dispatches": len(xs), "avg_per_dispatch": sum(xs) / len(xs),
+                        "min": min(xs), "max": max(xs)}
+    for k, ctrs in out["counters"].items():
+        if "FETCH_SIZE" in ctrs and "WRITE_SIZE" in ctrs:
+            ctrs["hbm_bytes_per_dispatch_corrected"] = (
+                2 * ctrs["FETCH_SIZE"]["avg_per_dispatch"] + ctrs["WRITE_SIZE"]["avg_per_dispatch"]) * 1024
+            ctrs["hbm_bytes_per_dispatch_raw"] = (
+                ctrs["FETCH_SIZE"]["avg_per_dispatch"] + ctrs["WRITE_SIZE"]["avg_per_dispatch"]) * 1024
+    with open(out_path, "w") as f:
+        json.dump(out, f, indent=1)
+
+
+if __name__ == "__main__":
+    main(sys.argv[1], sys.argv[2])
