@@ -95,6 +95,9 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="c4", choices=sorted(CONFIGS))
     ap.add_argument("--docs", type=int, default=0, help="override docs per GPU")
+    ap.add_argument("--sampler", default="dense", choices=["dense", "sparse"])
+    ap.add_argument("--burnin", type=int, default=0,
+                    help="extra untimed sweeps before the warm-up (steady-state measurement)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=15.0)
     args = ap.parse_args()
@@ -125,7 +128,8 @@ def main():
     t_gen = time.perf_counter() - t_gen
     n_local = corpus.num_tokens
     sampler = GibbsSampler(K, V, corpus.doc_off, corpus.words, np.full(K, alpha_sum / K), beta,
-                           seed=1, device=local_rank, token_base=rank * n_local)
+                           seed=1, device=local_rank, token_base=rank * n_local,
+                           sampler=args.sampler)
     stream = torch.cuda.current_stream()
     sampler.set_stream(stream.cuda_stream)
     # AD-LDA: sample; all-reduce (SUM) of every rank's int32 nw/nwsum delta; apply
@@ -135,7 +139,7 @@ def main():
     def step():
         trainer.sweep(1)
 
-    for _ in range(args.warmup):
+    for _ in range(args.burnin + args.warmup):
         step()
     torch.cuda.synchronize()
     if world > 1:
@@ -169,7 +173,7 @@ def main():
     if rank == 0:
         bpt = bytes_per_token(K)
         achieved = n_local * bpt / (kern_ms * 1e-3) / 1e9      # GB/s, algorithmic
-        traffic_gb, traffic_src = pmc_traffic(K, n_local, "k_sample<")
+        traffic_gb, traffic_src = pmc_traffic(K, n_local, "k_sample<" if args.sampler == "dense" else "k_sample_sparse<")
         result = {
             "metric": "Gibbs tokens sampled/sec at K=512",
             "value": value,
@@ -177,6 +181,8 @@ def main():
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
+            "burnin": args.burnin,
+            "sampler": args.sampler,
             "ms_per_step": elapsed * 1e3 / args.steps,
             "higher_is_better": True,
             "scaling": "weak",
@@ -204,7 +210,7 @@ def main():
                 "traffic_unit": "GB per launch (rocprofv3 PMC, gfx950-corrected)",
                 "traffic_source": traffic_src,
                 "algorithmic_gb_per_launch": n_local * bpt / 1e9,
-                "kernel": f"k_sample<C={sampler.Kp // 64}> avg {kern_ms:.3f} ms/launch over "
+                "kernel": f"{'k_sample' if args.sampler == 'dense' else 'k_sample_sparse'}<C={sampler.Kp // 64}> avg {kern_ms:.3f} ms/launch over "
                           f"{n_local} tokens, B(K)={bpt} B/token",
             },
             "ll_per_token": ll / (n_local * world),

@@ -47,7 +47,15 @@ typedef int32_t lda_status;
 #define LDA_ERR_STATE (-4)        /* call out of order (e.g. sample with a pending delta) */
 #define LDA_ERR_UNSUPPORTED (-5)  /* e.g. K above the compiled maximum */
 
-#define LDA_MAX_TOPICS 1024       /* dense-kernel instantiations: K <= 1024 */
+#define LDA_MAX_TOPICS 1024       /* kernel instantiations: K <= 1024 */
+
+/* Draw kernels.  Both are exact against the CPU oracle;
+ * they differ in how the same categorical weights are summed:
+ *  DENSE  reads the word's whole nw row (4K bytes per token);
+ *  SPARSE reads only the row's nonzero (count, topic) entries (4 bytes each),
+ *         SparseLDA-style split into a word part and a dense doc part. */
+#define LDA_SAMPLER_DENSE 0
+#define LDA_SAMPLER_SPARSE 1
 
 typedef struct lda_ctx lda_ctx;
 
@@ -59,7 +67,7 @@ typedef struct lda_config {
   double beta;            /* beta   (ParallelTopicModel(.., .., beta))         */
   uint64_t seed;          /* Philox key (ParallelTopicModel.setRandomSeed)     */
   int32_t device;         /* HIP device ordinal                                */
-  int32_t reserved0;
+  int32_t sampler;        /* LDA_SAMPLER_DENSE (0) or LDA_SAMPLER_SPARSE (1)   */
   int64_t token_base;     /* global index of this shard's first token          */
   int64_t tokens_per_range; /* work-queue granule (0 = default)                */
 } lda_config;

@@ -24,6 +24,7 @@ STATUS_NAMES = {
     -5: "LDA_ERR_UNSUPPORTED",
 }
 MAX_TOPICS = 1024
+SAMPLERS = {"dense": 0, "sparse": 1}
 
 
 class LdaError(RuntimeError):
@@ -41,7 +42,7 @@ class lda_config(C.Structure):
         ("beta", C.c_double),
         ("seed", C.c_uint64),
         ("device", C.c_int32),
-        ("reserved0", C.c_int32),
+        ("sampler", C.c_int32),
         ("token_base", C.c_int64),
         ("tokens_per_range", C.c_int64),
     ]

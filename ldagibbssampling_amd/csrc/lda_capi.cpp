@@ -96,7 +96,13 @@ struct lda_ctx {
   uint32_t sweep = 0;
   bool pending = true;
   int cus = 256;
+  int sampler = LDA_SAMPLER_DENSE;
   int sample_blocks = 0, sample_blocks_frozen = 0;
+  // sparse rows of the snapshot (LDA_SAMPLER_SPARSE)
+  uint32_t* ent = nullptr;
+  int64_t* row_off = nullptr;
+  int32_t* row_nnz = nullptr;
+  bool rows_ready = false;
   int64_t tokens_per_range = 0;
   std::vector<int64_t> doc_off_h;
 
@@ -122,7 +128,8 @@ struct lda_ctx {
     if (device >= 0) (void)hipSetDevice(device);
     for (void* p : {(void*)words, (void*)z, (void*)doc_off, (void*)range_doc, (void*)queue,
                     (void*)nw, (void*)nwsum, (void*)delta, (void*)alpha_d, (void*)alpha_f,
-                    (void*)inv, (void*)inv_m1, (void*)partial, (void*)nonzero})
+                    (void*)inv, (void*)inv_m1, (void*)partial, (void*)nonzero, (void*)ent,
+                    (void*)row_off, (void*)row_nnz})
       if (p) (void)hipFree(p);
     if (ev0) (void)hipEventDestroy(ev0);
     if (ev1) (void)hipEventDestroy(ev1);
@@ -150,10 +157,36 @@ struct lda_ctx {
     p.k1 = (uint32_t)(seed >> 32);
     p.c2 = sweep;
     p.c3 = lda::STREAM_SAMPLE;
+    p.ent = ent;
+    p.row_off = row_off;
+    p.row_nnz = row_nnz;
     (void)frozen;
     return p;
   }
 };
+
+// Sparse-row capacities: min(Kp, total count of the word), fixed once the
+// global counts exist (word totals never change afterwards).
+static lda_status build_row_capacity(lda_ctx* c) {
+  int32_t* caps = nullptr;
+  HIP_TRY(dalloc(&caps, c->V));
+  std::vector<int32_t> h(c->V);
+  hipError_t e = lda::launch_row_caps(c->nw, c->V, c->Kp, caps, c->stream);
+  if (e == hipSuccess) e = hipMemcpyAsync(h.data(), caps, sizeof(int32_t) * c->V, hipMemcpyDeviceToHost, c->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+  (void)hipFree(caps);
+  HIP_TRY(e);
+  std::vector<int64_t> off(c->V + 1);
+  off[0] = 0;
+  for (int w = 0; w < c->V; ++w) off[w + 1] = off[w] + h[w];
+  HIP_TRY(dalloc(&c->row_off, c->V + 1));
+  HIP_TRY(dalloc(&c->row_nnz, c->V));
+  HIP_TRY(dalloc(&c->ent, (size_t)off[c->V]));
+  HIP_TRY(hipMemcpyAsync(c->row_off, off.data(), sizeof(int64_t) * (c->V + 1), hipMemcpyHostToDevice, c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  c->rows_ready = true;
+  return LDA_OK;
+}
 
 static lda_status apply_impl(lda_ctx* c) {
   HIP_TRY(hipSetDevice(c->device));
@@ -161,6 +194,13 @@ static lda_status apply_impl(lda_ctx* c) {
   HIP_TRY(lda::launch_prepare_topics(c->nwsum, c->delta + (int64_t)c->V * c->Kp, c->alpha_d,
                                      c->beta, (double)c->V * c->beta, c->K, c->Kp, c->alpha_f,
                                      c->inv, c->inv_m1, c->stream));
+  if (c->sampler == LDA_SAMPLER_SPARSE) {
+    if (!c->rows_ready) {
+      lda_status s = build_row_capacity(c);
+      if (s) return s;
+    }
+    HIP_TRY(lda::launch_build_sparse(c->nw, c->V, c->Kp, c->row_off, c->ent, c->row_nnz, c->stream));
+  }
   c->pending = false;
   return LDA_OK;
 }
@@ -193,6 +233,8 @@ lda_status lda_create(lda_ctx** out, const lda_config* cfg, const int64_t* doc_o
   if (cfg->num_docs < 0) return fail(LDA_ERR_INVALID_ARG, "num_docs must be >= 0");
   if (!cfg->alpha) return fail(LDA_ERR_INVALID_ARG, "alpha is null");
   if (!(cfg->beta > 0.0)) return fail(LDA_ERR_INVALID_ARG, "beta must be > 0");
+  if (cfg->sampler != LDA_SAMPLER_DENSE && cfg->sampler != LDA_SAMPLER_SPARSE)
+    return fail(LDA_ERR_INVALID_ARG, "sampler must be LDA_SAMPLER_DENSE or LDA_SAMPLER_SPARSE");
   for (int k = 0; k < cfg->num_topics; ++k)
     if (!(cfg->alpha[k] > 0.0)) return fail(LDA_ERR_INVALID_ARG, "alpha must be > 0");
   const int64_t D = cfg->num_docs;
@@ -214,6 +256,7 @@ lda_status lda_create(lda_ctx** out, const lda_config* cfg, const int64_t* doc_o
   lda_ctx* c = new (std::nothrow) lda_ctx();
   if (!c) return fail(LDA_ERR_OUT_OF_MEMORY, "host allocation");
   c->device = cfg->device;
+  c->sampler = cfg->sampler;
   c->K = cfg->num_topics;
   c->Kp = pad_topics(c->K);
   c->C = c->Kp / 64;
@@ -244,8 +287,13 @@ lda_status lda_create(lda_ctx** out, const lda_config* cfg, const int64_t* doc_o
   hipDeviceProp_t prop;
   CT(hipGetDeviceProperties(&prop, c->device));
   c->cus = prop.multiProcessorCount;
-  c->sample_blocks = lda::sample_blocks_per_cu(c->C, false) * c->cus;
-  c->sample_blocks_frozen = lda::sample_blocks_per_cu(c->C, true) * c->cus;
+  if (c->sampler == LDA_SAMPLER_SPARSE) {
+    c->sample_blocks = lda::sample_sparse_blocks_per_cu(c->C, false) * c->cus;
+    c->sample_blocks_frozen = lda::sample_sparse_blocks_per_cu(c->C, true) * c->cus;
+  } else {
+    c->sample_blocks = lda::sample_blocks_per_cu(c->C, false) * c->cus;
+    c->sample_blocks_frozen = lda::sample_blocks_per_cu(c->C, true) * c->cus;
+  }
   const int64_t waves = (int64_t)c->sample_blocks * 4;
   int64_t tpr = cfg->tokens_per_range;
   if (tpr <= 0) tpr = std::max<int64_t>(256, std::min<int64_t>(65536, N / std::max<int64_t>(1, waves * 8)));
@@ -349,7 +397,10 @@ lda_status lda_sample(lda_ctx* c) {
     const lda::SampleParams p = c->params(false);
     const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>(c->sample_blocks, (c->R + 3) / 4));
     HIP_TRY(hipEventRecord(c->ev0, c->stream));
-    HIP_TRY(lda::launch_sample(c->C, false, p, blocks, c->stream));
+    if (c->sampler == LDA_SAMPLER_SPARSE)
+      HIP_TRY(lda::launch_sample_sparse(c->C, false, p, blocks, c->stream));
+    else
+      HIP_TRY(lda::launch_sample(c->C, false, p, blocks, c->stream));
     HIP_TRY(hipEventRecord(c->ev1, c->stream));
     c->timed = true;
   }
@@ -551,7 +602,9 @@ lda_status lda_infer(lda_ctx* c, int64_t Dh, const int64_t* doc_off, const int32
   for (int32_t it = 1; it <= n_iter && e == hipSuccess && N > 0; ++it) {
     p.c2 = (uint32_t)(it - 1);
     chk(hipMemsetAsync(q, 0, sizeof(int32_t), c->stream));
-    if (e == hipSuccess) chk(lda::launch_sample(c->C, true, p, blocks, c->stream));
+    if (e == hipSuccess)
+      chk(c->sampler == LDA_SAMPLER_SPARSE ? lda::launch_sample_sparse(c->C, true, p, blocks, c->stream)
+                                           : lda::launch_sample(c->C, true, p, blocks, c->stream));
     if (it > burn_in && (it - burn_in) % thin == 0) {
       ++nsamples;
       if (e == hipSuccess) chk(lda::launch_doc_topics(dz, doff, Dh, c->K, c->Kp, acc, 1, c->stream));

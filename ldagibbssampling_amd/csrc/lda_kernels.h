@@ -18,6 +18,9 @@ constexpr uint32_t STREAM_INFER = 2u;
 #define SAMPLE_P4 4
 #define SAMPLE_P8 4
 #define SAMPLE_P16 2
+// sparse sampler: tokens in flight, 64-entry rounds prefetched per token
+#define SPARSE_P 4
+#define SPARSE_R0 2
 
 struct SampleParams {
   const int32_t* words;     // [N] token stream (doc-contiguous)
@@ -37,10 +40,27 @@ struct SampleParams {
   int64_t token_base;       // Philox counter offset (global token index)
   uint32_t k0, k1;          // Philox key (seed)
   uint32_t c2, c3;          // Philox counter words 2 (sweep) and 3 (stream)
+  // sparse rows of the snapshot (k_sample_sparse only)
+  const uint32_t* ent;      // packed (count << 12) | topic, count saturated at 0xFFFFF
+  const int64_t* row_off;   // [V+1] capacity offsets (min(Kp, word total) per row)
+  const int32_t* row_nnz;   // [V] live entries per row
 };
+
+// Sparse-row packing: 12 topic bits (K <= 4096), 20 count bits; a saturated
+// count field means "read the exact count from the dense nw row".
+constexpr uint32_t ENT_TOPIC_BITS = 12;
+constexpr uint32_t ENT_TOPIC_MASK = (1u << ENT_TOPIC_BITS) - 1;
+constexpr uint32_t ENT_COUNT_SAT = (1u << (32 - ENT_TOPIC_BITS)) - 1;
 
 hipError_t launch_sample(int C, bool frozen, const SampleParams& p, int blocks, hipStream_t st);
 int sample_blocks_per_cu(int C, bool frozen);
+hipError_t launch_sample_sparse(int C, bool frozen, const SampleParams& p, int blocks,
+                                hipStream_t st);
+int sample_sparse_blocks_per_cu(int C, bool frozen);
+// row totals of nw (saturating at Kp) -> host prefix -> capacity offsets
+hipError_t launch_row_caps(const int32_t* nw, int64_t V, int32_t Kp, int32_t* caps, hipStream_t st);
+hipError_t launch_build_sparse(const int32_t* nw, int64_t V, int32_t Kp, const int64_t* row_off,
+                               uint32_t* ent, int32_t* row_nnz, hipStream_t st);
 hipError_t launch_init_z(int32_t* z, int64_t n, int32_t K, int64_t token_base, uint32_t k0,
                          uint32_t k1, hipStream_t st);
 hipError_t launch_count(const int32_t* words, const int32_t* z, int64_t n, int32_t Kp,

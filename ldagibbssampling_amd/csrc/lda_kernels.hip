@@ -302,6 +302,369 @@ __global__ __launch_bounds__(256) void k_sample(SampleParams p) {
   }
 }
 
+// ------------------------------------------------------ the sparse sampler
+// Same semantics and Philox keying as k_sample; the categorical weights are
+// split SparseLDA-style so that a token reads only the NONZERO entries of its
+// word row (packed (count << 12) | topic, built per sweep by k_build_sparse):
+//   coef_k = (float(nd_k) + alpha_k) * (k == z_old ? inv_m1_k : inv_k)
+//   B_e    = coef[t_e] * float(c_e - [t_e == z_old])   (word part, sparse)
+//   A_k    = coef_k * beta                               (doc part, dense)
+// Exact fp32 order (oracle/lda_oracle.c:exact_draw_sparse): lane l holds
+// entries e = l + 64r, serial add over r, DPP scan; lane l owns topics
+// [l*C, l*C+C) for A, serial fma chain, DPP scan; thr = u * (sumB + sumA),
+// B searched first.  coef and nd live in LDS per wave; the per-lane A
+// partial is a register recomputed only for the lanes whose topics changed.
+template <int C>
+__device__ __forceinline__ float coef_partial(const float* __restrict__ coef_lane, float beta) {
+  float a = 0.0f;
+#pragma unroll
+  for (int q = 0; q < C; q += 4) {
+    if constexpr (C >= 4) {
+      const float4 v = *reinterpret_cast<const float4*>(coef_lane + q);
+      a = __builtin_fmaf(v.x, beta, a);
+      a = __builtin_fmaf(v.y, beta, a);
+      a = __builtin_fmaf(v.z, beta, a);
+      a = __builtin_fmaf(v.w, beta, a);
+    } else {
+#pragma unroll
+      for (int j = 0; j < C; ++j) a = __builtin_fmaf(coef_lane[j], beta, a);
+    }
+  }
+  return a;
+}
+
+template <int C, int P, int R0, bool FROZEN>
+__global__ __launch_bounds__(256) void k_sample_sparse(SampleParams p) {
+  extern __shared__ __attribute__((aligned(16))) int32_t smem[];
+  constexpr int KP = C * 64;
+  const int lane = threadIdx.x & 63;
+  const int wid = threadIdx.x >> 6;
+  float* t_alpha = reinterpret_cast<float*>(smem);  // per-block topic tables
+  float* t_inv = t_alpha + KP;
+  float* t_invm1 = t_inv + KP;
+  int32_t* bsum = smem + 3 * KP;                    // per-block nwsum delta
+  int32_t* nd = smem + 4 * KP + wid * 2 * KP;       // per-wave live doc counts
+  float* coef = reinterpret_cast<float*>(nd + KP);  // per-wave coefficients
+
+  for (int i = threadIdx.x; i < KP; i += 256) {
+    t_alpha[i] = p.alpha[i];
+    t_inv[i] = p.inv[i];
+    t_invm1[i] = FROZEN ? 0.0f : p.inv_m1[i];
+    bsum[i] = 0;
+  }
+  for (int i = threadIdx.x; i < 8 * KP; i += 256) smem[4 * KP + i] = 0;
+  __syncthreads();
+
+  const float beta = p.beta;
+  const int last_lane = (p.K - 1) / C;
+  const int last_j = (lane < last_lane) ? C - 1 : (p.K - 1) % C;
+  const int32_t* __restrict__ nw = p.nw;
+  const uint32_t* __restrict__ ent = p.ent;
+  const int64_t* __restrict__ row_off = p.row_off;
+  const int32_t* __restrict__ row_nnz = p.row_nnz;
+
+  while (true) {
+    int r = 0;
+    if (lane == 0) r = atomicAdd(p.queue, 1);
+    r = uniform_i(__shfl(r, 0));
+    if (r >= p.num_ranges) break;
+    const int64_t d0 = p.range_doc[r], d1 = p.range_doc[r + 1];
+    const int64_t t0 = p.doc_off[d0], t1 = p.doc_off[d1];
+    if (t1 <= t0) continue;
+
+    // --- chunk registers: chunk c (cw, cz, cu, cn, row meta), chunk c+1
+    // (words, z, row meta), chunk c+2 (words, z).  Row meta of chunk c+1 is
+    // gathered one chunk ahead, so entry prefetches never wait on it.
+    int64_t cbase = t0;
+    int cw = 0, cz = 0, w1 = 0, z1 = 0, w2 = 0, z2 = 0;
+    if (t0 + lane < t1) {
+      cw = p.words[t0 + lane];
+      cz = p.z[t0 + lane];
+    }
+    if (t0 + 64 + lane < t1) {
+      w1 = p.words[t0 + 64 + lane];
+      z1 = p.z[t0 + 64 + lane];
+    }
+    if (t0 + 128 + lane < t1) {
+      w2 = p.words[t0 + 128 + lane];
+      z2 = p.z[t0 + 128 + lane];
+    }
+    int cmn = row_nnz[cw], m1n = row_nnz[w1];
+    int64_t cmo = row_off[cw], m1o = row_off[w1];
+    int cn = cz;
+    float cu = u01(draw_u32((uint64_t)(p.token_base + t0 + lane), p.c2, p.c3, p.k0, p.k1));
+
+    // --- first document of the range
+    int64_t doc = d0;
+    while (p.doc_off[doc + 1] <= t0) ++doc;
+    int64_t doc_end = p.doc_off[doc + 1];
+    float TA;
+    {
+      for (int64_t i = t0 + lane; i < doc_end; i += 64) atomicAdd(&nd[p.z[i]], 1);
+      float a = 0.0f;
+#pragma unroll
+      for (int j = 0; j < C; ++j) {
+        const int k = lane * C + j;
+        const float cf = ((float)nd[k] + t_alpha[k]) * t_inv[k];
+        coef[k] = cf;
+        a = __builtin_fmaf(cf, beta, a);
+      }
+      TA = a;
+    }
+
+    // --- prime the entry pipeline: first R0 rounds of the next P tokens
+    uint32_t ring[P][R0];
+#pragma unroll
+    for (int s = 0; s < P; ++s) {
+      const int64_t tp = t0 + s;
+      const int n = readlane_i(cmn, s);
+      const int64_t o = ((int64_t)readlane_i((int)(cmo >> 32), s) << 32) |
+                        (uint32_t)readlane_i((int)cmo, s);
+#pragma unroll
+      for (int q = 0; q < R0; ++q)
+        ring[s][q] = (tp < t1 && q * 64 + lane < n) ? ent[o + q * 64 + lane] : 0u;
+    }
+
+    for (int64_t tb = t0; tb < t1; tb += P) {
+#pragma unroll
+      for (int s = 0; s < P; ++s) {
+        const int64_t t = tb + s;
+        if (t >= t1) break;
+        int idx = (int)(t - cbase);
+        if (idx == 64) {
+          p.z[cbase + lane] = cn;
+          cbase += 64;
+          idx = 0;
+          cw = w1;
+          cz = z1;
+          cmn = m1n;
+          cmo = m1o;
+          w1 = w2;
+          z1 = z2;
+          m1n = row_nnz[w1];
+          m1o = row_off[w1];
+          cn = cz;
+          cu = u01(draw_u32((uint64_t)(p.token_base + cbase + lane), p.c2, p.c3, p.k0, p.k1));
+          if (cbase + 128 + lane < t1) {
+            w2 = p.words[cbase + 128 + lane];
+            z2 = p.z[cbase + 128 + lane];
+          }
+        }
+        if (t == doc_end) {
+#pragma unroll
+          for (int j = 0; j < C; ++j) nd[lane * C + j] = 0;
+          ++doc;
+          while (p.doc_off[doc + 1] <= t) ++doc;
+          doc_end = p.doc_off[doc + 1];
+          for (int64_t i = t + lane; i < doc_end; i += 64) atomicAdd(&nd[p.z[i]], 1);
+          float a = 0.0f;
+#pragma unroll
+          for (int j = 0; j < C; ++j) {
+            const int k = lane * C + j;
+            const float cf = ((float)nd[k] + t_alpha[k]) * t_inv[k];
+            coef[k] = cf;
+            a = __builtin_fmaf(cf, beta, a);
+          }
+          TA = a;
+        }
+
+        const int w = readlane_i(cw, idx);
+        const int zo = readlane_i(cz, idx);
+        const float u = readlane_f(cu, idx);
+        const int n = readlane_i(cmn, idx);
+        const int64_t off = ((int64_t)readlane_i((int)(cmo >> 32), idx) << 32) |
+                            (uint32_t)readlane_i((int)cmo, idx);
+        const int lo = zo / C;
+
+        // remove the token from its document (and, unless frozen, from the
+        // snapshot's row/total through inv_m1 and c - 1 below)
+        {
+          const int ndz = nd[zo] - 1;
+          const float cf = ((float)ndz + t_alpha[zo]) * (FROZEN ? t_inv[zo] : t_invm1[zo]);
+          if (lane == 0) {
+            nd[zo] = ndz;
+            coef[zo] = cf;
+          }
+          if (lane == lo) TA = coef_partial<C>(coef + lane * C, beta);
+        }
+
+        // word part over the nonzero entries of row w
+        uint32_t e[C];
+        float SB[C];
+#pragma unroll
+        for (int q = 0; q < C; ++q) {
+          if (q < R0)
+            e[q] = ring[s][q];
+          else
+            e[q] = (q * 64 < n && q * 64 + lane < n) ? ent[off + q * 64 + lane] : 0u;
+        }
+        float accB = 0.0f;
+        int tsel_r[C];
+#pragma unroll
+        for (int q = 0; q < C; ++q) {
+          SB[q] = accB;
+          tsel_r[q] = 0;
+          if (q * 64 < n) {
+            const bool valid = q * 64 + lane < n;
+            const int tq = (int)(e[q] & ENT_TOPIC_MASK);
+            int cq = (int)(e[q] >> ENT_TOPIC_BITS);
+            if (valid && (uint32_t)cq == ENT_COUNT_SAT) cq = nw[(int64_t)w * KP + tq];
+            if (!FROZEN) cq -= (tq == zo) ? 1 : 0;
+            const float b = valid ? coef[tq] * (float)cq : 0.0f;
+            accB = accB + b;
+            SB[q] = accB;
+            tsel_r[q] = tq;
+          }
+        }
+        const float TB = wave_incl_scan(accB);
+        const float TAs = wave_incl_scan(TA);
+        const float sumB = readlane_f(TB, 63);
+        const float sumA = readlane_f(TAs, 63);
+        const float thr = u * (sumB + sumA);
+        int kn;
+        if (thr < sumB) {
+          const int nl = n < 64 ? n : 64;
+          const uint64_t m = __ballot((TB > thr) && (lane < nl));
+          const int lstar = m ? (int)__builtin_ctzll(m) : nl - 1;
+          const float E = lstar > 0 ? readlane_f(TB, lstar - 1) : 0.0f;
+          const int nr = lane < n ? (n - lane + 63) / 64 : 0;
+          int cnt = 0;
+#pragma unroll
+          for (int q = 0; q < C; ++q)
+            if (q * 64 < n) cnt += (q < nr && E + SB[q] <= thr) ? 1 : 0;
+          const int rsel = cnt < nr ? cnt : nr - 1;
+          int tsel = 0;
+#pragma unroll
+          for (int q = 0; q < C; ++q) tsel = (q == rsel) ? tsel_r[q] : tsel;
+          kn = readlane_i(tsel, lstar);
+        } else {
+          const float thr2 = thr - sumB;
+          const uint64_t m = __ballot((TAs > thr2) && (lane <= last_lane));
+          const int lstar = m ? (int)__builtin_ctzll(m) : last_lane;
+          const float E = lstar > 0 ? readlane_f(TAs, lstar - 1) : 0.0f;
+          int jsel = 0;
+          if (lane == lstar) {
+            float a = 0.0f;
+            int cnt = 0;
+#pragma unroll
+            for (int j = 0; j < C; ++j) {
+              a = __builtin_fmaf(coef[lane * C + j], beta, a);
+              cnt += (E + a <= thr2) ? 1 : 0;
+            }
+            jsel = cnt < C ? cnt : last_j;
+          }
+          kn = lstar * C + readlane_i(jsel, lstar);
+        }
+
+        // add the token back under its new topic
+        {
+          const int ndk = nd[kn] + 1;
+          if (lane == 0) nd[kn] = ndk;
+          const int ndz = (kn == zo) ? ndk : nd[zo];
+          const float cfz = ((float)ndz + t_alpha[zo]) * t_inv[zo];
+          const float cfk = ((float)ndk + t_alpha[kn]) * t_inv[kn];
+          if (lane == 0) {
+            coef[zo] = cfz;
+            coef[kn] = cfk;
+          }
+          if (lane == lo || lane == kn / C) TA = coef_partial<C>(coef + lane * C, beta);
+        }
+        cn = (lane == idx) ? kn : cn;
+        if (!FROZEN && kn != zo) {
+          if (lane < 2) {
+            const int k = lane == 0 ? zo : kn;
+            const int v = lane == 0 ? -1 : 1;
+            atomicAdd(&p.delta[(int64_t)w * KP + k], v);
+            atomicAdd(&bsum[k], v);
+          }
+        }
+
+        // keep the pipeline full: first R0 rounds of token t+P
+        const int64_t tp = t + P;
+        if (tp < t1) {
+          const int pidx = (int)(tp - cbase);
+          int np;
+          int64_t op;
+          if (pidx < 64) {
+            np = readlane_i(cmn, pidx);
+            op = ((int64_t)readlane_i((int)(cmo >> 32), pidx) << 32) | (uint32_t)readlane_i((int)cmo, pidx);
+          } else {
+            np = readlane_i(m1n, pidx - 64);
+            op = ((int64_t)readlane_i((int)(m1o >> 32), pidx - 64) << 32) |
+                 (uint32_t)readlane_i((int)m1o, pidx - 64);
+          }
+#pragma unroll
+          for (int q = 0; q < R0; ++q) ring[s][q] = (q * 64 + lane < np) ? ent[op + q * 64 + lane] : 0u;
+        }
+      }
+    }
+    if (cbase + lane < t1) p.z[cbase + lane] = cn;
+#pragma unroll
+    for (int j = 0; j < C; ++j) nd[lane * C + j] = 0;
+  }
+
+  if (!FROZEN) {
+    __syncthreads();
+    for (int i = threadIdx.x; i < KP; i += 256) {
+      const int v = bsum[i];
+      if (v != 0) atomicAdd(&p.dsum[i], v);
+    }
+  }
+}
+
+// Inclusive integer wavefront scan (any order is exact for integers).
+__device__ __forceinline__ int wave_incl_scan_i(int x) {
+  x += __builtin_amdgcn_update_dpp(0, x, 0x111, 0xf, 0xf, true);
+  x += __builtin_amdgcn_update_dpp(0, x, 0x112, 0xf, 0xf, true);
+  x += __builtin_amdgcn_update_dpp(0, x, 0x114, 0xf, 0xf, true);
+  x += __builtin_amdgcn_update_dpp(0, x, 0x118, 0xf, 0xf, true);
+  x += __builtin_amdgcn_update_dpp(0, x, 0x142, 0xa, 0xf, false);
+  x += __builtin_amdgcn_update_dpp(0, x, 0x143, 0xc, 0xf, false);
+  return x;
+}
+
+// Row capacities min(Kp, word total) (one wave per row).
+__global__ __launch_bounds__(256) void k_row_caps(const int32_t* __restrict__ nw, int64_t V,
+                                                  int32_t Kp, int32_t* __restrict__ caps) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  for (int64_t w = (int64_t)blockIdx.x * 4 + wid; w < V; w += (int64_t)gridDim.x * 4) {
+    int64_t tot = 0;
+    for (int k = lane; k < Kp; k += 64) tot += nw[w * Kp + k];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) tot += __shfl_xor(tot, o);
+    if (lane == 0) caps[w] = (int32_t)(tot < Kp ? tot : Kp);
+  }
+}
+
+// Compact every nw row into its sparse entries, topic ascending (one wave per row).
+template <int C>
+__global__ __launch_bounds__(256) void k_build_sparse(const int32_t* __restrict__ nw, int64_t V,
+                                                      const int64_t* __restrict__ row_off,
+                                                      uint32_t* __restrict__ ent,
+                                                      int32_t* __restrict__ row_nnz) {
+  constexpr int KP = C * 64;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  for (int64_t w = (int64_t)blockIdx.x * 4 + wid; w < V; w += (int64_t)gridDim.x * 4) {
+    int32_t c[C];
+    load_row<C>(c, nw + w * KP + lane * C);
+    int cnt = 0;
+#pragma unroll
+    for (int j = 0; j < C; ++j) cnt += c[j] > 0 ? 1 : 0;
+    const int incl = wave_incl_scan_i(cnt);
+    int pos = incl - cnt;
+    const int64_t o = row_off[w];
+#pragma unroll
+    for (int j = 0; j < C; ++j) {
+      if (c[j] > 0) {
+        const uint32_t cc = (uint32_t)c[j] >= ENT_COUNT_SAT ? ENT_COUNT_SAT : (uint32_t)c[j];
+        ent[o + pos] = (cc << ENT_TOPIC_BITS) | (uint32_t)(lane * C + j);
+        ++pos;
+      }
+    }
+    if (lane == 63) row_nnz[w] = incl;
+  }
+}
+
 // ----------------------------------------------------------- count kernels
 __global__ __launch_bounds__(256) void k_init_z(int32_t* __restrict__ z, int64_t n, int32_t K,
                                                 int64_t token_base, uint32_t k0, uint32_t k1) {
@@ -547,6 +910,70 @@ hipError_t launch_sample(int C, bool frozen, const SampleParams& p, int blocks, 
 }
 int sample_blocks_per_cu(int C, bool frozen) {
   return frozen ? occupancy_c<true>(C) : occupancy_c<false>(C);
+}
+
+template <int C, int P, int R0, bool FROZEN>
+static hipError_t launch_sparse_t(const SampleParams& p, int blocks, hipStream_t st) {
+  const size_t lds = 12 * 64 * C * sizeof(int32_t);
+  hipLaunchKernelGGL((k_sample_sparse<C, P, R0, FROZEN>), dim3(blocks), dim3(256), lds, st, p);
+  return hipGetLastError();
+}
+template <int C, int P, int R0, bool FROZEN>
+static int occupancy_sparse_t() {
+  int nb = 0;
+  const size_t lds = 12 * 64 * C * sizeof(int32_t);
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_sample_sparse<C, P, R0, FROZEN>, 256,
+                                                   lds) != hipSuccess)
+    return 1;
+  return nb > 0 ? nb : 1;
+}
+#define LDA_DISPATCH_SPARSE(C_, FN, ...)                            \
+  switch (C_) {                                                     \
+    case 1: return FN<1, SPARSE_P, 1, FROZEN>(__VA_ARGS__);         \
+    case 2: return FN<2, SPARSE_P, 1, FROZEN>(__VA_ARGS__);         \
+    case 4: return FN<4, SPARSE_P, SPARSE_R0, FROZEN>(__VA_ARGS__); \
+    case 8: return FN<8, SPARSE_P, SPARSE_R0, FROZEN>(__VA_ARGS__); \
+    case 16: return FN<16, SPARSE_P, SPARSE_R0, FROZEN>(__VA_ARGS__); \
+    default: break;                                                 \
+  }
+template <bool FROZEN>
+static hipError_t launch_sparse_c(int C, const SampleParams& p, int blocks, hipStream_t st) {
+  LDA_DISPATCH_SPARSE(C, launch_sparse_t, p, blocks, st)
+  return hipErrorInvalidValue;
+}
+template <bool FROZEN>
+static int occupancy_sparse_c(int C) {
+  LDA_DISPATCH_SPARSE(C, occupancy_sparse_t)
+  return 1;
+}
+hipError_t launch_sample_sparse(int C, bool frozen, const SampleParams& p, int blocks,
+                                hipStream_t st) {
+  return frozen ? launch_sparse_c<true>(C, p, blocks, st) : launch_sparse_c<false>(C, p, blocks, st);
+}
+int sample_sparse_blocks_per_cu(int C, bool frozen) {
+  return frozen ? occupancy_sparse_c<true>(C) : occupancy_sparse_c<false>(C);
+}
+
+hipError_t launch_row_caps(const int32_t* nw, int64_t V, int32_t Kp, int32_t* caps, hipStream_t st) {
+  if (V <= 0) return hipSuccess;
+  const int blocks = (int)std::min<int64_t>((V + 3) / 4, 8192);
+  hipLaunchKernelGGL(k_row_caps, dim3(blocks), dim3(256), 0, st, nw, V, Kp, caps);
+  return hipGetLastError();
+}
+
+hipError_t launch_build_sparse(const int32_t* nw, int64_t V, int32_t Kp, const int64_t* row_off,
+                               uint32_t* ent, int32_t* row_nnz, hipStream_t st) {
+  if (V <= 0) return hipSuccess;
+  const int blocks = (int)std::min<int64_t>((V + 3) / 4, 16384);
+  switch (Kp / 64) {
+    case 1: hipLaunchKernelGGL(k_build_sparse<1>, dim3(blocks), dim3(256), 0, st, nw, V, row_off, ent, row_nnz); break;
+    case 2: hipLaunchKernelGGL(k_build_sparse<2>, dim3(blocks), dim3(256), 0, st, nw, V, row_off, ent, row_nnz); break;
+    case 4: hipLaunchKernelGGL(k_build_sparse<4>, dim3(blocks), dim3(256), 0, st, nw, V, row_off, ent, row_nnz); break;
+    case 8: hipLaunchKernelGGL(k_build_sparse<8>, dim3(blocks), dim3(256), 0, st, nw, V, row_off, ent, row_nnz); break;
+    case 16: hipLaunchKernelGGL(k_build_sparse<16>, dim3(blocks), dim3(256), 0, st, nw, V, row_off, ent, row_nnz); break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
 }
 
 hipError_t launch_init_z(int32_t* z, int64_t n, int32_t K, int64_t token_base, uint32_t k0,

@@ -31,7 +31,7 @@ class _DeviceArray:
 class GibbsSampler:
     def __init__(self, num_topics: int, num_types: int, doc_off, words, alpha, beta: float,
                  seed: int = 0, z_init=None, device: int = 0, token_base: int = 0,
-                 tokens_per_range: int = 0):
+                 tokens_per_range: int = 0, sampler: str = "dense"):
         L = capi.load()
         self.K = int(num_topics)
         self.V = int(num_types)
@@ -49,6 +49,8 @@ class GibbsSampler:
         cfg.beta = float(beta)
         cfg.seed = int(seed) & (2**64 - 1)
         cfg.device = int(device)
+        cfg.sampler = capi.SAMPLERS[sampler]
+        self.sampler_kind = sampler
         cfg.token_base = int(token_base)
         cfg.tokens_per_range = int(tokens_per_range)
         zp = None

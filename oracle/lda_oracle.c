@@ -135,6 +135,7 @@ struct orc_exact {
   uint64_t seed;
   int64_t token_base;
   uint32_t sweep;
+  int kind; /* 0 = dense draw, 1 = sparse (SparseLDA-split) draw */
 };
 
 static void exact_prepare_topics(orc_exact* s) {
@@ -209,6 +210,7 @@ void orc_exact_destroy(orc_exact* s) {
 int32_t orc_exact_kpad(const orc_exact* s) { return s->Kp; }
 int32_t* orc_exact_delta(orc_exact* s) { return s->delta; }
 void orc_exact_set_sweep(orc_exact* s, uint32_t sweep) { s->sweep = sweep; }
+void orc_exact_set_kind(orc_exact* s, int kind) { s->kind = kind; }
 uint32_t orc_exact_get_sweep(const orc_exact* s) { return s->sweep; }
 
 void orc_exact_apply(orc_exact* s) {
@@ -298,12 +300,85 @@ static int exact_draw(const orc_exact* s, const int32_t* nwrow, const int32_t* n
   return lstar * C + jsel;
 }
 
+/* The sparse draw (kind 1, ldagibbssampling_amd/csrc/lda_kernels.hip:
+ * k_sample_sparse).  The same p_k = (nd_k + a_k)(nw_k + b) inv_k is split as
+ *   coef_k = (float(nd_k) + alpha_k) * (k == zo ? inv_m1_k : inv_k)
+ *   B_e    = coef[t_e] * float(c_e - [t_e == zo])   over the word's nonzero
+ *            entries e (topic ascending), lane l holding e = l, l+64, ...
+ *   A_k    = coef_k * beta  (all topics, lane l owning [l*C, l*C+C))
+ * B: per-lane serial sums (add), DPP scan; A: per-lane serial fma chain, DPP
+ * scan; thr = u * (sumB + sumA); B is searched first. */
+static int exact_draw_sparse(const orc_exact* s, const int32_t* nwrow, const int32_t* nd, int zo,
+                             float u, float* coef, int32_t* et, int32_t* ec) {
+  const int C = s->C, K = s->K, Kp = s->Kp;
+  for (int k = 0; k < Kp; ++k)
+    coef[k] = ((float)nd[k] + s->alpha_f[k]) * (k == zo ? s->inv_m1[k] : s->inv[k]);
+  int n = 0;
+  for (int k = 0; k < K; ++k)
+    if (nwrow[k] > 0) {
+      et[n] = k;
+      ec[n] = nwrow[k] - (k == zo ? 1 : 0);
+      n++;
+    }
+  float TB[64], TA[64];
+  for (int l = 0; l < 64; ++l) {
+    float acc = 0.0f;
+    for (int e = l; e < n; e += 64) acc = acc + coef[et[e]] * (float)ec[e];
+    TB[l] = acc;
+    float a = 0.0f;
+    for (int j = 0; j < C; ++j) a = fmaf(coef[l * C + j], s->beta_f, a);
+    TA[l] = a;
+  }
+  wave_scan_emulate(TB);
+  wave_scan_emulate(TA);
+  const float sumB = TB[63], sumA = TA[63];
+  const float thr = u * (sumB + sumA);
+  if (thr < sumB) {
+    const int nl = n < 64 ? n : 64;
+    int lstar = nl - 1;
+    for (int l = 0; l < nl; ++l)
+      if (TB[l] > thr) {
+        lstar = l;
+        break;
+      }
+    const float E = lstar > 0 ? TB[lstar - 1] : 0.0f;
+    float acc = 0.0f;
+    int cnt = 0, nr = 0;
+    for (int e = lstar; e < n; e += 64) {
+      acc = acc + coef[et[e]] * (float)ec[e];
+      cnt += (E + acc <= thr) ? 1 : 0;
+      nr++;
+    }
+    const int r = cnt < nr ? cnt : nr - 1;
+    return et[lstar + 64 * r];
+  }
+  const float thr2 = thr - sumB;
+  const int last_lane = (K - 1) / C;
+  int lstar = last_lane;
+  for (int l = 0; l <= last_lane; ++l)
+    if (TA[l] > thr2) {
+      lstar = l;
+      break;
+    }
+  const float E = lstar > 0 ? TA[lstar - 1] : 0.0f;
+  float a = 0.0f;
+  int cnt = 0;
+  for (int j = 0; j < C; ++j) {
+    a = fmaf(coef[lstar * C + j], s->beta_f, a);
+    cnt += (E + a <= thr2) ? 1 : 0;
+  }
+  const int jsel = cnt < C ? cnt : ((lstar < last_lane) ? C - 1 : (K - 1) % C);
+  return lstar * C + jsel;
+}
+
 /* Sample the docs [d0, d1) of a token stream against the snapshot. */
 static void exact_sample_docs(const orc_exact* s, const int64_t* doc_off, const int32_t* words,
                               int32_t* z, int64_t d0, int64_t d1, int frozen, uint32_t c2,
                               uint32_t c3, int64_t token_base, int32_t* delta) {
   int32_t* nd = (int32_t*)calloc(s->Kp, sizeof(int32_t));
   float* S = (float*)malloc(sizeof(float) * s->Kp);
+  int32_t* et = (int32_t*)malloc(sizeof(int32_t) * s->Kp);
+  int32_t* ec = (int32_t*)malloc(sizeof(int32_t) * s->Kp);
   int32_t* dsum = delta ? delta + (size_t)s->V * s->Kp : NULL;
   for (int64_t d = d0; d < d1; ++d) {
     memset(nd, 0, sizeof(int32_t) * s->Kp);
@@ -313,7 +388,9 @@ static void exact_sample_docs(const orc_exact* s, const int64_t* doc_off, const 
       int zo = z[i];
       float u = orc_u01(orc_draw(s->seed, (uint64_t)(token_base + i), c2, c3));
       nd[zo]--;
-      int kn = exact_draw(s, s->nw + (size_t)w * s->Kp, nd, frozen ? -1 : zo, u, S);
+      int kn = s->kind == 1
+                   ? exact_draw_sparse(s, s->nw + (size_t)w * s->Kp, nd, frozen ? -1 : zo, u, S, et, ec)
+                   : exact_draw(s, s->nw + (size_t)w * s->Kp, nd, frozen ? -1 : zo, u, S);
       nd[kn]++;
       z[i] = kn;
       if (!frozen && kn != zo) {
@@ -326,6 +403,8 @@ static void exact_sample_docs(const orc_exact* s, const int64_t* doc_off, const 
   }
   free(nd);
   free(S);
+  free(et);
+  free(ec);
 }
 
 void orc_exact_sample(orc_exact* s, int frozen) {

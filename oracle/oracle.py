@@ -64,6 +64,7 @@ def lib():
     L.orc_exact_apply.argtypes = [C.c_void_p]
     L.orc_exact_set_alpha_beta.argtypes = [C.c_void_p, _f64p, C.c_double]
     L.orc_exact_set_sweep.argtypes = [C.c_void_p, C.c_uint32]
+    L.orc_exact_set_kind.argtypes = [C.c_void_p, C.c_int]
     L.orc_exact_get_sweep.restype = C.c_uint32
     L.orc_exact_get_sweep.argtypes = [C.c_void_p]
     L.orc_exact_get_z.argtypes = [C.c_void_p, _i32p]
@@ -135,7 +136,8 @@ class JavaRandom:
 class ExactSampler:
     """cpu_exact: the bit-exact definition of the GPU sampler (one shard)."""
 
-    def __init__(self, K, V, doc_off, words, alpha, beta, seed, z_init=None, token_base=0):
+    def __init__(self, K, V, doc_off, words, alpha, beta, seed, z_init=None, token_base=0,
+                 kind="dense"):
         self.K, self.V = int(K), int(V)
         self.doc_off = np.ascontiguousarray(doc_off, dtype=np.int64)
         self.words = np.ascontiguousarray(words, dtype=np.int32)
@@ -150,6 +152,7 @@ class ExactSampler:
                                          alpha, float(beta), int(seed) & (2**64 - 1), int(token_base))
         self.Kp = int(lib().orc_exact_kpad(self._h))
         self._pending = True      # create leaves the shard's counts as the pending delta
+        lib().orc_exact_set_kind(self._h, {"dense": 0, "sparse": 1}[kind])
 
     def __del__(self):
         h = getattr(self, "_h", None)

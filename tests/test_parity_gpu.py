@@ -27,13 +27,16 @@ def _ragged_corpus(D, V, seed, max_len=300, empty_every=17):
     return Corpus(off, words, V)
 
 
-def _pair(oracle, corpus, K, alpha, beta, seed, tokens_per_range=0, z_init=None):
+def _pair(oracle, corpus, K, alpha, beta, seed, tokens_per_range=0, z_init=None, kind="dense"):
     from ldagibbssampling_amd.sampler import GibbsSampler
     g = GibbsSampler(K, corpus.num_types, corpus.doc_off, corpus.words, alpha, beta, seed=seed,
-                     z_init=z_init, tokens_per_range=tokens_per_range)
+                     z_init=z_init, tokens_per_range=tokens_per_range, sampler=kind)
     o = oracle.ExactSampler(K, corpus.num_types, corpus.doc_off, corpus.words, alpha, beta, seed,
-                            z_init=z_init)
+                            z_init=z_init, kind=kind)
     return g, o
+
+
+KINDS = ["dense", "sparse"]
 
 
 def _assert_same_state(g, o, with_nd=True):
@@ -47,11 +50,12 @@ def _assert_same_state(g, o, with_nd=True):
         np.testing.assert_array_equal(gnd, ond)
 
 
+@pytest.mark.parametrize("kind", KINDS)
 @pytest.mark.parametrize("K", [20, 64, 100, 128, 256, 512, 1000, 1024])
-def test_sweeps_bit_exact(oracle, K):
+def test_sweeps_bit_exact(oracle, K, kind):
     corpus = _ragged_corpus(D=120, V=700, seed=K)
     alpha = np.full(K, 0.1)
-    g, o = _pair(oracle, corpus, K, alpha, 0.01, seed=1234 + K, tokens_per_range=300)
+    g, o = _pair(oracle, corpus, K, alpha, 0.01, seed=1234 + K, tokens_per_range=300, kind=kind)
     g.sweep(0)
     o.apply()
     _assert_same_state(g, o)                  # Philox initialisation
@@ -61,11 +65,12 @@ def test_sweeps_bit_exact(oracle, K):
         _assert_same_state(g, o)
 
 
-def test_many_sweeps_and_loglik(oracle):
+@pytest.mark.parametrize("kind", KINDS)
+def test_many_sweeps_and_loglik(oracle, kind):
     c = synthetic_lda(num_docs=300, num_types=2000, num_topics=128, doc_len=None, mean_len=80,
                       min_len=1, max_len=400, seed=7)
     K = 128
-    g, o = _pair(oracle, c, K, np.full(K, 0.1), 0.01, seed=99)
+    g, o = _pair(oracle, c, K, np.full(K, 0.1), 0.01, seed=99, kind=kind)
     g.sweep(10)
     o.sweep(10)
     _assert_same_state(g, o)
@@ -73,13 +78,14 @@ def test_many_sweeps_and_loglik(oracle):
     assert abs(lg - lo) <= 1e-9 * abs(lo), (lg, lo)
 
 
-def test_asymmetric_alpha_and_z_init(oracle):
+@pytest.mark.parametrize("kind", KINDS)
+def test_asymmetric_alpha_and_z_init(oracle, kind):
     c = synthetic_changelists(num_docs=400, num_types=900, seed=3)
     K = 20
     rng = np.random.default_rng(5)
     alpha = rng.uniform(0.05, 2.0, size=K)
     z0 = rng.integers(0, K, size=c.num_tokens).astype(np.int32)
-    g, o = _pair(oracle, c, K, alpha, 0.001, seed=2**40 + 17, z_init=z0)
+    g, o = _pair(oracle, c, K, alpha, 0.001, seed=2**40 + 17, z_init=z0, kind=kind)
     g.sweep(5)
     o.sweep(5)
     _assert_same_state(g, o)
@@ -92,16 +98,17 @@ def test_asymmetric_alpha_and_z_init(oracle):
     _assert_same_state(g, o)
 
 
-def test_sharded_equals_single(oracle):
+@pytest.mark.parametrize("kind", KINDS)
+def test_sharded_equals_single(oracle, kind):
     """AD-LDA over 3 shards (delta summed on the host) == one shard, bit for bit."""
     from ldagibbssampling_amd.sampler import GibbsSampler
     c = _ragged_corpus(D=90, V=500, seed=11)
     K, seed = 128, 77
     alpha = np.full(K, 0.2)
-    single = GibbsSampler(K, c.num_types, c.doc_off, c.words, alpha, 0.01, seed=seed)
+    single = GibbsSampler(K, c.num_types, c.doc_off, c.words, alpha, 0.01, seed=seed, sampler=kind)
     cuts = [0, 30, 61, 90]
     shards = [GibbsSampler(K, c.num_types, c.doc_off[a:b + 1], c.words[c.doc_off[a]:c.doc_off[b]],
-                           alpha, 0.01, seed=seed, token_base=int(c.doc_off[a]))
+                           alpha, 0.01, seed=seed, token_base=int(c.doc_off[a]), sampler=kind)
               for a, b in zip(cuts[:-1], cuts[1:])]
     import torch
 
@@ -131,17 +138,18 @@ def test_sharded_equals_single(oracle):
     for s in shards:
         np.testing.assert_array_equal(s.counts()[0], single.counts()[0])
         np.testing.assert_array_equal(s.counts()[1], single.counts()[1])
-    o = oracle.ExactSampler(K, c.num_types, c.doc_off, c.words, alpha, 0.01, seed)
+    o = oracle.ExactSampler(K, c.num_types, c.doc_off, c.words, alpha, 0.01, seed, kind=kind)
     o.sweep(3)
     np.testing.assert_array_equal(single.z(), o.z())
 
 
-def test_inference_matches_oracle(oracle):
+@pytest.mark.parametrize("kind", KINDS)
+def test_inference_matches_oracle(oracle, kind):
     c = synthetic_lda(num_docs=200, num_types=1500, num_topics=64, doc_len=None, mean_len=60,
                       min_len=2, max_len=200, seed=21)
     train, held = c.subset(range(0, 160)), c.subset(range(160, 200))
     K = 64
-    g, o = _pair(oracle, train, K, np.full(K, 0.1), 0.01, seed=5)
+    g, o = _pair(oracle, train, K, np.full(K, 0.1), 0.01, seed=5, kind=kind)
     g.sweep(20)
     o.sweep(20)
     _assert_same_state(g, o, with_nd=False)
@@ -191,3 +199,19 @@ def test_empty_corpus():
     g.sweep(2)
     nw, nwsum, nd, ndsum = g.counts(with_nd=True)
     assert nw.sum() == 0 and nwsum.sum() == 0 and nd.sum() == 0 and ndsum.sum() == 0
+
+
+def test_sparse_saturated_counts(oracle):
+    """Entries whose count overflows the packed 20-bit field (>= 2^20 - 1) are
+    read exactly from the dense row: one very frequent word."""
+    from ldagibbssampling_amd.corpus import Corpus
+    D, L = 40, 60000
+    rng = np.random.default_rng(1)
+    words = np.where(rng.random(D * L) < 0.97, 0, rng.integers(1, 50, D * L)).astype(np.int32)
+    c = Corpus(np.arange(D + 1, dtype=np.int64) * L, words, 50)
+    K = 2
+    g, o = _pair(oracle, c, K, np.full(K, 0.1), 0.01, seed=3, kind="sparse")
+    g.sweep(2)
+    o.sweep(2)
+    assert g.counts()[0].max() >= (1 << 20) - 1
+    _assert_same_state(g, o, with_nd=False)
