@@ -409,6 +409,29 @@ lda_status lda_sample(lda_ctx* c) {
   return LDA_OK;
 }
 
+// Debug (not in the public header): one sparse sampling pass that also
+// records 8 floats per token (kn, sumB, sumA, thr, nnz, z_old, word, u).
+lda_status lda_debug_sample_trace(lda_ctx* c, float* host_trace) {
+  if (!c || !host_trace) return fail(LDA_ERR_INVALID_ARG, "null argument");
+  if (c->pending) return fail(LDA_ERR_STATE, "pending delta");
+  if (c->sampler != LDA_SAMPLER_SPARSE) return fail(LDA_ERR_UNSUPPORTED, "sparse sampler only");
+  HIP_TRY(hipSetDevice(c->device));
+  float* tr = nullptr;
+  HIP_TRY(dalloc(&tr, (size_t)8 * std::max<int64_t>(c->N, 1)));
+  hipError_t e = hipMemsetAsync(c->queue, 0, sizeof(int32_t), c->stream);
+  lda::SampleParams p = c->params(false);
+  p.trace = tr;
+  const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>(c->sample_blocks, (c->R + 3) / 4));
+  if (e == hipSuccess && c->N > 0) e = lda::launch_sample_sparse(c->C, false, p, blocks, c->stream);
+  if (e == hipSuccess) e = hipMemcpyAsync(host_trace, tr, sizeof(float) * 8 * c->N, hipMemcpyDeviceToHost, c->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+  (void)hipFree(tr);
+  HIP_TRY(e);
+  c->sweep++;
+  c->pending = true;
+  return LDA_OK;
+}
+
 lda_status lda_last_sample_ms(lda_ctx* c, float* ms) {
   if (!c || !ms) return fail(LDA_ERR_INVALID_ARG, "null argument");
   *ms = 0.0f;

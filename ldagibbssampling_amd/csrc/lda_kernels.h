@@ -44,6 +44,7 @@ struct SampleParams {
   const uint32_t* ent;      // packed (count << 12) | topic, count saturated at 0xFFFFF
   const int64_t* row_off;   // [V+1] capacity offsets (min(Kp, word total) per row)
   const int32_t* row_nnz;   // [V] live entries per row
+  float* trace;             // debug only: 8 floats per token when non-null
 };
 
 // Sparse-row packing: 12 topic bits (K <= 4096), 20 count bits; a saturated

@@ -93,6 +93,14 @@ __device__ __forceinline__ float readlane_f(float v, int l) {
 }
 __device__ __forceinline__ int uniform_i(int v) { return __builtin_amdgcn_readfirstlane(v); }
 
+// Lanes of one wavefront hand LDS values to each other (histogram atomics,
+// lane-0 updates read by every lane).  Without a fence that is a data race in
+// the C++ model and hipcc may forward a lane's OWN earlier store to its later
+// load (observed: the doc-histogram zeroing store forwarded past other lanes'
+// ds_add).  A wavefront-scope fence is a compiler memory barrier; DS
+// instructions of one wave already execute in order, so it costs nothing.
+__device__ __forceinline__ void wave_lds_fence() { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront"); }
+
 template <int C>
 __device__ __forceinline__ void load_row(int32_t (&r)[C], const int32_t* __restrict__ p) {
   if constexpr (C >= 4) {
@@ -174,11 +182,13 @@ __global__ __launch_bounds__(256) void k_sample(SampleParams p) {
     float ndv[C];
     {
       for (int64_t i = t0 + lane; i < doc_end; i += 64) atomicAdd(&hist[p.z[i]], 1);
+      wave_lds_fence();
 #pragma unroll
       for (int j = 0; j < C; ++j) {
         ndv[j] = (float)hist[lane * C + j];
         hist[lane * C + j] = 0;
       }
+      wave_lds_fence();
     }
 
     // --- prime the row pipeline
@@ -216,11 +226,13 @@ __global__ __launch_bounds__(256) void k_sample(SampleParams p) {
           while (p.doc_off[doc + 1] <= t) ++doc;
           doc_end = p.doc_off[doc + 1];
           for (int64_t i = t + lane; i < doc_end; i += 64) atomicAdd(&hist[p.z[i]], 1);
+          wave_lds_fence();
 #pragma unroll
           for (int j = 0; j < C; ++j) {
             ndv[j] = (float)hist[lane * C + j];
             hist[lane * C + j] = 0;
           }
+          wave_lds_fence();
         }
 
         const int w = readlane_i(cw, idx);
@@ -401,6 +413,7 @@ __global__ __launch_bounds__(256) void k_sample_sparse(SampleParams p) {
     float TA;
     {
       for (int64_t i = t0 + lane; i < doc_end; i += 64) atomicAdd(&nd[p.z[i]], 1);
+      wave_lds_fence();
       float a = 0.0f;
 #pragma unroll
       for (int j = 0; j < C; ++j) {
@@ -410,6 +423,7 @@ __global__ __launch_bounds__(256) void k_sample_sparse(SampleParams p) {
         a = __builtin_fmaf(cf, beta, a);
       }
       TA = a;
+      wave_lds_fence();
     }
 
     // --- prime the entry pipeline: first R0 rounds of the next P tokens
@@ -453,10 +467,12 @@ __global__ __launch_bounds__(256) void k_sample_sparse(SampleParams p) {
         if (t == doc_end) {
 #pragma unroll
           for (int j = 0; j < C; ++j) nd[lane * C + j] = 0;
+          wave_lds_fence();
           ++doc;
           while (p.doc_off[doc + 1] <= t) ++doc;
           doc_end = p.doc_off[doc + 1];
           for (int64_t i = t + lane; i < doc_end; i += 64) atomicAdd(&nd[p.z[i]], 1);
+          wave_lds_fence();
           float a = 0.0f;
 #pragma unroll
           for (int j = 0; j < C; ++j) {
@@ -466,6 +482,7 @@ __global__ __launch_bounds__(256) void k_sample_sparse(SampleParams p) {
             a = __builtin_fmaf(cf, beta, a);
           }
           TA = a;
+          wave_lds_fence();
         }
 
         const int w = readlane_i(cw, idx);
@@ -485,6 +502,7 @@ __global__ __launch_bounds__(256) void k_sample_sparse(SampleParams p) {
             nd[zo] = ndz;
             coef[zo] = cf;
           }
+          wave_lds_fence();
           if (lane == lo) TA = coef_partial<C>(coef + lane * C, beta);
         }
 
@@ -556,10 +574,22 @@ __global__ __launch_bounds__(256) void k_sample_sparse(SampleParams p) {
           kn = lstar * C + readlane_i(jsel, lstar);
         }
 
+        if (p.trace != nullptr && lane == 0) {
+          float* tr = p.trace + 8 * t;
+          tr[0] = (float)kn;
+          tr[1] = sumB;
+          tr[2] = sumA;
+          tr[3] = thr;
+          tr[4] = (float)n;
+          tr[5] = (float)zo;
+          tr[6] = (float)w;
+          tr[7] = u;
+        }
         // add the token back under its new topic
         {
           const int ndk = nd[kn] + 1;
           if (lane == 0) nd[kn] = ndk;
+          wave_lds_fence();
           const int ndz = (kn == zo) ? ndk : nd[zo];
           const float cfz = ((float)ndz + t_alpha[zo]) * t_inv[zo];
           const float cfk = ((float)ndk + t_alpha[kn]) * t_inv[kn];
@@ -567,6 +597,7 @@ __global__ __launch_bounds__(256) void k_sample_sparse(SampleParams p) {
             coef[zo] = cfz;
             coef[kn] = cfk;
           }
+          wave_lds_fence();
           if (lane == lo || lane == kn / C) TA = coef_partial<C>(coef + lane * C, beta);
         }
         cn = (lane == idx) ? kn : cn;
@@ -601,6 +632,7 @@ __global__ __launch_bounds__(256) void k_sample_sparse(SampleParams p) {
     if (cbase + lane < t1) p.z[cbase + lane] = cn;
 #pragma unroll
     for (int j = 0; j < C; ++j) nd[lane * C + j] = 0;
+    wave_lds_fence();
   }
 
   if (!FROZEN) {
