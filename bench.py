@@ -95,7 +95,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="c4", choices=sorted(CONFIGS))
     ap.add_argument("--docs", type=int, default=0, help="override docs per GPU")
-    ap.add_argument("--sampler", default="dense", choices=["dense", "sparse"])
+    ap.add_argument("--sampler", default="dense", choices=["dense", "sparse", "dense32"])
     ap.add_argument("--burnin", type=int, default=0,
                     help="extra untimed sweeps before the warm-up (steady-state measurement)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -173,7 +173,7 @@ def main():
     if rank == 0:
         bpt = bytes_per_token(K)
         achieved = n_local * bpt / (kern_ms * 1e-3) / 1e9      # GB/s, algorithmic
-        traffic_gb, traffic_src = pmc_traffic(K, n_local, "k_sample<" if args.sampler == "dense" else "k_sample_sparse<")
+        traffic_gb, traffic_src = pmc_traffic(K, n_local, "k_sample_sparse<" if args.sampler == "sparse" else "k_sample<")
         result = {
             "metric": "Gibbs tokens sampled/sec at K=512",
             "value": value,
@@ -210,7 +210,7 @@ def main():
                 "traffic_unit": "GB per launch (rocprofv3 PMC, gfx950-corrected)",
                 "traffic_source": traffic_src,
                 "algorithmic_gb_per_launch": n_local * bpt / 1e9,
-                "kernel": f"{'k_sample' if args.sampler == 'dense' else 'k_sample_sparse'}<C={sampler.Kp // 64}> avg {kern_ms:.3f} ms/launch over "
+                "kernel": f"{'k_sample_sparse' if args.sampler == 'sparse' else 'k_sample'}<C={sampler.Kp // 64}> avg {kern_ms:.3f} ms/launch over "
                           f"{n_local} tokens, B(K)={bpt} B/token",
             },
             "ll_per_token": ll / (n_local * world),

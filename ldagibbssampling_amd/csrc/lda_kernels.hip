@@ -125,13 +125,74 @@ __device__ __forceinline__ void load_row(int32_t (&r)[C], const int32_t* __restr
 // One wavefront walks one work range (a run of whole documents) at a time,
 // pulling ranges from a device queue.  The wave keeps a 64-token chunk of the
 // token stream in registers (lane i <-> token i of the chunk: word, old z,
-// Philox uniform, new z), the next chunk's words/z one chunk ahead, and the
-// nw rows of the next P tokens in flight (the snapshot makes row loads
-// independent of the draws, so they pipeline across tokens and documents).
-template <int C, int P, bool FROZEN>
+// Philox uniform, new z), the next two chunks' words/z ahead, and the nw rows
+// of the next P tokens in flight (the snapshot makes row loads independent of
+// the draws, so they pipeline across tokens and documents).
+//
+// PACKED: rows are read from the 16-bit copy nw16 (half the bytes) unless the
+// word's row holds a count > 65535 ("wide", flag gathered one chunk ahead),
+// in which case the int32 row is read.  Same counts, same arithmetic.
+template <int C>
+__device__ __forceinline__ void load_raw(uint32_t (&r)[C], const uint32_t* __restrict__ p, int ndw) {
+  // ndw = dwords this lane loads: C (int32 row) or C/2 (u16 row, C >= 2)
+  if constexpr (C >= 8) {
+#pragma unroll
+    for (int q = 0; q < C / 4; ++q) {
+      if (q * 4 < ndw) {
+        const uint4 v = reinterpret_cast<const uint4*>(p)[q];
+        r[4 * q + 0] = v.x;
+        r[4 * q + 1] = v.y;
+        r[4 * q + 2] = v.z;
+        r[4 * q + 3] = v.w;
+      }
+    }
+  } else if constexpr (C == 4) {
+    if (ndw == 4) {
+      const uint4 v = *reinterpret_cast<const uint4*>(p);
+      r[0] = v.x; r[1] = v.y; r[2] = v.z; r[3] = v.w;
+    } else {
+      const uint2 v = *reinterpret_cast<const uint2*>(p);
+      r[0] = v.x; r[1] = v.y;
+    }
+  } else if constexpr (C == 2) {
+    if (ndw == 2) {
+      const uint2 v = *reinterpret_cast<const uint2*>(p);
+      r[0] = v.x; r[1] = v.y;
+    } else {
+      r[0] = p[0];
+    }
+  } else {
+    r[0] = p[0];
+  }
+}
+
+template <int C, bool PACKED>
+__device__ __forceinline__ const uint32_t* row_ptr(const SampleParams& p, int w, bool wide, int lane) {
+  if (PACKED && !wide) {
+    if constexpr (C == 1) {
+      // one u16 per lane: lanes pair up on a dword, the odd lane takes the high half
+      return reinterpret_cast<const uint32_t*>(p.nw16 + (int64_t)w * (C * 64)) + (lane >> 1);
+    } else {
+      return reinterpret_cast<const uint32_t*>(p.nw16 + (int64_t)w * (C * 64) + lane * C);
+    }
+  }
+  return reinterpret_cast<const uint32_t*>(p.nw + (int64_t)w * (C * 64) + lane * C);
+}
+
+template <int C, bool PACKED>
+__device__ __forceinline__ int32_t row_count(const uint32_t (&r)[C], int j, bool wide, int lane) {
+  if (PACKED && !wide) {
+    if constexpr (C == 1) return (int32_t)((lane & 1) ? (r[0] >> 16) : (r[0] & 0xFFFFu));
+    else return (int32_t)((j & 1) ? (r[j >> 1] >> 16) : (r[j >> 1] & 0xFFFFu));
+  }
+  return (int32_t)r[j];
+}
+
+template <int C, int P, bool FROZEN, bool PACKED>
 __global__ __launch_bounds__(256) void k_sample(SampleParams p) {
   extern __shared__ __attribute__((aligned(16))) int32_t smem[];
   constexpr int KP = C * 64;
+  constexpr int NDW_PACKED = C >= 2 ? C / 2 : 1;
   const int lane = threadIdx.x & 63;
   const int wid = threadIdx.x >> 6;
   int32_t* hist = smem + wid * KP;  // per-wave doc-topic histogram scratch
@@ -150,7 +211,7 @@ __global__ __launch_bounds__(256) void k_sample(SampleParams p) {
   const float beta = p.beta;
   const int last_lane = (p.K - 1) / C;
   const int last_j = (lane < last_lane) ? C - 1 : (p.K - 1) % C;
-  const int32_t* __restrict__ nw = p.nw;
+  const uint8_t* __restrict__ wide_of = p.wide;
 
   while (true) {
     int r = 0;
@@ -161,17 +222,22 @@ __global__ __launch_bounds__(256) void k_sample(SampleParams p) {
     const int64_t t0 = p.doc_off[d0], t1 = p.doc_off[d1];
     if (t1 <= t0) continue;
 
-    // --- chunk registers
+    // --- chunk registers: chunk c (cw, cz, cu, cn, cf), c+1 (w1, z1, f1), c+2 (w2, z2)
     int64_t cbase = t0;
-    int cw = 0, cz = 0, czn = 0, cwn = 0;
+    int cw = 0, cz = 0, w1 = 0, z1 = 0, w2 = 0, z2 = 0;
     if (t0 + lane < t1) {
       cw = p.words[t0 + lane];
       cz = p.z[t0 + lane];
     }
     if (t0 + 64 + lane < t1) {
-      cwn = p.words[t0 + 64 + lane];
-      czn = p.z[t0 + 64 + lane];
+      w1 = p.words[t0 + 64 + lane];
+      z1 = p.z[t0 + 64 + lane];
     }
+    if (t0 + 128 + lane < t1) {
+      w2 = p.words[t0 + 128 + lane];
+      z2 = p.z[t0 + 128 + lane];
+    }
+    int cf = PACKED ? (int)wide_of[cw] : 1, f1 = PACKED ? (int)wide_of[w1] : 1;
     int cn = cz;
     float cu = u01(draw_u32((uint64_t)(p.token_base + t0 + lane), p.c2, p.c3, p.k0, p.k1));
 
@@ -192,13 +258,13 @@ __global__ __launch_bounds__(256) void k_sample(SampleParams p) {
     }
 
     // --- prime the row pipeline
-    int32_t rows[P][C];
+    uint32_t rows[P][C];
 #pragma unroll
     for (int s = 0; s < P; ++s) {
       const int64_t tp = t0 + s;
-      const int wp = readlane_i(cw, s);
-      const int64_t wrow = (tp < t1) ? (int64_t)wp : 0;
-      load_row<C>(rows[s], nw + wrow * KP + lane * C);
+      const int wp = (tp < t1) ? readlane_i(cw, s) : 0;
+      const bool wd = PACKED ? (readlane_i(cf, s) != 0) : true;
+      load_raw<C>(rows[s], row_ptr<C, PACKED>(p, wp, wd, lane), wd ? C : NDW_PACKED);
     }
 
     for (int64_t tb = t0; tb < t1; tb += P) {
@@ -212,13 +278,17 @@ __global__ __launch_bounds__(256) void k_sample(SampleParams p) {
           p.z[cbase + lane] = cn;
           cbase += 64;
           idx = 0;
-          cw = cwn;
-          cz = czn;
+          cw = w1;
+          cz = z1;
+          cf = f1;
+          w1 = w2;
+          z1 = z2;
+          if (PACKED) f1 = (int)wide_of[w1];
           cn = cz;
           cu = u01(draw_u32((uint64_t)(p.token_base + cbase + lane), p.c2, p.c3, p.k0, p.k1));
-          if (cbase + 64 + lane < t1) {
-            cwn = p.words[cbase + 64 + lane];
-            czn = p.z[cbase + 64 + lane];
+          if (cbase + 128 + lane < t1) {
+            w2 = p.words[cbase + 128 + lane];
+            z2 = p.z[cbase + 128 + lane];
           }
         }
         if (t == doc_end) {
@@ -238,6 +308,7 @@ __global__ __launch_bounds__(256) void k_sample(SampleParams p) {
         const int w = readlane_i(cw, idx);
         const int zo = readlane_i(cz, idx);
         const float u = readlane_f(cu, idx);
+        const bool wide = PACKED ? (readlane_i(cf, idx) != 0) : true;
         const int lo = zo / C, jo = zo % C;
         const bool own_old = (lane == lo);
 
@@ -251,7 +322,7 @@ __global__ __launch_bounds__(256) void k_sample(SampleParams p) {
         float acc = 0.0f;
 #pragma unroll
         for (int j = 0; j < C; ++j) {
-          int32_t c = rows[s][j];
+          int32_t c = row_count<C, PACKED>(rows[s], j, wide, lane);
           float iv = inv_r[j];
           if (!FROZEN) {
             const bool me = own_old && (j == jo);
@@ -297,8 +368,9 @@ __global__ __launch_bounds__(256) void k_sample(SampleParams p) {
         const int64_t tp = t + P;
         if (tp < t1) {
           const int pidx = (int)(tp - cbase);
-          const int wp = pidx < 64 ? readlane_i(cw, pidx) : readlane_i(cwn, pidx - 64);
-          load_row<C>(rows[s], nw + (int64_t)wp * KP + lane * C);
+          const int wp = pidx < 64 ? readlane_i(cw, pidx) : readlane_i(w1, pidx - 64);
+          const bool wd = PACKED ? ((pidx < 64 ? readlane_i(cf, pidx) : readlane_i(f1, pidx - 64)) != 0) : true;
+          load_raw<C>(rows[s], row_ptr<C, PACKED>(p, wp, wd, lane), wd ? C : NDW_PACKED);
         }
       }
     }
@@ -311,6 +383,26 @@ __global__ __launch_bounds__(256) void k_sample(SampleParams p) {
       const int v = bsum[i];
       if (v != 0) atomicAdd(&p.dsum[i], v);
     }
+  }
+}
+
+// 16-bit copy of nw (+ per-word "wide" flag when a count exceeds 65535).
+template <int C>
+__global__ __launch_bounds__(256) void k_build_packed(const int32_t* __restrict__ nw, int64_t V,
+                                                      uint16_t* __restrict__ nw16,
+                                                      uint8_t* __restrict__ wide) {
+  constexpr int KP = C * 64;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  for (int64_t w = (int64_t)blockIdx.x * 4 + wid; w < V; w += (int64_t)gridDim.x * 4) {
+    int32_t c[C];
+    load_row<C>(c, nw + w * KP + lane * C);
+    bool big = false;
+#pragma unroll
+    for (int j = 0; j < C; ++j) big |= (uint32_t)c[j] > 0xFFFFu;
+#pragma unroll
+    for (int j = 0; j < C; ++j) nw16[w * KP + lane * C + j] = (uint16_t)((uint32_t)c[j] > 0xFFFFu ? 0xFFFFu : c[j]);
+    const uint64_t any = __ballot(big);
+    if (lane == 0) wide[w] = any ? 1 : 0;
   }
 }
 
@@ -902,7 +994,10 @@ __global__ __launch_bounds__(256) void k_infer_init(const int32_t* __restrict__ 
 template <int C, int P, bool FROZEN>
 static hipError_t launch_sample_t(const SampleParams& p, int blocks, hipStream_t st) {
   const size_t lds = 5 * 64 * C * sizeof(int32_t);
-  hipLaunchKernelGGL((k_sample<C, P, FROZEN>), dim3(blocks), dim3(256), lds, st, p);
+  if (p.nw16 != nullptr)
+    hipLaunchKernelGGL((k_sample<C, P, FROZEN, true>), dim3(blocks), dim3(256), lds, st, p);
+  else
+    hipLaunchKernelGGL((k_sample<C, P, FROZEN, false>), dim3(blocks), dim3(256), lds, st, p);
   return hipGetLastError();
 }
 
@@ -910,7 +1005,7 @@ template <int C, int P, bool FROZEN>
 static int occupancy_t() {
   int nb = 0;
   const size_t lds = 5 * 64 * C * sizeof(int32_t);
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_sample<C, P, FROZEN>, 256, lds) !=
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_sample<C, P, FROZEN, true>, 256, lds) !=
       hipSuccess)
     return 1;
   return nb > 0 ? nb : 1;
@@ -1003,6 +1098,21 @@ hipError_t launch_build_sparse(const int32_t* nw, int64_t V, int32_t Kp, const i
     case 4: hipLaunchKernelGGL(k_build_sparse<4>, dim3(blocks), dim3(256), 0, st, nw, V, row_off, ent, row_nnz); break;
     case 8: hipLaunchKernelGGL(k_build_sparse<8>, dim3(blocks), dim3(256), 0, st, nw, V, row_off, ent, row_nnz); break;
     case 16: hipLaunchKernelGGL(k_build_sparse<16>, dim3(blocks), dim3(256), 0, st, nw, V, row_off, ent, row_nnz); break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+hipError_t launch_build_packed(const int32_t* nw, int64_t V, int32_t Kp, uint16_t* nw16,
+                               uint8_t* wide, hipStream_t st) {
+  if (V <= 0) return hipSuccess;
+  const int blocks = (int)std::min<int64_t>((V + 3) / 4, 16384);
+  switch (Kp / 64) {
+    case 1: hipLaunchKernelGGL(k_build_packed<1>, dim3(blocks), dim3(256), 0, st, nw, V, nw16, wide); break;
+    case 2: hipLaunchKernelGGL(k_build_packed<2>, dim3(blocks), dim3(256), 0, st, nw, V, nw16, wide); break;
+    case 4: hipLaunchKernelGGL(k_build_packed<4>, dim3(blocks), dim3(256), 0, st, nw, V, nw16, wide); break;
+    case 8: hipLaunchKernelGGL(k_build_packed<8>, dim3(blocks), dim3(256), 0, st, nw, V, nw16, wide); break;
+    case 16: hipLaunchKernelGGL(k_build_packed<16>, dim3(blocks), dim3(256), 0, st, nw, V, nw16, wide); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();

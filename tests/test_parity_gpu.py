@@ -32,11 +32,12 @@ def _pair(oracle, corpus, K, alpha, beta, seed, tokens_per_range=0, z_init=None,
     g = GibbsSampler(K, corpus.num_types, corpus.doc_off, corpus.words, alpha, beta, seed=seed,
                      z_init=z_init, tokens_per_range=tokens_per_range, sampler=kind)
     o = oracle.ExactSampler(K, corpus.num_types, corpus.doc_off, corpus.words, alpha, beta, seed,
-                            z_init=z_init, kind=kind)
+                            z_init=z_init, kind="sparse" if kind == "sparse" else "dense")
     return g, o
 
 
-KINDS = ["dense", "sparse"]
+# dense (16-bit rows + int32 escape), dense32 (int32 rows) share one oracle
+KINDS = ["dense", "dense32", "sparse"]
 
 
 def _assert_same_state(g, o, with_nd=True):
@@ -214,4 +215,21 @@ def test_sparse_saturated_counts(oracle):
     g.sweep(2)
     o.sweep(2)
     assert g.counts()[0].max() >= (1 << 20) - 1
+    _assert_same_state(g, o, with_nd=False)
+
+
+@pytest.mark.parametrize("kind", ["dense", "sparse"])
+def test_wide_rows_escape(oracle, kind):
+    """Counts above 65535 (packed dense: wide rows read the int32 row) and above
+    2^20 - 1 (sparse: saturated entries read the dense row)."""
+    from ldagibbssampling_amd.corpus import Corpus
+    D, L = 8, 40000
+    rng = np.random.default_rng(2)
+    words = np.where(rng.random(D * L) < 0.9, 0, rng.integers(1, 300, D * L)).astype(np.int32)
+    c = Corpus(np.arange(D + 1, dtype=np.int64) * L, words, 300)
+    K = 3
+    g, o = _pair(oracle, c, K, np.full(K, 0.1), 0.01, seed=4, kind=kind)
+    g.sweep(2)
+    o.sweep(2)
+    assert g.counts()[0].max() > 65535
     _assert_same_state(g, o, with_nd=False)
