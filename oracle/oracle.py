@@ -152,7 +152,7 @@ class ExactSampler:
                                          alpha, float(beta), int(seed) & (2**64 - 1), int(token_base))
         self.Kp = int(lib().orc_exact_kpad(self._h))
         self._pending = True      # create leaves the shard's counts as the pending delta
-        lib().orc_exact_set_kind(self._h, {"dense": 0, "sparse": 1}[kind])
+        lib().orc_exact_set_kind(self._h, {"dense": 0, "dense32": 0, "sparse": 1}[kind])
 
     def __del__(self):
         h = getattr(self, "_h", None)
