@@ -95,7 +95,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="c4", choices=sorted(CONFIGS))
     ap.add_argument("--docs", type=int, default=0, help="override docs per GPU")
-    ap.add_argument("--sampler", default="dense", choices=["dense", "sparse", "dense32"])
+    ap.add_argument("--sampler", default="dense", choices=["dense", "sparse"])
     ap.add_argument("--burnin", type=int, default=0,
                     help="extra untimed sweeps before the warm-up (steady-state measurement)")
     ap.add_argument("--no-cpu-baseline", action="store_true")

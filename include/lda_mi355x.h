@@ -49,18 +49,14 @@ typedef int32_t lda_status;
 
 #define LDA_MAX_TOPICS 1024       /* kernel instantiations: K <= 1024 */
 
-/* Draw kernels.  All are exact against the CPU oracle.
- *  DENSE   the dense draw; the word's whole row is read from a 16-bit copy of
- *          nw (2K bytes per token), or from the int32 row when it holds a
- *          count > 65535;
+/* Draw kernels.  Both are exact against the CPU oracle.
+ *  DENSE   reads the word's whole row of per-sweep fp32 word factors
+ *          (float(nw) + beta) * inv (4K bytes per token);
  *  SPARSE  reads only the row's nonzero (count, topic) entries (4 bytes each),
  *          SparseLDA-style split into a word part and a dense doc part
- *          (a different fp32 summation: its own oracle restatement);
- *  DENSE32 the dense draw on int32 rows only (4K bytes per token; same results
- *          as DENSE). */
+ *          (a different fp32 summation with its own oracle restatement). */
 #define LDA_SAMPLER_DENSE 0
 #define LDA_SAMPLER_SPARSE 1
-#define LDA_SAMPLER_DENSE32 2
 
 typedef struct lda_ctx lda_ctx;
 
@@ -72,7 +68,7 @@ typedef struct lda_config {
   double beta;            /* beta   (ParallelTopicModel(.., .., beta))         */
   uint64_t seed;          /* Philox key (ParallelTopicModel.setRandomSeed)     */
   int32_t device;         /* HIP device ordinal                                */
-  int32_t sampler;        /* LDA_SAMPLER_DENSE / _SPARSE / _DENSE32           */
+  int32_t sampler;        /* LDA_SAMPLER_DENSE (0) or LDA_SAMPLER_SPARSE (1)   */
   int64_t token_base;     /* global index of this shard's first token          */
   int64_t tokens_per_range; /* work-queue granule (0 = default)                */
 } lda_config;

@@ -24,7 +24,7 @@ STATUS_NAMES = {
     -5: "LDA_ERR_UNSUPPORTED",
 }
 MAX_TOPICS = 1024
-SAMPLERS = {"dense": 0, "sparse": 1, "dense32": 2}
+SAMPLERS = {"dense": 0, "sparse": 1}
 
 
 class LdaError(RuntimeError):

@@ -103,9 +103,8 @@ struct lda_ctx {
   int64_t* row_off = nullptr;
   int32_t* row_nnz = nullptr;
   bool rows_ready = false;
-  // packed dense rows (LDA_SAMPLER_DENSE)
-  uint16_t* nw16 = nullptr;
-  uint8_t* wide = nullptr;
+  // dense draw word factors (LDA_SAMPLER_DENSE)
+  float* btab = nullptr;
   int64_t tokens_per_range = 0;
   std::vector<int64_t> doc_off_h;
 
@@ -132,7 +131,7 @@ struct lda_ctx {
     for (void* p : {(void*)words, (void*)z, (void*)doc_off, (void*)range_doc, (void*)queue,
                     (void*)nw, (void*)nwsum, (void*)delta, (void*)alpha_d, (void*)alpha_f,
                     (void*)inv, (void*)inv_m1, (void*)partial, (void*)nonzero, (void*)ent,
-                    (void*)row_off, (void*)row_nnz, (void*)nw16, (void*)wide})
+                    (void*)row_off, (void*)row_nnz, (void*)btab})
       if (p) (void)hipFree(p);
     if (ev0) (void)hipEventDestroy(ev0);
     if (ev1) (void)hipEventDestroy(ev1);
@@ -163,8 +162,7 @@ struct lda_ctx {
     p.ent = ent;
     p.row_off = row_off;
     p.row_nnz = row_nnz;
-    p.nw16 = sampler == LDA_SAMPLER_DENSE ? nw16 : nullptr;
-    p.wide = sampler == LDA_SAMPLER_DENSE ? wide : nullptr;
+    p.btab = btab;
     (void)frozen;
     return p;
   }
@@ -205,8 +203,8 @@ static lda_status apply_impl(lda_ctx* c) {
       if (s) return s;
     }
     HIP_TRY(lda::launch_build_sparse(c->nw, c->V, c->Kp, c->row_off, c->ent, c->row_nnz, c->stream));
-  } else if (c->sampler == LDA_SAMPLER_DENSE) {
-    HIP_TRY(lda::launch_build_packed(c->nw, c->V, c->Kp, c->nw16, c->wide, c->stream));
+  } else {
+    HIP_TRY(lda::launch_build_btable(c->nw, c->V, c->Kp, (float)c->beta, c->inv, c->btab, c->stream));
   }
   c->pending = false;
   return LDA_OK;
@@ -240,9 +238,8 @@ lda_status lda_create(lda_ctx** out, const lda_config* cfg, const int64_t* doc_o
   if (cfg->num_docs < 0) return fail(LDA_ERR_INVALID_ARG, "num_docs must be >= 0");
   if (!cfg->alpha) return fail(LDA_ERR_INVALID_ARG, "alpha is null");
   if (!(cfg->beta > 0.0)) return fail(LDA_ERR_INVALID_ARG, "beta must be > 0");
-  if (cfg->sampler != LDA_SAMPLER_DENSE && cfg->sampler != LDA_SAMPLER_SPARSE &&
-      cfg->sampler != LDA_SAMPLER_DENSE32)
-    return fail(LDA_ERR_INVALID_ARG, "sampler must be LDA_SAMPLER_DENSE, _SPARSE or _DENSE32");
+  if (cfg->sampler != LDA_SAMPLER_DENSE && cfg->sampler != LDA_SAMPLER_SPARSE)
+    return fail(LDA_ERR_INVALID_ARG, "sampler must be LDA_SAMPLER_DENSE or LDA_SAMPLER_SPARSE");
   for (int k = 0; k < cfg->num_topics; ++k)
     if (!(cfg->alpha[k] > 0.0)) return fail(LDA_ERR_INVALID_ARG, "alpha must be > 0");
   const int64_t D = cfg->num_docs;
@@ -316,10 +313,7 @@ lda_status lda_create(lda_ctx** out, const lda_config* cfg, const int64_t* doc_o
   CT(dalloc(&c->queue, 4));
   CT(dalloc(&c->nw, (size_t)c->V * c->Kp));
   CT(dalloc(&c->nwsum, c->Kp));
-  if (c->sampler == LDA_SAMPLER_DENSE) {
-    CT(dalloc(&c->nw16, (size_t)c->V * c->Kp));
-    CT(dalloc(&c->wide, (size_t)c->V));
-  }
+  if (c->sampler == LDA_SAMPLER_DENSE) CT(dalloc(&c->btab, (size_t)c->V * c->Kp));
   CT(dalloc(&c->delta, (size_t)c->V * c->Kp + c->Kp));
   CT(dalloc(&c->alpha_d, c->K));
   CT(dalloc(&c->alpha_f, c->Kp));

@@ -125,93 +125,76 @@ __device__ __forceinline__ void load_row(int32_t (&r)[C], const int32_t* __restr
 // One wavefront walks one work range (a run of whole documents) at a time,
 // pulling ranges from a device queue.  The wave keeps a 64-token chunk of the
 // token stream in registers (lane i <-> token i of the chunk: word, old z,
-// Philox uniform, new z), the next two chunks' words/z ahead, and the nw rows
-// of the next P tokens in flight (the snapshot makes row loads independent of
-// the draws, so they pipeline across tokens and documents).
-//
-// PACKED: rows are read from the 16-bit copy nw16 (half the bytes) unless the
-// word's row holds a count > 65535 ("wide", flag gathered one chunk ahead),
-// in which case the int32 row is read.  Same counts, same arithmetic.
+// Philox uniform, new z), the next chunk's words/z one chunk ahead, and for
+// the next P tokens: the word's row of Bt = (float(nw) + beta) * inv (built
+// per sweep by k_build_btable), the int count nw[w][z_old] and inv_m1[z_old]
+// (the snapshot makes all of them independent of the draws, so they pipeline
+// across tokens and documents).  Per lane and topic the draw is one fma:
+//   S_j = fma(a_j, b_j, S_{j-1}),  a_j = float(nd_j) + alpha_j kept in
+// registers and refreshed only at the topic that changed; the z_old element
+// of lane z_old/C uses the corrected b computed once per token.
+
 template <int C>
-__device__ __forceinline__ void load_raw(uint32_t (&r)[C], const uint32_t* __restrict__ p, int ndw) {
-  // ndw = dwords this lane loads: C (int32 row) or C/2 (u16 row, C >= 2)
-  if constexpr (C >= 8) {
+__device__ __forceinline__ void load_brow(float (&r)[C], const float* __restrict__ p) {
+  if constexpr (C >= 4) {
 #pragma unroll
     for (int q = 0; q < C / 4; ++q) {
-      if (q * 4 < ndw) {
-        const uint4 v = reinterpret_cast<const uint4*>(p)[q];
-        r[4 * q + 0] = v.x;
-        r[4 * q + 1] = v.y;
-        r[4 * q + 2] = v.z;
-        r[4 * q + 3] = v.w;
-      }
-    }
-  } else if constexpr (C == 4) {
-    if (ndw == 4) {
-      const uint4 v = *reinterpret_cast<const uint4*>(p);
-      r[0] = v.x; r[1] = v.y; r[2] = v.z; r[3] = v.w;
-    } else {
-      const uint2 v = *reinterpret_cast<const uint2*>(p);
-      r[0] = v.x; r[1] = v.y;
+      const float4 v = reinterpret_cast<const float4*>(p)[q];
+      r[4 * q + 0] = v.x;
+      r[4 * q + 1] = v.y;
+      r[4 * q + 2] = v.z;
+      r[4 * q + 3] = v.w;
     }
   } else if constexpr (C == 2) {
-    if (ndw == 2) {
-      const uint2 v = *reinterpret_cast<const uint2*>(p);
-      r[0] = v.x; r[1] = v.y;
-    } else {
-      r[0] = p[0];
-    }
+    const float2 v = *reinterpret_cast<const float2*>(p);
+    r[0] = v.x;
+    r[1] = v.y;
   } else {
     r[0] = p[0];
   }
 }
 
-template <int C, bool PACKED>
-__device__ __forceinline__ const uint32_t* row_ptr(const SampleParams& p, int w, bool wide, int lane) {
-  if (PACKED && !wide) {
-    if constexpr (C == 1) {
-      // one u16 per lane: lanes pair up on a dword, the odd lane takes the high half
-      return reinterpret_cast<const uint32_t*>(p.nw16 + (int64_t)w * (C * 64)) + (lane >> 1);
-    } else {
-      return reinterpret_cast<const uint32_t*>(p.nw16 + (int64_t)w * (C * 64) + lane * C);
+template <int C>
+__device__ __forceinline__ void load_lds_f(float (&r)[C], const float* p) {
+  if constexpr (C >= 4) {
+#pragma unroll
+    for (int q = 0; q < C / 4; ++q) {
+      const float4 v = reinterpret_cast<const float4*>(p)[q];
+      r[4 * q + 0] = v.x;
+      r[4 * q + 1] = v.y;
+      r[4 * q + 2] = v.z;
+      r[4 * q + 3] = v.w;
     }
+  } else {
+#pragma unroll
+    for (int j = 0; j < C; ++j) r[j] = p[j];
   }
-  return reinterpret_cast<const uint32_t*>(p.nw + (int64_t)w * (C * 64) + lane * C);
 }
 
-template <int C, bool PACKED>
-__device__ __forceinline__ int32_t row_count(const uint32_t (&r)[C], int j, bool wide, int lane) {
-  if (PACKED && !wide) {
-    if constexpr (C == 1) return (int32_t)((lane & 1) ? (r[0] >> 16) : (r[0] & 0xFFFFu));
-    else return (int32_t)((j & 1) ? (r[j >> 1] >> 16) : (r[j >> 1] & 0xFFFFu));
-  }
-  return (int32_t)r[j];
-}
-
-template <int C, int P, bool FROZEN, bool PACKED>
+template <int C, int P, bool FROZEN>
 __global__ __launch_bounds__(256) void k_sample(SampleParams p) {
   extern __shared__ __attribute__((aligned(16))) int32_t smem[];
   constexpr int KP = C * 64;
-  constexpr int NDW_PACKED = C >= 2 ? C / 2 : 1;
   const int lane = threadIdx.x & 63;
   const int wid = threadIdx.x >> 6;
-  int32_t* hist = smem + wid * KP;  // per-wave doc-topic histogram scratch
-  int32_t* bsum = smem + 4 * KP;    // per-block nwsum delta
+  float* t_alpha = reinterpret_cast<float*>(smem);   // [KP] per block
+  int32_t* bsum = smem + KP;                         // [KP] per-block nwsum delta
+  int32_t* nd = smem + 2 * KP + wid * 2 * KP;        // [KP] per-wave live doc counts
+  float* av = reinterpret_cast<float*>(nd + KP);     // [KP] per-wave a_k = float(nd_k) + alpha_k
 
-  for (int i = threadIdx.x; i < 5 * KP; i += 256) smem[i] = 0;
+  for (int i = threadIdx.x; i < KP; i += 256) {
+    t_alpha[i] = p.alpha[i];
+    bsum[i] = 0;
+  }
+  for (int i = threadIdx.x; i < 8 * KP; i += 256) smem[2 * KP + i] = 0;
   __syncthreads();
 
-  float alpha_r[C], inv_r[C], invm1_r[C];
-#pragma unroll
-  for (int j = 0; j < C; ++j) {
-    alpha_r[j] = p.alpha[lane * C + j];
-    inv_r[j] = p.inv[lane * C + j];
-    invm1_r[j] = FROZEN ? 0.0f : p.inv_m1[lane * C + j];
-  }
   const float beta = p.beta;
   const int last_lane = (p.K - 1) / C;
-  const int last_j = (lane < last_lane) ? C - 1 : (p.K - 1) % C;
-  const uint8_t* __restrict__ wide_of = p.wide;
+  const int last_j_tail = (p.K - 1) % C;
+  const float* __restrict__ bt = p.btab;
+  const int32_t* __restrict__ nw = p.nw;
+  const float* __restrict__ inv_m1 = p.inv_m1;
 
   while (true) {
     int r = 0;
@@ -222,49 +205,46 @@ __global__ __launch_bounds__(256) void k_sample(SampleParams p) {
     const int64_t t0 = p.doc_off[d0], t1 = p.doc_off[d1];
     if (t1 <= t0) continue;
 
-    // --- chunk registers: chunk c (cw, cz, cu, cn, cf), c+1 (w1, z1, f1), c+2 (w2, z2)
+    // --- chunk registers
     int64_t cbase = t0;
-    int cw = 0, cz = 0, w1 = 0, z1 = 0, w2 = 0, z2 = 0;
+    int cw = 0, cz = 0, czn = 0, cwn = 0;
     if (t0 + lane < t1) {
       cw = p.words[t0 + lane];
       cz = p.z[t0 + lane];
     }
     if (t0 + 64 + lane < t1) {
-      w1 = p.words[t0 + 64 + lane];
-      z1 = p.z[t0 + 64 + lane];
+      cwn = p.words[t0 + 64 + lane];
+      czn = p.z[t0 + 64 + lane];
     }
-    if (t0 + 128 + lane < t1) {
-      w2 = p.words[t0 + 128 + lane];
-      z2 = p.z[t0 + 128 + lane];
-    }
-    int cf = PACKED ? (int)wide_of[cw] : 1, f1 = PACKED ? (int)wide_of[w1] : 1;
     int cn = cz;
     float cu = u01(draw_u32((uint64_t)(p.token_base + t0 + lane), p.c2, p.c3, p.k0, p.k1));
 
-    // --- first document of the range
+    // --- first document of the range (nd is all zero here)
     int64_t doc = d0;
     while (p.doc_off[doc + 1] <= t0) ++doc;
     int64_t doc_end = p.doc_off[doc + 1];
-    float ndv[C];
     {
-      for (int64_t i = t0 + lane; i < doc_end; i += 64) atomicAdd(&hist[p.z[i]], 1);
+      for (int64_t i = t0 + lane; i < doc_end; i += 64) atomicAdd(&nd[p.z[i]], 1);
       wave_lds_fence();
 #pragma unroll
-      for (int j = 0; j < C; ++j) {
-        ndv[j] = (float)hist[lane * C + j];
-        hist[lane * C + j] = 0;
-      }
+      for (int j = 0; j < C; ++j) av[lane * C + j] = (float)nd[lane * C + j] + t_alpha[lane * C + j];
       wave_lds_fence();
     }
 
-    // --- prime the row pipeline
-    uint32_t rows[P][C];
+    // --- prime the pipeline: Bt rows (+ z_old count and inv_m1) of P tokens
+    float rows[P][C];
+    int ccnt[P];
+    float cinv[P];
 #pragma unroll
     for (int s = 0; s < P; ++s) {
       const int64_t tp = t0 + s;
       const int wp = (tp < t1) ? readlane_i(cw, s) : 0;
-      const bool wd = PACKED ? (readlane_i(cf, s) != 0) : true;
-      load_raw<C>(rows[s], row_ptr<C, PACKED>(p, wp, wd, lane), wd ? C : NDW_PACKED);
+      const int zp = (tp < t1) ? readlane_i(cz, s) : 0;
+      load_brow<C>(rows[s], bt + (int64_t)wp * KP + lane * C);
+      if (!FROZEN) {
+        ccnt[s] = nw[(int64_t)wp * KP + zp];
+        cinv[s] = inv_m1[zp];
+      }
     }
 
     for (int64_t tb = t0; tb < t1; tb += P) {
@@ -278,60 +258,56 @@ __global__ __launch_bounds__(256) void k_sample(SampleParams p) {
           p.z[cbase + lane] = cn;
           cbase += 64;
           idx = 0;
-          cw = w1;
-          cz = z1;
-          cf = f1;
-          w1 = w2;
-          z1 = z2;
-          if (PACKED) f1 = (int)wide_of[w1];
+          cw = cwn;
+          cz = czn;
           cn = cz;
           cu = u01(draw_u32((uint64_t)(p.token_base + cbase + lane), p.c2, p.c3, p.k0, p.k1));
-          if (cbase + 128 + lane < t1) {
-            w2 = p.words[cbase + 128 + lane];
-            z2 = p.z[cbase + 128 + lane];
+          if (cbase + 64 + lane < t1) {
+            cwn = p.words[cbase + 64 + lane];
+            czn = p.z[cbase + 64 + lane];
           }
         }
         if (t == doc_end) {
+#pragma unroll
+          for (int j = 0; j < C; ++j) nd[lane * C + j] = 0;
+          wave_lds_fence();
           ++doc;
           while (p.doc_off[doc + 1] <= t) ++doc;
           doc_end = p.doc_off[doc + 1];
-          for (int64_t i = t + lane; i < doc_end; i += 64) atomicAdd(&hist[p.z[i]], 1);
+          for (int64_t i = t + lane; i < doc_end; i += 64) atomicAdd(&nd[p.z[i]], 1);
           wave_lds_fence();
 #pragma unroll
-          for (int j = 0; j < C; ++j) {
-            ndv[j] = (float)hist[lane * C + j];
-            hist[lane * C + j] = 0;
-          }
+          for (int j = 0; j < C; ++j) av[lane * C + j] = (float)nd[lane * C + j] + t_alpha[lane * C + j];
           wave_lds_fence();
         }
 
         const int w = readlane_i(cw, idx);
         const int zo = readlane_i(cz, idx);
         const float u = readlane_f(cu, idx);
-        const bool wide = PACKED ? (readlane_i(cf, idx) != 0) : true;
         const int lo = zo / C, jo = zo % C;
+
+        // remove the token from its document (uniform address: lane 0 writes)
+        {
+          const int ndz = nd[zo] - 1;
+          const float az = (float)ndz + t_alpha[zo];
+          if (lane == 0) {
+            nd[zo] = ndz;
+            av[zo] = az;
+          }
+          wave_lds_fence();
+        }
+        float a[C];
+        load_lds_f<C>(a, av + lane * C);
+        const float bc = FROZEN ? 0.0f : ((float)(ccnt[s] - 1) + beta) * cinv[s];
         const bool own_old = (lane == lo);
 
-        // remove the token from its document
-#pragma unroll
-        for (int j = 0; j < C; ++j)
-          if (j == jo) ndv[j] = own_old ? ndv[j] - 1.0f : ndv[j];
-
-        // weights and the lane-serial prefix
+        // lane-serial fma prefix (the z_old element of lane lo uses bc)
         float S[C];
         float acc = 0.0f;
 #pragma unroll
         for (int j = 0; j < C; ++j) {
-          int32_t c = row_count<C, PACKED>(rows[s], j, wide, lane);
-          float iv = inv_r[j];
-          if (!FROZEN) {
-            const bool me = own_old && (j == jo);
-            c = me ? c - 1 : c;
-            iv = me ? invm1_r[j] : iv;
-          }
-          const float b = ((float)c + beta) * iv;
-          const float a = ndv[j] + alpha_r[j];
-          acc = __builtin_fmaf(a, b, acc);
+          const float b = (!FROZEN && j == jo && own_old) ? bc : rows[s][j];
+          acc = __builtin_fmaf(a[j], b, acc);
           S[j] = acc;
         }
 
@@ -344,16 +320,20 @@ __global__ __launch_bounds__(256) void k_sample(SampleParams p) {
         const float E = lstar > 0 ? readlane_f(T, lstar - 1) : 0.0f;
         int cnt = 0;
 #pragma unroll
-        for (int j = 0; j < C; ++j) cnt += (E + S[j] <= thr) ? 1 : 0;
-        const int jsel = cnt < C ? cnt : last_j;
-        const int jn = readlane_i(jsel, lstar);
-        const int kn = lstar * C + jn;
+        for (int j = 0; j < C; ++j) cnt += (int)((__ballot(E + S[j] <= thr) >> lstar) & 1ull);
+        const int jsel = cnt < C ? cnt : (lstar < last_lane ? C - 1 : last_j_tail);
+        const int kn = lstar * C + jsel;
 
         // add the token back under its new topic
-        const bool own_new = (lane == lstar);
-#pragma unroll
-        for (int j = 0; j < C; ++j)
-          if (j == jn) ndv[j] = own_new ? ndv[j] + 1.0f : ndv[j];
+        {
+          const int ndk = nd[kn] + 1;
+          const float ak = (float)ndk + t_alpha[kn];
+          if (lane == 0) {
+            nd[kn] = ndk;
+            av[kn] = ak;
+          }
+          wave_lds_fence();
+        }
         cn = (lane == idx) ? kn : cn;
         if (!FROZEN && kn != zo) {
           if (lane < 2) {
@@ -364,17 +344,24 @@ __global__ __launch_bounds__(256) void k_sample(SampleParams p) {
           }
         }
 
-        // keep the pipeline full: row of token t+P
+        // keep the pipeline full: token t+P
         const int64_t tp = t + P;
         if (tp < t1) {
           const int pidx = (int)(tp - cbase);
-          const int wp = pidx < 64 ? readlane_i(cw, pidx) : readlane_i(w1, pidx - 64);
-          const bool wd = PACKED ? ((pidx < 64 ? readlane_i(cf, pidx) : readlane_i(f1, pidx - 64)) != 0) : true;
-          load_raw<C>(rows[s], row_ptr<C, PACKED>(p, wp, wd, lane), wd ? C : NDW_PACKED);
+          const int wp = pidx < 64 ? readlane_i(cw, pidx) : readlane_i(cwn, pidx - 64);
+          load_brow<C>(rows[s], bt + (int64_t)wp * KP + lane * C);
+          if (!FROZEN) {
+            const int zp = pidx < 64 ? readlane_i(cz, pidx) : readlane_i(czn, pidx - 64);
+            ccnt[s] = nw[(int64_t)wp * KP + zp];
+            cinv[s] = inv_m1[zp];
+          }
         }
       }
     }
     if (cbase + lane < t1) p.z[cbase + lane] = cn;
+#pragma unroll
+    for (int j = 0; j < C; ++j) nd[lane * C + j] = 0;
+    wave_lds_fence();
   }
 
   if (!FROZEN) {
@@ -386,23 +373,21 @@ __global__ __launch_bounds__(256) void k_sample(SampleParams p) {
   }
 }
 
-// 16-bit copy of nw (+ per-word "wide" flag when a count exceeds 65535).
-template <int C>
-__global__ __launch_bounds__(256) void k_build_packed(const int32_t* __restrict__ nw, int64_t V,
-                                                      uint16_t* __restrict__ nw16,
-                                                      uint8_t* __restrict__ wide) {
-  constexpr int KP = C * 64;
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  for (int64_t w = (int64_t)blockIdx.x * 4 + wid; w < V; w += (int64_t)gridDim.x * 4) {
-    int32_t c[C];
-    load_row<C>(c, nw + w * KP + lane * C);
-    bool big = false;
-#pragma unroll
-    for (int j = 0; j < C; ++j) big |= (uint32_t)c[j] > 0xFFFFu;
-#pragma unroll
-    for (int j = 0; j < C; ++j) nw16[w * KP + lane * C + j] = (uint16_t)((uint32_t)c[j] > 0xFFFFu ? 0xFFFFu : c[j]);
-    const uint64_t any = __ballot(big);
-    if (lane == 0) wide[w] = any ? 1 : 0;
+// Bt[w][k] = (float(nw[w][k]) + beta) * inv[k]: the word factor of the dense
+// draw for the snapshot (padded topics: inv = 0 -> 0).
+__global__ __launch_bounds__(256) void k_build_btable(const int4* __restrict__ nw, int64_t n4,
+                                                      int32_t Kp, float beta,
+                                                      const float* __restrict__ inv,
+                                                      float4* __restrict__ bt) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += (int64_t)gridDim.x * 256) {
+    const int4 c = nw[i];
+    const int k = (int)((i * 4) % Kp);
+    float4 o;
+    o.x = ((float)c.x + beta) * inv[k + 0];
+    o.y = ((float)c.y + beta) * inv[k + 1];
+    o.z = ((float)c.z + beta) * inv[k + 2];
+    o.w = ((float)c.w + beta) * inv[k + 3];
+    bt[i] = o;
   }
 }
 
@@ -993,19 +978,16 @@ __global__ __launch_bounds__(256) void k_infer_init(const int32_t* __restrict__ 
 // ------------------------------------------------------------- launchers
 template <int C, int P, bool FROZEN>
 static hipError_t launch_sample_t(const SampleParams& p, int blocks, hipStream_t st) {
-  const size_t lds = 5 * 64 * C * sizeof(int32_t);
-  if (p.nw16 != nullptr)
-    hipLaunchKernelGGL((k_sample<C, P, FROZEN, true>), dim3(blocks), dim3(256), lds, st, p);
-  else
-    hipLaunchKernelGGL((k_sample<C, P, FROZEN, false>), dim3(blocks), dim3(256), lds, st, p);
+  const size_t lds = 10 * 64 * C * sizeof(int32_t);
+  hipLaunchKernelGGL((k_sample<C, P, FROZEN>), dim3(blocks), dim3(256), lds, st, p);
   return hipGetLastError();
 }
 
 template <int C, int P, bool FROZEN>
 static int occupancy_t() {
   int nb = 0;
-  const size_t lds = 5 * 64 * C * sizeof(int32_t);
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_sample<C, P, FROZEN, true>, 256, lds) !=
+  const size_t lds = 10 * 64 * C * sizeof(int32_t);
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_sample<C, P, FROZEN>, 256, lds) !=
       hipSuccess)
     return 1;
   return nb > 0 ? nb : 1;
@@ -1103,18 +1085,14 @@ hipError_t launch_build_sparse(const int32_t* nw, int64_t V, int32_t Kp, const i
   return hipGetLastError();
 }
 
-hipError_t launch_build_packed(const int32_t* nw, int64_t V, int32_t Kp, uint16_t* nw16,
-                               uint8_t* wide, hipStream_t st) {
-  if (V <= 0) return hipSuccess;
-  const int blocks = (int)std::min<int64_t>((V + 3) / 4, 16384);
-  switch (Kp / 64) {
-    case 1: hipLaunchKernelGGL(k_build_packed<1>, dim3(blocks), dim3(256), 0, st, nw, V, nw16, wide); break;
-    case 2: hipLaunchKernelGGL(k_build_packed<2>, dim3(blocks), dim3(256), 0, st, nw, V, nw16, wide); break;
-    case 4: hipLaunchKernelGGL(k_build_packed<4>, dim3(blocks), dim3(256), 0, st, nw, V, nw16, wide); break;
-    case 8: hipLaunchKernelGGL(k_build_packed<8>, dim3(blocks), dim3(256), 0, st, nw, V, nw16, wide); break;
-    case 16: hipLaunchKernelGGL(k_build_packed<16>, dim3(blocks), dim3(256), 0, st, nw, V, nw16, wide); break;
-    default: return hipErrorInvalidValue;
-  }
+hipError_t launch_build_btable(const int32_t* nw, int64_t V, int32_t Kp, float beta,
+                               const float* inv, float* bt, hipStream_t st) {
+  const int64_t n4 = V * Kp / 4;
+  if (n4 <= 0) return hipSuccess;
+  const int blocks = (int)std::min<int64_t>((n4 + 255) / 256, 8192);
+  hipLaunchKernelGGL(k_build_btable, dim3(blocks), dim3(256), 0, st,
+                     reinterpret_cast<const int4*>(nw), n4, Kp, beta, inv,
+                     reinterpret_cast<float4*>(bt));
   return hipGetLastError();
 }
 

@@ -3,7 +3,7 @@ cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out
 timeout -k 10 1200 python -m pytest tests -m gpu -x -q -k "not perplexity" > gpurun_out/pytest_gpu.log 2>&1 || { echo "PYTEST FAILED rc=$?"; tail -60 gpurun_out/pytest_gpu.log; exit 1; }
 echo "pytest ok"; tail -2 gpurun_out/pytest_gpu.log
-for smp in dense dense32 sparse; do
+for smp in dense sparse; do
   timeout -k 10 600 python bench.py --sampler $smp --no-cpu-baseline --steps 5 --warmup 2 > gpurun_out/bench_$smp.log 2>&1 || { echo BENCH $smp FAILED; tail -20 gpurun_out/bench_$smp.log; exit 1; }
   python -c "import json;d=json.loads(open('gpurun_out/bench_$smp.log').read().strip().splitlines()[-1]);print('$smp', d['value']/1e9, 'Gtok/s', d['roofline']['kernel'])"
 done
