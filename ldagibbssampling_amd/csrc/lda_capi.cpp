@@ -523,11 +523,14 @@ lda_status lda_set_alpha_beta(lda_ctx* c, const double* alpha, double beta) {
   c->alpha.assign(alpha, alpha + c->K);
   c->beta = beta;
   HIP_TRY(hipMemcpyAsync(c->alpha_d, c->alpha.data(), sizeof(double) * c->K, hipMemcpyHostToDevice, c->stream));
-  // refresh the fp32 tables (the nwsum delta part is zero unless pending)
+  // refresh the fp32 tables (the nwsum delta part is zero unless pending);
+  // the dense word factors depend on beta and inv, so they are rebuilt too
   if (!c->pending) {
     HIP_TRY(lda::launch_prepare_topics(c->nwsum, c->delta + (int64_t)c->V * c->Kp, c->alpha_d,
                                        c->beta, (double)c->V * c->beta, c->K, c->Kp, c->alpha_f,
                                        c->inv, c->inv_m1, c->stream));
+    if (c->sampler == LDA_SAMPLER_DENSE)
+      HIP_TRY(lda::launch_build_btable(c->nw, c->V, c->Kp, (float)c->beta, c->inv, c->btab, c->stream));
   }
   HIP_TRY(hipStreamSynchronize(c->stream));
   return LDA_OK;
