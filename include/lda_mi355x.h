@@ -50,8 +50,8 @@ typedef int32_t lda_status;
 #define LDA_MAX_TOPICS 1024       /* kernel instantiations: K <= 1024 */
 
 /* Draw kernels.  Both are exact against the CPU oracle.
- *  DENSE   reads the word's whole row of per-sweep fp32 word factors
- *          (float(nw) + beta) * inv (4K bytes per token);
+ *  DENSE   reads the word's whole row from a 16-bit copy of nw (2K bytes per
+ *          token; the int32 row for words with a count > 65535);
  *  SPARSE  reads only the row's nonzero (count, topic) entries (4 bytes each),
  *          SparseLDA-style split into a word part and a dense doc part
  *          (a different fp32 summation with its own oracle restatement). */

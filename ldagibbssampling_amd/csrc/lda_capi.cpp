@@ -103,8 +103,9 @@ struct lda_ctx {
   int64_t* row_off = nullptr;
   int32_t* row_nnz = nullptr;
   bool rows_ready = false;
-  // dense draw word factors (LDA_SAMPLER_DENSE)
-  float* btab = nullptr;
+  // 16-bit rows of the snapshot (LDA_SAMPLER_DENSE)
+  uint16_t* nw16 = nullptr;
+  uint8_t* wide = nullptr;
   int64_t tokens_per_range = 0;
   std::vector<int64_t> doc_off_h;
 
@@ -131,7 +132,7 @@ struct lda_ctx {
     for (void* p : {(void*)words, (void*)z, (void*)doc_off, (void*)range_doc, (void*)queue,
                     (void*)nw, (void*)nwsum, (void*)delta, (void*)alpha_d, (void*)alpha_f,
                     (void*)inv, (void*)inv_m1, (void*)partial, (void*)nonzero, (void*)ent,
-                    (void*)row_off, (void*)row_nnz, (void*)btab})
+                    (void*)row_off, (void*)row_nnz, (void*)nw16, (void*)wide})
       if (p) (void)hipFree(p);
     if (ev0) (void)hipEventDestroy(ev0);
     if (ev1) (void)hipEventDestroy(ev1);
@@ -162,7 +163,8 @@ struct lda_ctx {
     p.ent = ent;
     p.row_off = row_off;
     p.row_nnz = row_nnz;
-    p.btab = btab;
+    p.nw16 = nw16;
+    p.wide = wide;
     (void)frozen;
     return p;
   }
@@ -204,7 +206,7 @@ static lda_status apply_impl(lda_ctx* c) {
     }
     HIP_TRY(lda::launch_build_sparse(c->nw, c->V, c->Kp, c->row_off, c->ent, c->row_nnz, c->stream));
   } else {
-    HIP_TRY(lda::launch_build_btable(c->nw, c->V, c->Kp, (float)c->beta, c->inv, c->btab, c->stream));
+    HIP_TRY(lda::launch_build_packed(c->nw, c->V, c->Kp, c->nw16, c->wide, c->stream));
   }
   c->pending = false;
   return LDA_OK;
@@ -313,7 +315,10 @@ lda_status lda_create(lda_ctx** out, const lda_config* cfg, const int64_t* doc_o
   CT(dalloc(&c->queue, 4));
   CT(dalloc(&c->nw, (size_t)c->V * c->Kp));
   CT(dalloc(&c->nwsum, c->Kp));
-  if (c->sampler == LDA_SAMPLER_DENSE) CT(dalloc(&c->btab, (size_t)c->V * c->Kp));
+  if (c->sampler == LDA_SAMPLER_DENSE) {
+    CT(dalloc(&c->nw16, (size_t)c->V * c->Kp));
+    CT(dalloc(&c->wide, (size_t)c->V));
+  }
   CT(dalloc(&c->delta, (size_t)c->V * c->Kp + c->Kp));
   CT(dalloc(&c->alpha_d, c->K));
   CT(dalloc(&c->alpha_f, c->Kp));
@@ -523,14 +528,12 @@ lda_status lda_set_alpha_beta(lda_ctx* c, const double* alpha, double beta) {
   c->alpha.assign(alpha, alpha + c->K);
   c->beta = beta;
   HIP_TRY(hipMemcpyAsync(c->alpha_d, c->alpha.data(), sizeof(double) * c->K, hipMemcpyHostToDevice, c->stream));
-  // refresh the fp32 tables (the nwsum delta part is zero unless pending);
-  // the dense word factors depend on beta and inv, so they are rebuilt too
+  // refresh the fp32 tables (the nwsum delta part is zero unless pending)
   if (!c->pending) {
     HIP_TRY(lda::launch_prepare_topics(c->nwsum, c->delta + (int64_t)c->V * c->Kp, c->alpha_d,
                                        c->beta, (double)c->V * c->beta, c->K, c->Kp, c->alpha_f,
                                        c->inv, c->inv_m1, c->stream));
-    if (c->sampler == LDA_SAMPLER_DENSE)
-      HIP_TRY(lda::launch_build_btable(c->nw, c->V, c->Kp, (float)c->beta, c->inv, c->btab, c->stream));
+
   }
   HIP_TRY(hipStreamSynchronize(c->stream));
   return LDA_OK;

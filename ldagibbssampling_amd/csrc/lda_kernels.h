@@ -45,8 +45,9 @@ struct SampleParams {
   const int64_t* row_off;   // [V+1] capacity offsets (min(Kp, word total) per row)
   const int32_t* row_nnz;   // [V] live entries per row
   float* trace;             // debug only: 8 floats per token when non-null
-  // dense draw word factors of the snapshot (k_sample)
-  const float* btab;        // [V*Kp] (float(nw) + beta) * inv
+  // 16-bit copy of the snapshot rows (k_sample)
+  const uint16_t* nw16;     // [V*Kp] counts, clamped at 65535
+  const uint8_t* wide;      // [V] 1 when the row holds a count > 65535 (read nw)
 };
 
 // Sparse-row packing: 12 topic bits (K <= 4096), 20 count bits; a saturated
@@ -64,8 +65,8 @@ int sample_sparse_blocks_per_cu(int C, bool frozen);
 hipError_t launch_row_caps(const int32_t* nw, int64_t V, int32_t Kp, int32_t* caps, hipStream_t st);
 hipError_t launch_build_sparse(const int32_t* nw, int64_t V, int32_t Kp, const int64_t* row_off,
                                uint32_t* ent, int32_t* row_nnz, hipStream_t st);
-hipError_t launch_build_btable(const int32_t* nw, int64_t V, int32_t Kp, float beta,
-                               const float* inv, float* bt, hipStream_t st);
+hipError_t launch_build_packed(const int32_t* nw, int64_t V, int32_t Kp, uint16_t* nw16,
+                               uint8_t* wide, hipStream_t st);
 hipError_t launch_init_z(int32_t* z, int64_t n, int32_t K, int64_t token_base, uint32_t k0,
                          uint32_t k1, hipStream_t st);
 hipError_t launch_count(const int32_t* words, const int32_t* z, int64_t n, int32_t Kp,

@@ -171,10 +171,41 @@ __device__ __forceinline__ void load_lds_f(float (&r)[C], const float* p) {
   }
 }
 
+// Row of 16-bit counts: C u16 per lane = C/2 dwords (C >= 2), one u16 for C = 1.
+template <int C>
+__device__ __forceinline__ void load_row16(uint32_t (&r)[(C + 1) / 2], const uint16_t* __restrict__ row,
+                                           int lane) {
+  if constexpr (C >= 8) {
+#pragma unroll
+    for (int q = 0; q < C / 8; ++q) {
+      const uint4 v = reinterpret_cast<const uint4*>(row + lane * C)[q];
+      r[4 * q + 0] = v.x;
+      r[4 * q + 1] = v.y;
+      r[4 * q + 2] = v.z;
+      r[4 * q + 3] = v.w;
+    }
+  } else if constexpr (C == 4) {
+    const uint2 v = *reinterpret_cast<const uint2*>(row + lane * C);
+    r[0] = v.x;
+    r[1] = v.y;
+  } else if constexpr (C == 2) {
+    r[0] = *reinterpret_cast<const uint32_t*>(row + lane * C);
+  } else {
+    r[0] = row[lane];
+  }
+}
+
+template <int C>
+__device__ __forceinline__ int32_t row16_count(const uint32_t (&r)[(C + 1) / 2], int j) {
+  if constexpr (C == 1) return (int32_t)r[0];
+  else return (int32_t)((j & 1) ? (r[j >> 1] >> 16) : (r[j >> 1] & 0xFFFFu));
+}
+
 template <int C, int P, bool FROZEN>
 __global__ __launch_bounds__(256) void k_sample(SampleParams p) {
   extern __shared__ __attribute__((aligned(16))) int32_t smem[];
   constexpr int KP = C * 64;
+  constexpr int H = (C + 1) / 2;                     // dwords of a 16-bit row per lane
   const int lane = threadIdx.x & 63;
   const int wid = threadIdx.x >> 6;
   float* t_alpha = reinterpret_cast<float*>(smem);   // [KP] per block
@@ -189,10 +220,14 @@ __global__ __launch_bounds__(256) void k_sample(SampleParams p) {
   for (int i = threadIdx.x; i < 8 * KP; i += 256) smem[2 * KP + i] = 0;
   __syncthreads();
 
+  float inv_r[C];
+#pragma unroll
+  for (int j = 0; j < C; ++j) inv_r[j] = p.inv[lane * C + j];
   const float beta = p.beta;
   const int last_lane = (p.K - 1) / C;
   const int last_j_tail = (p.K - 1) % C;
-  const float* __restrict__ bt = p.btab;
+  const uint16_t* __restrict__ nw16 = p.nw16;
+  const uint8_t* __restrict__ wide_of = p.wide;
   const int32_t* __restrict__ nw = p.nw;
   const float* __restrict__ inv_m1 = p.inv_m1;
 
@@ -205,17 +240,23 @@ __global__ __launch_bounds__(256) void k_sample(SampleParams p) {
     const int64_t t0 = p.doc_off[d0], t1 = p.doc_off[d1];
     if (t1 <= t0) continue;
 
-    // --- chunk registers
+    // --- chunk registers: chunk c (cw, cz, cu, cn, cf), c+1 (w1, z1, f1), c+2 (w2, z2);
+    // f = 1 when the word's row holds a count > 65535 (read the int32 row)
     int64_t cbase = t0;
-    int cw = 0, cz = 0, czn = 0, cwn = 0;
+    int cw = 0, cz = 0, w1 = 0, z1 = 0, w2 = 0, z2 = 0;
     if (t0 + lane < t1) {
       cw = p.words[t0 + lane];
       cz = p.z[t0 + lane];
     }
     if (t0 + 64 + lane < t1) {
-      cwn = p.words[t0 + 64 + lane];
-      czn = p.z[t0 + 64 + lane];
+      w1 = p.words[t0 + 64 + lane];
+      z1 = p.z[t0 + 64 + lane];
     }
+    if (t0 + 128 + lane < t1) {
+      w2 = p.words[t0 + 128 + lane];
+      z2 = p.z[t0 + 128 + lane];
+    }
+    int cf = (int)wide_of[cw], f1 = (int)wide_of[w1];
     int cn = cz;
     float cu = u01(draw_u32((uint64_t)(p.token_base + t0 + lane), p.c2, p.c3, p.k0, p.k1));
 
@@ -231,8 +272,8 @@ __global__ __launch_bounds__(256) void k_sample(SampleParams p) {
       wave_lds_fence();
     }
 
-    // --- prime the pipeline: Bt rows (+ z_old count and inv_m1) of P tokens
-    float rows[P][C];
+    // --- prime the pipeline: 16-bit rows (+ z_old count and inv_m1) of P tokens
+    uint32_t rows[P][H];
     int ccnt[P];
     float cinv[P];
 #pragma unroll
@@ -240,7 +281,7 @@ __global__ __launch_bounds__(256) void k_sample(SampleParams p) {
       const int64_t tp = t0 + s;
       const int wp = (tp < t1) ? readlane_i(cw, s) : 0;
       const int zp = (tp < t1) ? readlane_i(cz, s) : 0;
-      load_brow<C>(rows[s], bt + (int64_t)wp * KP + lane * C);
+      load_row16<C>(rows[s], nw16 + (int64_t)wp * KP, lane);
       if (!FROZEN) {
         ccnt[s] = nw[(int64_t)wp * KP + zp];
         cinv[s] = inv_m1[zp];
@@ -258,13 +299,17 @@ __global__ __launch_bounds__(256) void k_sample(SampleParams p) {
           p.z[cbase + lane] = cn;
           cbase += 64;
           idx = 0;
-          cw = cwn;
-          cz = czn;
+          cw = w1;
+          cz = z1;
+          cf = f1;
+          w1 = w2;
+          z1 = z2;
+          f1 = (int)wide_of[w1];
           cn = cz;
           cu = u01(draw_u32((uint64_t)(p.token_base + cbase + lane), p.c2, p.c3, p.k0, p.k1));
-          if (cbase + 64 + lane < t1) {
-            cwn = p.words[cbase + 64 + lane];
-            czn = p.z[cbase + 64 + lane];
+          if (cbase + 128 + lane < t1) {
+            w2 = p.words[cbase + 128 + lane];
+            z2 = p.z[cbase + 128 + lane];
           }
         }
         if (t == doc_end) {
@@ -284,6 +329,7 @@ __global__ __launch_bounds__(256) void k_sample(SampleParams p) {
         const int w = readlane_i(cw, idx);
         const int zo = readlane_i(cz, idx);
         const float u = readlane_f(cu, idx);
+        const bool wide = readlane_i(cf, idx) != 0;
         const int lo = zo / C, jo = zo % C;
 
         // remove the token from its document (uniform address: lane 0 writes)
@@ -301,12 +347,25 @@ __global__ __launch_bounds__(256) void k_sample(SampleParams p) {
         const float bc = FROZEN ? 0.0f : ((float)(ccnt[s] - 1) + beta) * cinv[s];
         const bool own_old = (lane == lo);
 
+        // word factors b = (float(c) + beta) * inv; rows with a count > 65535
+        // come from the int32 row instead (rare: uniform branch, not prefetched)
+        int32_t cfull[C];
+        if (wide) {
+          const int32_t* wr = nw + (int64_t)w * KP + lane * C;
+#pragma unroll
+          for (int j = 0; j < C; ++j) cfull[j] = wr[j];
+        } else {
+#pragma unroll
+          for (int j = 0; j < C; ++j) cfull[j] = row16_count<C>(rows[s], j);
+        }
+
         // lane-serial fma prefix (the z_old element of lane lo uses bc)
         float S[C];
         float acc = 0.0f;
 #pragma unroll
         for (int j = 0; j < C; ++j) {
-          const float b = (!FROZEN && j == jo && own_old) ? bc : rows[s][j];
+          const float bj = ((float)cfull[j] + beta) * inv_r[j];
+          const float b = (!FROZEN && j == jo && own_old) ? bc : bj;
           acc = __builtin_fmaf(a[j], b, acc);
           S[j] = acc;
         }
@@ -348,10 +407,10 @@ __global__ __launch_bounds__(256) void k_sample(SampleParams p) {
         const int64_t tp = t + P;
         if (tp < t1) {
           const int pidx = (int)(tp - cbase);
-          const int wp = pidx < 64 ? readlane_i(cw, pidx) : readlane_i(cwn, pidx - 64);
-          load_brow<C>(rows[s], bt + (int64_t)wp * KP + lane * C);
+          const int wp = pidx < 64 ? readlane_i(cw, pidx) : readlane_i(w1, pidx - 64);
+          load_row16<C>(rows[s], nw16 + (int64_t)wp * KP, lane);
           if (!FROZEN) {
-            const int zp = pidx < 64 ? readlane_i(cz, pidx) : readlane_i(czn, pidx - 64);
+            const int zp = pidx < 64 ? readlane_i(cz, pidx) : readlane_i(z1, pidx - 64);
             ccnt[s] = nw[(int64_t)wp * KP + zp];
             cinv[s] = inv_m1[zp];
           }
@@ -373,21 +432,24 @@ __global__ __launch_bounds__(256) void k_sample(SampleParams p) {
   }
 }
 
-// Bt[w][k] = (float(nw[w][k]) + beta) * inv[k]: the word factor of the dense
-// draw for the snapshot (padded topics: inv = 0 -> 0).
-__global__ __launch_bounds__(256) void k_build_btable(const int4* __restrict__ nw, int64_t n4,
-                                                      int32_t Kp, float beta,
-                                                      const float* __restrict__ inv,
-                                                      float4* __restrict__ bt) {
-  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += (int64_t)gridDim.x * 256) {
-    const int4 c = nw[i];
-    const int k = (int)((i * 4) % Kp);
-    float4 o;
-    o.x = ((float)c.x + beta) * inv[k + 0];
-    o.y = ((float)c.y + beta) * inv[k + 1];
-    o.z = ((float)c.z + beta) * inv[k + 2];
-    o.w = ((float)c.w + beta) * inv[k + 3];
-    bt[i] = o;
+// 16-bit copy of nw (+ per-word "wide" flag when a count exceeds 65535).
+template <int C>
+__global__ __launch_bounds__(256) void k_build_packed(const int32_t* __restrict__ nw, int64_t V,
+                                                      uint16_t* __restrict__ nw16,
+                                                      uint8_t* __restrict__ wide) {
+  constexpr int KP = C * 64;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  for (int64_t w = (int64_t)blockIdx.x * 4 + wid; w < V; w += (int64_t)gridDim.x * 4) {
+    int32_t c[C];
+    load_row<C>(c, nw + w * KP + lane * C);
+    bool big = false;
+#pragma unroll
+    for (int j = 0; j < C; ++j) big |= (uint32_t)c[j] > 0xFFFFu;
+#pragma unroll
+    for (int j = 0; j < C; ++j)
+      nw16[w * KP + lane * C + j] = (uint16_t)((uint32_t)c[j] > 0xFFFFu ? 0xFFFFu : (uint32_t)c[j]);
+    const uint64_t any = __ballot(big);
+    if (lane == 0) wide[w] = any ? 1 : 0;
   }
 }
 
@@ -1085,14 +1147,18 @@ hipError_t launch_build_sparse(const int32_t* nw, int64_t V, int32_t Kp, const i
   return hipGetLastError();
 }
 
-hipError_t launch_build_btable(const int32_t* nw, int64_t V, int32_t Kp, float beta,
-                               const float* inv, float* bt, hipStream_t st) {
-  const int64_t n4 = V * Kp / 4;
-  if (n4 <= 0) return hipSuccess;
-  const int blocks = (int)std::min<int64_t>((n4 + 255) / 256, 8192);
-  hipLaunchKernelGGL(k_build_btable, dim3(blocks), dim3(256), 0, st,
-                     reinterpret_cast<const int4*>(nw), n4, Kp, beta, inv,
-                     reinterpret_cast<float4*>(bt));
+hipError_t launch_build_packed(const int32_t* nw, int64_t V, int32_t Kp, uint16_t* nw16,
+                               uint8_t* wide, hipStream_t st) {
+  if (V <= 0) return hipSuccess;
+  const int blocks = (int)std::min<int64_t>((V + 3) / 4, 16384);
+  switch (Kp / 64) {
+    case 1: hipLaunchKernelGGL(k_build_packed<1>, dim3(blocks), dim3(256), 0, st, nw, V, nw16, wide); break;
+    case 2: hipLaunchKernelGGL(k_build_packed<2>, dim3(blocks), dim3(256), 0, st, nw, V, nw16, wide); break;
+    case 4: hipLaunchKernelGGL(k_build_packed<4>, dim3(blocks), dim3(256), 0, st, nw, V, nw16, wide); break;
+    case 8: hipLaunchKernelGGL(k_build_packed<8>, dim3(blocks), dim3(256), 0, st, nw, V, nw16, wide); break;
+    case 16: hipLaunchKernelGGL(k_build_packed<16>, dim3(blocks), dim3(256), 0, st, nw, V, nw16, wide); break;
+    default: return hipErrorInvalidValue;
+  }
   return hipGetLastError();
 }
 

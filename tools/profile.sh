@@ -1,0 +1,24 @@
+# rocprofv3 passes over one bench command; summaries under gpurun_out/prof_<label>/
+# usage: LABEL=x BENCH_ARGS="--sampler dense" bash tools/profile.sh
+set -o pipefail
+cd "$GRAFT_REPO_ROOT"
+export TMPDIR=/tmp
+P=gpurun_out/prof_${LABEL:-run}
+mkdir -p $P
+B="python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline ${BENCH_ARGS:-}"
+SEL='--kernel-include-regex k_sample|k_apply|k_prepare|k_count|k_build'
+run() {  # name, rocprof args...
+  local name=$1; shift
+  timeout -k 10 600 rocprofv3 "$@" -d $P/$name -o $name --output-format csv -- $B > $P/$name.log 2>&1 || { echo "$name FAILED"; tail -20 $P/$name.log; return 1; }
+  python3 tools/summarize_prof.py $P/$name $P/summary_$name.json && cp $P/$name/*kernel_stats.csv $P/ 2>/dev/null; rm -rf $P/$name
+  echo "$name ok"
+}
+run kt --kernel-trace --stats &&
+run fetch $SEL --pmc FETCH_SIZE &&
+run write $SEL --pmc WRITE_SIZE &&
+run sq $SEL --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU &&
+run lat $SEL --pmc SQ_INSTS_VMEM_RD SQ_INST_LEVEL_VMEM SQ_ACCUM_PREV_HIRES &&
+run tcc $SEL --pmc TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_DRAM_sum &&
+run ea $SEL --pmc TCC_EA0_RDREQ_LEVEL_sum TCC_EA0_RDREQ_DRAM_CREDIT_STALL_sum TCC_BUSY_avr &&
+run lds $SEL --pmc SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_VMEM_WR SQ_WAIT_INST_LDS
+ls $P
