@@ -33,6 +33,8 @@ CONFIGS = {
                desc="C4 shard: 1.25M docs x 200 tok per GPU, V=100k, K=512 (N=8 == C4: 10M docs)"),
     "c2": dict(docs=100_000, doc_len=200, V=50_000, K=128, desc="C2: 100k docs x 200 tok, V=50k, K=128"),
     "c3": dict(docs=100_000, doc_len=200, V=50_000, K=1024, desc="C3: 100k docs x 200 tok, V=50k, K=1024"),
+    "c5": dict(docs=1_250_000, doc_len=200, V=262_144, K=4096, sampler="sparse",
+               desc="C5 shard: 1.25M docs x 200 tok per GPU, V=262144, K=4096, sparse sampler"),
 }
 HBM_PEAK_GBS = 8000.0   # MI355X spec (MI355X_MICROARCH.md: 8.0 TB/s)
 
@@ -95,7 +97,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="c4", choices=sorted(CONFIGS))
     ap.add_argument("--docs", type=int, default=0, help="override docs per GPU")
-    ap.add_argument("--sampler", default="dense", choices=["dense", "sparse"])
+    ap.add_argument("--sampler", default=None, choices=["dense", "sparse"],
+                    help="draw kernel (default: dense, sparse for c5)")
     ap.add_argument("--burnin", type=int, default=0,
                     help="extra untimed sweeps before the warm-up (steady-state measurement)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -119,6 +122,8 @@ def main():
     from ldagibbssampling_amd.sampler import GibbsSampler
 
     cfg = CONFIGS[args.config]
+    if args.sampler is None:
+        args.sampler = cfg.get("sampler", "dense")
     K, V, L = cfg["K"], cfg["V"], cfg["doc_len"]
     docs = args.docs or cfg["docs"]
     alpha_sum, beta = 0.1 * K, 0.01
@@ -173,7 +178,7 @@ def main():
     if rank == 0:
         bpt = bytes_per_token(K)
         achieved = n_local * bpt / (kern_ms * 1e-3) / 1e9      # GB/s, algorithmic
-        traffic_gb, traffic_src = pmc_traffic(K, n_local, "k_sample_sparse<" if args.sampler == "sparse" else "k_sample<")
+        traffic_gb, traffic_src = pmc_traffic(K, n_local, ("k_sample_sparse_big<" if K > 1024 else "k_sample_sparse<") if args.sampler == "sparse" else "k_sample<")
         result = {
             "metric": "Gibbs tokens sampled/sec at K=512",
             "value": value,
@@ -210,7 +215,7 @@ def main():
                 "traffic_unit": "GB per launch (rocprofv3 PMC, gfx950-corrected)",
                 "traffic_source": traffic_src,
                 "algorithmic_gb_per_launch": n_local * bpt / 1e9,
-                "kernel": f"{'k_sample_sparse' if args.sampler == 'sparse' else 'k_sample'}<C={sampler.Kp // 64}> avg {kern_ms:.3f} ms/launch over "
+                "kernel": f"{('k_sample_sparse_big' if K > 1024 else 'k_sample_sparse') if args.sampler == 'sparse' else 'k_sample'}<C={sampler.Kp // 64}> avg {kern_ms:.3f} ms/launch over "
                           f"{n_local} tokens, B(K)={bpt} B/token",
             },
             "ll_per_token": ll / (n_local * world),

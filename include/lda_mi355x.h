@@ -47,7 +47,11 @@ typedef int32_t lda_status;
 #define LDA_ERR_STATE (-4)        /* call out of order (e.g. sample with a pending delta) */
 #define LDA_ERR_UNSUPPORTED (-5)  /* e.g. K above the compiled maximum */
 
-#define LDA_MAX_TOPICS 1024       /* kernel instantiations: K <= 1024 */
+#define LDA_MAX_TOPICS 4096       /* K <= 4096 (LDA_SAMPLER_SPARSE above 1024)       */
+#define LDA_MAX_TOPICS_DENSE 1024 /* the dense sampler's register-resident rows      */
+/* With K > 1024 (Kp > 1024) a document's topic counts live in LDS as 16-bit
+ * pairs: documents are limited to 65535 tokens there (LDA_ERR_UNSUPPORTED). */
+#define LDA_MAX_DOC_TOKENS_BIGK 65535
 
 /* Draw kernels.  Both are exact against the CPU oracle.
  *  DENSE   reads the word's whole row from a 16-bit copy of nw (2K bytes per
@@ -109,6 +113,8 @@ lda_status lda_synchronize(lda_ctx* ctx);
 lda_status lda_get_sweep(lda_ctx* ctx, uint32_t* sweep);
 lda_status lda_set_sweep(lda_ctx* ctx, uint32_t sweep);
 
+/* Kp = 64 * C, C the next power of two >= ceil(K/64) (1..64); lane l of a
+ * wavefront owns topics [l*C, (l+1)*C). */
 int32_t lda_padded_topics(int32_t num_topics);
 lda_status lda_get_shape(lda_ctx* ctx, int32_t* K, int32_t* Kp, int32_t* V, int64_t* D,
                          int64_t* N);

@@ -23,7 +23,9 @@ STATUS_NAMES = {
     -4: "LDA_ERR_STATE",
     -5: "LDA_ERR_UNSUPPORTED",
 }
-MAX_TOPICS = 1024
+MAX_TOPICS = 4096
+MAX_TOPICS_DENSE = 1024
+MAX_DOC_TOKENS_BIGK = 65535
 SAMPLERS = {"dense": 0, "sparse": 1}
 
 

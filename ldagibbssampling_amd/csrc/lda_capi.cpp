@@ -39,7 +39,12 @@ lda_status fail(lda_status code, const std::string& msg) {
                   std::string(#expr) + ": " + hipGetErrorString(e_));                     \
   } while (0)
 
-int pad_topics(int K) { return (K + 63) / 64 * 64; }
+// Kp = 64 * C with C a power of two (1..64): one kernel instantiation per C.
+int pad_topics(int K) {
+  int kp = 64;
+  while (kp < K) kp *= 2;
+  return kp;
+}
 
 double log_gamma_stirling(double z) {  // Dirichlet.logGammaStirling [M]
   const double HALF_LOG_TWO_PI = 0.91893853320467274178;
@@ -235,7 +240,10 @@ lda_status lda_create(lda_ctx** out, const lda_config* cfg, const int64_t* doc_o
   *out = nullptr;
   if (cfg->num_topics < 1) return fail(LDA_ERR_INVALID_ARG, "num_topics must be >= 1");
   if (cfg->num_topics > LDA_MAX_TOPICS)
-    return fail(LDA_ERR_UNSUPPORTED, "num_topics above LDA_MAX_TOPICS (1024)");
+    return fail(LDA_ERR_UNSUPPORTED, "num_topics above LDA_MAX_TOPICS (4096)");
+  if (cfg->num_topics > LDA_MAX_TOPICS_DENSE && cfg->sampler == LDA_SAMPLER_DENSE)
+    return fail(LDA_ERR_UNSUPPORTED,
+                "num_topics above LDA_MAX_TOPICS_DENSE (1024): use LDA_SAMPLER_SPARSE");
   if (cfg->num_types < 1) return fail(LDA_ERR_INVALID_ARG, "num_types must be >= 1");
   if (cfg->num_docs < 0) return fail(LDA_ERR_INVALID_ARG, "num_docs must be >= 0");
   if (!cfg->alpha) return fail(LDA_ERR_INVALID_ARG, "alpha is null");
@@ -252,6 +260,10 @@ lda_status lda_create(lda_ctx** out, const lda_config* cfg, const int64_t* doc_o
   }
   const int64_t N = off[D];
   if (N > 0 && !words) return fail(LDA_ERR_INVALID_ARG, "words is null");
+  if (pad_topics(cfg->num_topics) > 1024)
+    for (int64_t d = 0; d < D; ++d)
+      if (off[d + 1] - off[d] > LDA_MAX_DOC_TOKENS_BIGK)
+        return fail(LDA_ERR_UNSUPPORTED, "document longer than 65535 tokens with num_topics > 1024");
   for (int64_t i = 0; i < N; ++i)
     if (words[i] < 0 || words[i] >= cfg->num_types)
       return fail(LDA_ERR_INVALID_ARG, "word id out of range [0, V)");
@@ -597,8 +609,13 @@ lda_status lda_infer(lda_ctx* c, int64_t Dh, const int64_t* doc_off, const int32
     if (d > 0 && off[d] < off[d - 1]) return fail(LDA_ERR_INVALID_ARG, "doc_off not monotone");
   }
   const int64_t N = off[Dh];
+  if (N > 0 && !words) return fail(LDA_ERR_INVALID_ARG, "words is null");
   for (int64_t i = 0; i < N; ++i)
     if (words[i] < 0 || words[i] >= c->V) return fail(LDA_ERR_INVALID_ARG, "word id out of range (OOV must be removed)");
+  if (c->Kp > 1024)
+    for (int64_t d = 0; d < Dh; ++d)
+      if (off[d + 1] - off[d] > LDA_MAX_DOC_TOKENS_BIGK)
+        return fail(LDA_ERR_UNSUPPORTED, "document longer than 65535 tokens with num_topics > 1024");
   HIP_TRY(hipSetDevice(c->device));
   int32_t *dw = nullptr, *dz = nullptr, *acc = nullptr, *q = nullptr;
   int64_t *doff = nullptr, *drange = nullptr;

@@ -783,6 +783,329 @@ __global__ __launch_bounds__(256) void k_sample_sparse(SampleParams p) {
   }
 }
 
+// ------------------------------------------- the large-K sparse sampler
+// K up to 4096 (C = 32, 64): the same draw as k_sample_sparse with the dense
+// doc part's lane partials in groups of 16 topics (TG registers; see
+// oracle/lda_oracle.c:lane_partial_grouped), so a changed topic re-sums 16
+// coefficients, not C.  LDS: per block a float2 {alpha, inv} table; per wave
+// nd as 16-bit pairs (documents < 65536 tokens) and the fp32 coefficients.
+// The word part streams its rounds of 64 entries (the first SB_RB of the next
+// P tokens prefetched); the selected lane re-walks its entries.
+#define SB_RB 2
+template <int C>
+__device__ __forceinline__ float group_partial(const float* __restrict__ cl, float beta) {
+  float a = 0.0f;
+#pragma unroll
+  for (int q = 0; q < 16; q += 4) {
+    const float4 v = *reinterpret_cast<const float4*>(cl + q);
+    a = __builtin_fmaf(v.x, beta, a);
+    a = __builtin_fmaf(v.y, beta, a);
+    a = __builtin_fmaf(v.z, beta, a);
+    a = __builtin_fmaf(v.w, beta, a);
+  }
+  return a;
+}
+
+__device__ __forceinline__ int nd16_get(const uint32_t* nd2, int k) {
+  return (int)((nd2[k >> 1] >> ((k & 1) * 16)) & 0xFFFFu);
+}
+
+template <int C, int P, bool FROZEN>
+__global__ __launch_bounds__(256) void k_sample_sparse_big(SampleParams p) {
+  extern __shared__ __attribute__((aligned(16))) int32_t smem[];
+  constexpr int KP = C * 64;
+  constexpr int NG = C / 16;
+  const int lane = threadIdx.x & 63;
+  const int wid = threadIdx.x >> 6;
+  float2* tab = reinterpret_cast<float2*>(smem);                      // [KP] {alpha, inv}
+  uint32_t* nd2 = reinterpret_cast<uint32_t*>(smem + 2 * KP) + wid * (3 * KP / 2);  // [KP/2]
+  float* coef = reinterpret_cast<float*>(nd2 + KP / 2);               // [KP]
+
+  for (int i = threadIdx.x; i < KP; i += 256) tab[i] = make_float2(p.alpha[i], p.inv[i]);
+  for (int i = threadIdx.x; i < 4 * (3 * KP / 2); i += 256) smem[2 * KP + i] = 0;
+  __syncthreads();
+
+  const float beta = p.beta;
+  const int last_lane = (p.K - 1) / C;
+  const int last_j = (lane < last_lane) ? C - 1 : (p.K - 1) % C;
+  const int32_t* __restrict__ nw = p.nw;
+  const uint32_t* __restrict__ ent = p.ent;
+  const int64_t* __restrict__ row_off = p.row_off;
+  const int32_t* __restrict__ row_nnz = p.row_nnz;
+  const float* __restrict__ inv_m1 = p.inv_m1;
+
+  auto coef_of = [&](int k, int ndk, bool corrected, float invm1k) -> float {
+    const float2 ai = tab[k];
+    return ((float)ndk + ai.x) * (corrected ? invm1k : ai.y);
+  };
+  // recompute group g of this lane (exec: lanes that call it)
+  auto regroup = [&](float (&TG)[NG], int g) {
+    const float v = group_partial<C>(coef + lane * C + g * 16, beta);
+#pragma unroll
+    for (int q = 0; q < NG; ++q)
+      if (q == g) TG[q] = v;
+  };
+  auto lane_total = [&](const float (&TG)[NG]) -> float {
+    float t = TG[0];
+#pragma unroll
+    for (int q = 1; q < NG; ++q) t = t + TG[q];
+    return t;
+  };
+
+  while (true) {
+    int r = 0;
+    if (lane == 0) r = atomicAdd(p.queue, 1);
+    r = uniform_i(__shfl(r, 0));
+    if (r >= p.num_ranges) break;
+    const int64_t d0 = p.range_doc[r], d1 = p.range_doc[r + 1];
+    const int64_t t0 = p.doc_off[d0], t1 = p.doc_off[d1];
+    if (t1 <= t0) continue;
+
+    int64_t cbase = t0;
+    int cw = 0, cz = 0, w1 = 0, z1 = 0, w2 = 0, z2 = 0;
+    if (t0 + lane < t1) {
+      cw = p.words[t0 + lane];
+      cz = p.z[t0 + lane];
+    }
+    if (t0 + 64 + lane < t1) {
+      w1 = p.words[t0 + 64 + lane];
+      z1 = p.z[t0 + 64 + lane];
+    }
+    if (t0 + 128 + lane < t1) {
+      w2 = p.words[t0 + 128 + lane];
+      z2 = p.z[t0 + 128 + lane];
+    }
+    int cmn = row_nnz[cw], m1n = row_nnz[w1];
+    int64_t cmo = row_off[cw], m1o = row_off[w1];
+    int cn = cz;
+    float cu = u01(draw_u32((uint64_t)(p.token_base + t0 + lane), p.c2, p.c3, p.k0, p.k1));
+
+    float TG[NG];
+    auto build_doc = [&](int64_t ts, int64_t te) {
+      for (int64_t i = ts + lane; i < te; i += 64) {
+        const int k = p.z[i];
+        atomicAdd(&nd2[k >> 1], (k & 1) ? 0x10000u : 1u);
+      }
+      wave_lds_fence();
+#pragma unroll
+      for (int j = 0; j < C; ++j) {
+        const int k = lane * C + j;
+        coef[k] = coef_of(k, nd16_get(nd2, k), false, 0.0f);
+      }
+      wave_lds_fence();
+#pragma unroll
+      for (int g = 0; g < NG; ++g) TG[g] = group_partial<C>(coef + lane * C + g * 16, beta);
+    };
+    auto clear_doc = [&]() {
+#pragma unroll
+      for (int j = 0; j < C / 2; ++j) nd2[lane * (C / 2) + j] = 0u;
+      wave_lds_fence();
+    };
+
+    int64_t doc = d0;
+    while (p.doc_off[doc + 1] <= t0) ++doc;
+    int64_t doc_end = p.doc_off[doc + 1];
+    build_doc(t0, doc_end);
+
+    uint32_t ring[P][SB_RB];
+    float cinv[P];
+#pragma unroll
+    for (int s = 0; s < P; ++s) {
+      const int64_t tp = t0 + s;
+      const int n = readlane_i(cmn, s);
+      const int64_t o = ((int64_t)readlane_i((int)(cmo >> 32), s) << 32) | (uint32_t)readlane_i((int)cmo, s);
+#pragma unroll
+      for (int q = 0; q < SB_RB; ++q)
+        ring[s][q] = (tp < t1 && q * 64 + lane < n) ? ent[o + q * 64 + lane] : 0u;
+      if (!FROZEN) cinv[s] = inv_m1[(tp < t1) ? readlane_i(cz, s) : 0];
+    }
+
+    for (int64_t tb = t0; tb < t1; tb += P) {
+#pragma unroll
+      for (int s = 0; s < P; ++s) {
+        const int64_t t = tb + s;
+        if (t >= t1) break;
+        int idx = (int)(t - cbase);
+        if (idx == 64) {
+          p.z[cbase + lane] = cn;
+          cbase += 64;
+          idx = 0;
+          cw = w1;
+          cz = z1;
+          cmn = m1n;
+          cmo = m1o;
+          w1 = w2;
+          z1 = z2;
+          m1n = row_nnz[w1];
+          m1o = row_off[w1];
+          cn = cz;
+          cu = u01(draw_u32((uint64_t)(p.token_base + cbase + lane), p.c2, p.c3, p.k0, p.k1));
+          if (cbase + 128 + lane < t1) {
+            w2 = p.words[cbase + 128 + lane];
+            z2 = p.z[cbase + 128 + lane];
+          }
+        }
+        if (t == doc_end) {
+          clear_doc();
+          ++doc;
+          while (p.doc_off[doc + 1] <= t) ++doc;
+          doc_end = p.doc_off[doc + 1];
+          build_doc(t, doc_end);
+        }
+
+        const int w = readlane_i(cw, idx);
+        const int zo = readlane_i(cz, idx);
+        const float u = readlane_f(cu, idx);
+        const int n = readlane_i(cmn, idx);
+        const int64_t off = ((int64_t)readlane_i((int)(cmo >> 32), idx) << 32) | (uint32_t)readlane_i((int)cmo, idx);
+        const int lo = zo / C;
+        const int go = (zo % C) / 16;
+
+        // remove the token from its document (and, unless frozen, from the snapshot)
+        {
+          const int ndz = nd16_get(nd2, zo) - 1;
+          const float cf = coef_of(zo, ndz, !FROZEN, FROZEN ? 0.0f : cinv[s]);
+          if (lane == 0) {
+            nd2[zo >> 1] -= (zo & 1) ? 0x10000u : 1u;
+            coef[zo] = cf;
+          }
+          wave_lds_fence();
+          if (lane == lo) regroup(TG, go);
+        }
+
+        // word part: rounds of 64 entries, lane l holds e = l + 64 r
+        const int nr_all = (n + 63) >> 6;
+        float accB = 0.0f;
+        auto entry_b = [&](uint32_t e, bool valid, int& tq) -> float {
+          tq = (int)(e & ENT_TOPIC_MASK);
+          int cq = (int)(e >> ENT_TOPIC_BITS);
+          if (valid && (uint32_t)cq == ENT_COUNT_SAT) cq = nw[(int64_t)w * KP + tq];
+          if (!FROZEN) cq -= (tq == zo) ? 1 : 0;
+          return valid ? coef[tq] * (float)cq : 0.0f;
+        };
+#pragma unroll
+        for (int q = 0; q < SB_RB; ++q) {
+          if (q < nr_all) {
+            int tq;
+            accB = accB + entry_b(ring[s][q], q * 64 + lane < n, tq);
+          }
+        }
+        for (int q = SB_RB; q < nr_all; ++q) {
+          const bool valid = q * 64 + lane < n;
+          const uint32_t e = valid ? ent[off + q * 64 + lane] : 0u;
+          int tq;
+          accB = accB + entry_b(e, valid, tq);
+        }
+        const float TB = wave_incl_scan(accB);
+        const float TAs = wave_incl_scan(lane_total(TG));
+        const float sumB = readlane_f(TB, 63);
+        const float sumA = readlane_f(TAs, 63);
+        const float thr = u * (sumB + sumA);
+        int kn;
+        if (thr < sumB) {
+          const int nl = n < 64 ? n : 64;
+          const uint64_t m = __ballot((TB > thr) && (lane < nl));
+          const int lstar = m ? (int)__builtin_ctzll(m) : nl - 1;
+          const float E = lstar > 0 ? readlane_f(TB, lstar - 1) : 0.0f;
+          int tsel = 0;
+          if (lane == lstar) {
+            const int nr = (n - lane + 63) / 64;
+            float acc = 0.0f;
+            bool found = false;
+            for (int q = 0; q < nr; ++q) {
+              uint32_t e;
+              if (q < SB_RB) {
+                e = 0u;
+#pragma unroll
+                for (int qq = 0; qq < SB_RB; ++qq)
+                  if (qq == q) e = ring[s][qq];
+              } else {
+                e = ent[off + q * 64 + lane];
+              }
+              int tq;
+              acc = acc + entry_b(e, true, tq);
+              if (!found) tsel = tq;
+              if (!found && !(E + acc <= thr)) found = true;
+            }
+          }
+          kn = readlane_i(tsel, lstar);
+        } else {
+          const float thr2 = thr - sumB;
+          const uint64_t m = __ballot((TAs > thr2) && (lane <= last_lane));
+          const int lstar = m ? (int)__builtin_ctzll(m) : last_lane;
+          const float E = lstar > 0 ? readlane_f(TAs, lstar - 1) : 0.0f;
+          int jsel = 0;
+          if (lane == lstar) {
+            int cnt = 0;
+            float P_ = 0.0f;
+            for (int g = 0; g < NG; ++g) {
+              float a = 0.0f;
+#pragma unroll
+              for (int j = 0; j < 16; ++j) {
+                a = __builtin_fmaf(coef[lane * C + g * 16 + j], beta, a);
+                const float x = g == 0 ? a : P_ + a;
+                cnt += (E + x <= thr2) ? 1 : 0;
+              }
+              P_ = g == 0 ? a : P_ + a;
+            }
+            jsel = cnt < C ? cnt : last_j;
+          }
+          kn = lstar * C + readlane_i(jsel, lstar);
+        }
+
+        // add the token back under its new topic
+        {
+          const int ndk = nd16_get(nd2, kn) + 1;
+          if (lane == 0) nd2[kn >> 1] += (kn & 1) ? 0x10000u : 1u;
+          wave_lds_fence();
+          const int ndz = (kn == zo) ? ndk : nd16_get(nd2, zo);
+          const float cfz = coef_of(zo, ndz, false, 0.0f);
+          const float cfk = coef_of(kn, ndk, false, 0.0f);
+          if (lane == 0) {
+            coef[zo] = cfz;
+            coef[kn] = cfk;
+          }
+          wave_lds_fence();
+          if (lane == lo) regroup(TG, go);
+          if (lane == kn / C) regroup(TG, (kn % C) / 16);
+        }
+        cn = (lane == idx) ? kn : cn;
+        if (!FROZEN && kn != zo) {
+          if (lane < 2) {
+            const int k = lane == 0 ? zo : kn;
+            const int v = lane == 0 ? -1 : 1;
+            atomicAdd(&p.delta[(int64_t)w * KP + k], v);
+            atomicAdd(&p.dsum[k], v);
+          }
+        }
+
+        // keep the pipeline full: token t+P
+        const int64_t tp = t + P;
+        if (tp < t1) {
+          const int pidx = (int)(tp - cbase);
+          int np, zp;
+          int64_t op;
+          if (pidx < 64) {
+            np = readlane_i(cmn, pidx);
+            op = ((int64_t)readlane_i((int)(cmo >> 32), pidx) << 32) | (uint32_t)readlane_i((int)cmo, pidx);
+            zp = readlane_i(cz, pidx);
+          } else {
+            np = readlane_i(m1n, pidx - 64);
+            op = ((int64_t)readlane_i((int)(m1o >> 32), pidx - 64) << 32) |
+                 (uint32_t)readlane_i((int)m1o, pidx - 64);
+            zp = readlane_i(z1, pidx - 64);
+          }
+#pragma unroll
+          for (int q = 0; q < SB_RB; ++q) ring[s][q] = (q * 64 + lane < np) ? ent[op + q * 64 + lane] : 0u;
+          if (!FROZEN) cinv[s] = inv_m1[zp];
+        }
+      }
+    }
+    if (cbase + lane < t1) p.z[cbase + lane] = cn;
+    clear_doc();
+  }
+}
+
 // Inclusive integer wavefront scan (any order is exact for integers).
 __device__ __forceinline__ int wave_incl_scan_i(int x) {
   x += __builtin_amdgcn_update_dpp(0, x, 0x111, 0xf, 0xf, true);
@@ -886,7 +1209,7 @@ __global__ void k_prepare_topics(int32_t* __restrict__ nwsum, int32_t* __restric
                                  const double* __restrict__ alpha, double beta, double vbeta,
                                  int32_t K, int32_t Kp, float* __restrict__ alpha_f,
                                  float* __restrict__ inv, float* __restrict__ inv_m1) {
-  const int k = threadIdx.x;
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= Kp) return;
   const int32_t s = nwsum[k] + dsum[k];
   nwsum[k] = s;
@@ -1098,6 +1421,32 @@ static int occupancy_sparse_t() {
     return 1;
   return nb > 0 ? nb : 1;
 }
+template <int C, bool FROZEN>
+static size_t sparse_big_lds() {
+  // {alpha, inv} table + 4 waves x (nd pairs + coefficients); > 64 KiB at C = 64
+  const size_t lds = (2 * 64 * C + 4 * 3 * 32 * C) * sizeof(int32_t);
+  static bool attr = [lds] {
+    return hipFuncSetAttribute(reinterpret_cast<const void*>(&k_sample_sparse_big<C, SPARSE_P, FROZEN>),
+                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) == hipSuccess;
+  }();
+  (void)attr;
+  return lds;
+}
+template <int C, bool FROZEN>
+static hipError_t launch_sparse_big_t(const SampleParams& p, int blocks, hipStream_t st) {
+  const size_t lds = sparse_big_lds<C, FROZEN>();
+  hipLaunchKernelGGL((k_sample_sparse_big<C, SPARSE_P, FROZEN>), dim3(blocks), dim3(256), lds, st, p);
+  return hipGetLastError();
+}
+template <int C, bool FROZEN>
+static int occupancy_sparse_big_t() {
+  int nb = 0;
+  const size_t lds = sparse_big_lds<C, FROZEN>();
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_sample_sparse_big<C, SPARSE_P, FROZEN>, 256,
+                                                   lds) != hipSuccess)
+    return 1;
+  return nb > 0 ? nb : 1;
+}
 #define LDA_DISPATCH_SPARSE(C_, FN, ...)                            \
   switch (C_) {                                                     \
     case 1: return FN<1, SPARSE_P, 1, FROZEN>(__VA_ARGS__);         \
@@ -1109,11 +1458,15 @@ static int occupancy_sparse_t() {
   }
 template <bool FROZEN>
 static hipError_t launch_sparse_c(int C, const SampleParams& p, int blocks, hipStream_t st) {
+  if (C == 32) return launch_sparse_big_t<32, FROZEN>(p, blocks, st);
+  if (C == 64) return launch_sparse_big_t<64, FROZEN>(p, blocks, st);
   LDA_DISPATCH_SPARSE(C, launch_sparse_t, p, blocks, st)
   return hipErrorInvalidValue;
 }
 template <bool FROZEN>
 static int occupancy_sparse_c(int C) {
+  if (C == 32) return occupancy_sparse_big_t<32, FROZEN>();
+  if (C == 64) return occupancy_sparse_big_t<64, FROZEN>();
   LDA_DISPATCH_SPARSE(C, occupancy_sparse_t)
   return 1;
 }
@@ -1142,6 +1495,8 @@ hipError_t launch_build_sparse(const int32_t* nw, int64_t V, int32_t Kp, const i
     case 4: hipLaunchKernelGGL(k_build_sparse<4>, dim3(blocks), dim3(256), 0, st, nw, V, row_off, ent, row_nnz); break;
     case 8: hipLaunchKernelGGL(k_build_sparse<8>, dim3(blocks), dim3(256), 0, st, nw, V, row_off, ent, row_nnz); break;
     case 16: hipLaunchKernelGGL(k_build_sparse<16>, dim3(blocks), dim3(256), 0, st, nw, V, row_off, ent, row_nnz); break;
+    case 32: hipLaunchKernelGGL(k_build_sparse<32>, dim3(blocks), dim3(256), 0, st, nw, V, row_off, ent, row_nnz); break;
+    case 64: hipLaunchKernelGGL(k_build_sparse<64>, dim3(blocks), dim3(256), 0, st, nw, V, row_off, ent, row_nnz); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();
@@ -1191,8 +1546,8 @@ hipError_t launch_apply(int32_t* nw, int32_t* delta, int64_t n, hipStream_t st) 
 hipError_t launch_prepare_topics(int32_t* nwsum, int32_t* dsum, const double* alpha, double beta,
                                  double vbeta, int32_t K, int32_t Kp, float* alpha_f, float* inv,
                                  float* inv_m1, hipStream_t st) {
-  hipLaunchKernelGGL(k_prepare_topics, dim3(1), dim3(Kp), 0, st, nwsum, dsum, alpha, beta, vbeta, K,
-                     Kp, alpha_f, inv, inv_m1);
+  hipLaunchKernelGGL(k_prepare_topics, dim3((Kp + 255) / 256), dim3(256), 0, st, nwsum, dsum, alpha,
+                     beta, vbeta, K, Kp, alpha_f, inv, inv_m1);
   return hipGetLastError();
 }
 

@@ -56,6 +56,9 @@ def test_host_only_entry_points(lib):
     assert capi.padded_topics(64) == 64
     assert capi.padded_topics(65) == 128
     assert capi.padded_topics(1024) == 1024
+    assert capi.padded_topics(300) == 512          # Kp = 64 x power of two
+    assert capi.padded_topics(1025) == 2048
+    assert capi.padded_topics(4096) == 4096
 
 
 def test_config_struct_layout():

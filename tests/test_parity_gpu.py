@@ -66,6 +66,68 @@ def test_sweeps_bit_exact(oracle, K, kind):
 
 
 @pytest.mark.parametrize("kind", KINDS)
+def test_non_power_of_two_padding(oracle, kind):
+    """K=300 pads to Kp=512 (C=8): padded topics never drawn."""
+    corpus = _ragged_corpus(D=60, V=400, seed=300)
+    K = 300
+    g, o = _pair(oracle, corpus, K, np.full(K, 0.05), 0.01, seed=3, kind=kind)
+    assert g.Kp == 512
+    g.sweep(2)
+    o.sweep(2)
+    _assert_same_state(g, o)
+    assert g.z().max() < K
+
+
+@pytest.mark.parametrize("K", [1500, 2048, 4096])
+def test_large_k_sparse_bit_exact(oracle, K):
+    """K > 1024 (C = 32, 64): grouped doc-part partials, streamed word rounds,
+    16-bit document counts in LDS."""
+    corpus = _ragged_corpus(D=80, V=600, seed=K)
+    alpha = np.full(K, 50.0 / K)
+    g, o = _pair(oracle, corpus, K, alpha, 0.01, seed=K + 1, tokens_per_range=400, kind="sparse")
+    g.sweep(0)
+    o.apply()
+    _assert_same_state(g, o)
+    for n in (1, 3):
+        g.sweep(n)
+        o.sweep(n)
+        _assert_same_state(g, o)
+    lg, lo = g.log_likelihood(), o.log_likelihood()
+    assert abs(lg - lo) <= 1e-9 * abs(lo), (lg, lo)
+
+
+def test_large_k_sparse_long_rows_and_inference(oracle):
+    """Frequent words with > 128 nonzero topics (more rounds than the prefetch
+    ring holds), then frozen-model inference at K=4096."""
+    c = synthetic_lda(num_docs=150, num_types=300, num_topics=64, doc_len=None, mean_len=400,
+                      min_len=1, max_len=1200, seed=4)
+    train, held = c.subset(range(0, 120)), c.subset(range(120, 150))
+    K = 4096
+    g, o = _pair(oracle, train, K, np.full(K, 0.01), 0.05, seed=6, kind="sparse")
+    g.sweep(4)
+    o.sweep(4)
+    _assert_same_state(g, o)
+    assert (g.counts()[0] > 0).sum(1).max() > 128
+    tg = g.infer(held.doc_off, held.words, n_iter=6, burn_in=2, thin=2, seed=8)
+    to = o.infer(held.doc_off, held.words, n_iter=6, burn_in=2, thin=2, seed=8)
+    np.testing.assert_allclose(tg, to, rtol=0, atol=1e-12)
+
+
+def test_large_k_limits():
+    from ldagibbssampling_amd.sampler import GibbsSampler
+    from ldagibbssampling_amd.capi import LdaError
+    off = np.array([0, 3], dtype=np.int64)
+    w = np.array([1, 2, 3], np.int32)
+    with pytest.raises(LdaError, match="SPARSE"):
+        GibbsSampler(2000, 10, off, w, 0.1, 0.01, sampler="dense")
+    with pytest.raises(LdaError):
+        GibbsSampler(5000, 10, off, w, 0.1, 0.01, sampler="sparse")
+    long_off = np.array([0, 70000], dtype=np.int64)
+    with pytest.raises(LdaError, match="65535"):
+        GibbsSampler(2048, 10, long_off, np.zeros(70000, np.int32), 0.1, 0.01, sampler="sparse")
+
+
+@pytest.mark.parametrize("kind", KINDS)
 def test_many_sweeps_and_loglik(oracle, kind):
     c = synthetic_lda(num_docs=300, num_types=2000, num_topics=128, doc_len=None, mean_len=80,
                       min_len=1, max_len=400, seed=7)
