@@ -784,45 +784,37 @@ __global__ __launch_bounds__(256) void k_sample_sparse(SampleParams p) {
 }
 
 // ------------------------------------------- the large-K sparse sampler
-// K up to 4096 (C = 32, 64): the same draw as k_sample_sparse with the dense
-// doc part's lane partials in groups of 16 topics (TG registers; see
+// K up to 4096 (C = 32, 64): the same draw as k_sample_sparse with the doc
+// part's lane partials in groups of 16 topics (TG registers; see
 // oracle/lda_oracle.c:lane_partial_grouped), so a changed topic re-sums 16
-// coefficients, not C.  LDS: per block a float2 {alpha, inv} table; per wave
-// nd as 16-bit pairs (documents < 65536 tokens) and the fp32 coefficients.
-// The word part streams its rounds of 64 entries (the first SB_RB of the next
-// P tokens prefetched); the selected lane re-walks its entries.
+// coefficients, not C.  LDS holds only a per-block float2 {alpha, inv} table
+// and per-wave 16-bit document counts (documents < 65536 tokens); every
+// coefficient (nd + alpha) * inv is recomputed where it is used, which keeps
+// SB_WAVES waves per CU resident.  The word part streams its rounds of 64
+// entries (the first SB_RB of the next P tokens prefetched, the rest in
+// batches of SB_BATCH loads); the selected lane re-walks its entries.
 #define SB_RB 2
+#define SB_BATCH 4
 template <int C>
-__device__ __forceinline__ float group_partial(const float* __restrict__ cl, float beta) {
-  float a = 0.0f;
-#pragma unroll
-  for (int q = 0; q < 16; q += 4) {
-    const float4 v = *reinterpret_cast<const float4*>(cl + q);
-    a = __builtin_fmaf(v.x, beta, a);
-    a = __builtin_fmaf(v.y, beta, a);
-    a = __builtin_fmaf(v.z, beta, a);
-    a = __builtin_fmaf(v.w, beta, a);
-  }
-  return a;
-}
+constexpr int sb_waves() { return 12; }
 
 __device__ __forceinline__ int nd16_get(const uint32_t* nd2, int k) {
   return (int)((nd2[k >> 1] >> ((k & 1) * 16)) & 0xFFFFu);
 }
 
 template <int C, int P, bool FROZEN>
-__global__ __launch_bounds__(256) void k_sample_sparse_big(SampleParams p) {
+__global__ __launch_bounds__(64 * sb_waves<C>()) void k_sample_sparse_big(SampleParams p) {
   extern __shared__ __attribute__((aligned(16))) int32_t smem[];
   constexpr int KP = C * 64;
   constexpr int NG = C / 16;
+  constexpr int WB = sb_waves<C>();
   const int lane = threadIdx.x & 63;
   const int wid = threadIdx.x >> 6;
-  float2* tab = reinterpret_cast<float2*>(smem);                      // [KP] {alpha, inv}
-  uint32_t* nd2 = reinterpret_cast<uint32_t*>(smem + 2 * KP) + wid * (3 * KP / 2);  // [KP/2]
-  float* coef = reinterpret_cast<float*>(nd2 + KP / 2);               // [KP]
+  float2* tab = reinterpret_cast<float2*>(smem);                              // [KP] {alpha, inv}
+  uint32_t* nd2 = reinterpret_cast<uint32_t*>(smem + 2 * KP) + wid * (KP / 2); // [KP/2]
 
-  for (int i = threadIdx.x; i < KP; i += 256) tab[i] = make_float2(p.alpha[i], p.inv[i]);
-  for (int i = threadIdx.x; i < 4 * (3 * KP / 2); i += 256) smem[2 * KP + i] = 0;
+  for (int i = threadIdx.x; i < KP; i += 64 * WB) tab[i] = make_float2(p.alpha[i], p.inv[i]);
+  for (int i = threadIdx.x; i < WB * (KP / 2); i += 64 * WB) smem[2 * KP + i] = 0;
   __syncthreads();
 
   const float beta = p.beta;
@@ -834,13 +826,32 @@ __global__ __launch_bounds__(256) void k_sample_sparse_big(SampleParams p) {
   const int32_t* __restrict__ row_nnz = p.row_nnz;
   const float* __restrict__ inv_m1 = p.inv_m1;
 
-  auto coef_of = [&](int k, int ndk, bool corrected, float invm1k) -> float {
-    const float2 ai = tab[k];
-    return ((float)ndk + ai.x) * (corrected ? invm1k : ai.y);
+  // Coefficients of group g of this lane, 4 topics per step (few live
+  // registers); topic zc (if in the group) uses the own-token-removed invc.
+  auto quad_coefs = [&](float (&cf)[4], int k0, int zc, float invc) {
+    const uint2 nn = *reinterpret_cast<const uint2*>(nd2 + k0 / 2);
+    const float4 t0 = *reinterpret_cast<const float4*>(tab + k0);
+    const float4 t1 = *reinterpret_cast<const float4*>(tab + k0 + 2);
+    cf[0] = ((float)(nn.x & 0xFFFFu) + t0.x) * ((k0 == zc) ? invc : t0.y);
+    cf[1] = ((float)(nn.x >> 16) + t0.z) * ((k0 + 1 == zc) ? invc : t0.w);
+    cf[2] = ((float)(nn.y & 0xFFFFu) + t1.x) * ((k0 + 2 == zc) ? invc : t1.y);
+    cf[3] = ((float)(nn.y >> 16) + t1.z) * ((k0 + 3 == zc) ? invc : t1.w);
   };
-  // recompute group g of this lane (exec: lanes that call it)
-  auto regroup = [&](float (&TG)[NG], int g) {
-    const float v = group_partial<C>(coef + lane * C + g * 16, beta);
+  auto group_sum = [&](int g, int zc, float invc) -> float {
+    float a = 0.0f;
+#pragma nounroll
+    for (int q = 0; q < 16; q += 4) {
+      float cf[4];
+      quad_coefs(cf, lane * C + g * 16 + q, zc, invc);
+      a = __builtin_fmaf(cf[0], beta, a);
+      a = __builtin_fmaf(cf[1], beta, a);
+      a = __builtin_fmaf(cf[2], beta, a);
+      a = __builtin_fmaf(cf[3], beta, a);
+    }
+    return a;
+  };
+  auto regroup = [&](float (&TG)[NG], int g, int zc, float invc) {
+    const float v = group_sum(g, zc, invc);
 #pragma unroll
     for (int q = 0; q < NG; ++q)
       if (q == g) TG[q] = v;
@@ -888,17 +899,12 @@ __global__ __launch_bounds__(256) void k_sample_sparse_big(SampleParams p) {
       }
       wave_lds_fence();
 #pragma unroll
-      for (int j = 0; j < C; ++j) {
-        const int k = lane * C + j;
-        coef[k] = coef_of(k, nd16_get(nd2, k), false, 0.0f);
-      }
-      wave_lds_fence();
-#pragma unroll
-      for (int g = 0; g < NG; ++g) TG[g] = group_partial<C>(coef + lane * C + g * 16, beta);
+      for (int g = 0; g < NG; ++g) TG[g] = group_sum(g, -1, 0.0f);
     };
     auto clear_doc = [&]() {
 #pragma unroll
-      for (int j = 0; j < C / 2; ++j) nd2[lane * (C / 2) + j] = 0u;
+      for (int j = 0; j < C / 2; j += 4)
+        *reinterpret_cast<uint4*>(nd2 + lane * (C / 2) + j) = make_uint4(0u, 0u, 0u, 0u);
       wave_lds_fence();
     };
 
@@ -960,29 +966,27 @@ __global__ __launch_bounds__(256) void k_sample_sparse_big(SampleParams p) {
         const int64_t off = ((int64_t)readlane_i((int)(cmo >> 32), idx) << 32) | (uint32_t)readlane_i((int)cmo, idx);
         const int lo = zo / C;
         const int go = (zo % C) / 16;
+        // while the token is out: topic zc's coefficient uses invc (inv_m1[zo])
+        const int zc = FROZEN ? -1 : zo;
+        const float invc = FROZEN ? 0.0f : cinv[s];
 
-        // remove the token from its document (and, unless frozen, from the snapshot)
-        {
-          const int ndz = nd16_get(nd2, zo) - 1;
-          const float cf = coef_of(zo, ndz, !FROZEN, FROZEN ? 0.0f : cinv[s]);
-          if (lane == 0) {
-            nd2[zo >> 1] -= (zo & 1) ? 0x10000u : 1u;
-            coef[zo] = cf;
-          }
-          wave_lds_fence();
-          if (lane == lo) regroup(TG, go);
-        }
+        // remove the token from its document
+        if (lane == 0) nd2[zo >> 1] -= (zo & 1) ? 0x10000u : 1u;
+        wave_lds_fence();
+        if (lane == lo) regroup(TG, go, zc, invc);
 
         // word part: rounds of 64 entries, lane l holds e = l + 64 r
         const int nr_all = (n + 63) >> 6;
-        float accB = 0.0f;
         auto entry_b = [&](uint32_t e, bool valid, int& tq) -> float {
           tq = (int)(e & ENT_TOPIC_MASK);
           int cq = (int)(e >> ENT_TOPIC_BITS);
           if (valid && (uint32_t)cq == ENT_COUNT_SAT) cq = nw[(int64_t)w * KP + tq];
           if (!FROZEN) cq -= (tq == zo) ? 1 : 0;
-          return valid ? coef[tq] * (float)cq : 0.0f;
+          const float2 t = tab[tq];
+          const float cf = ((float)nd16_get(nd2, tq) + t.x) * ((tq == zc) ? invc : t.y);
+          return valid ? cf * (float)cq : 0.0f;
         };
+        float accB = 0.0f;
 #pragma unroll
         for (int q = 0; q < SB_RB; ++q) {
           if (q < nr_all) {
@@ -990,11 +994,20 @@ __global__ __launch_bounds__(256) void k_sample_sparse_big(SampleParams p) {
             accB = accB + entry_b(ring[s][q], q * 64 + lane < n, tq);
           }
         }
-        for (int q = SB_RB; q < nr_all; ++q) {
-          const bool valid = q * 64 + lane < n;
-          const uint32_t e = valid ? ent[off + q * 64 + lane] : 0u;
-          int tq;
-          accB = accB + entry_b(e, valid, tq);
+        for (int q0 = SB_RB; q0 < nr_all; q0 += SB_BATCH) {
+          uint32_t eb[SB_BATCH];
+#pragma unroll
+          for (int b = 0; b < SB_BATCH; ++b) {
+            const int e = (q0 + b) * 64 + lane;
+            eb[b] = e < n ? ent[off + e] : 0u;
+          }
+#pragma unroll
+          for (int b = 0; b < SB_BATCH; ++b) {
+            if (q0 + b < nr_all) {
+              int tq;
+              accB = accB + entry_b(eb[b], (q0 + b) * 64 + lane < n, tq);
+            }
+          }
         }
         const float TB = wave_incl_scan(accB);
         const float TAs = wave_incl_scan(lane_total(TG));
@@ -1012,20 +1025,29 @@ __global__ __launch_bounds__(256) void k_sample_sparse_big(SampleParams p) {
             const int nr = (n - lane + 63) / 64;
             float acc = 0.0f;
             bool found = false;
-            for (int q = 0; q < nr; ++q) {
-              uint32_t e;
-              if (q < SB_RB) {
-                e = 0u;
 #pragma unroll
-                for (int qq = 0; qq < SB_RB; ++qq)
-                  if (qq == q) e = ring[s][qq];
-              } else {
-                e = ent[off + q * 64 + lane];
+            for (int q = 0; q < SB_RB; ++q) {
+              if (q < nr) {
+                int tq;
+                acc = acc + entry_b(ring[s][q], true, tq);
+                if (!found) tsel = tq;
+                if (!found && !(E + acc <= thr)) found = true;
               }
-              int tq;
-              acc = acc + entry_b(e, true, tq);
-              if (!found) tsel = tq;
-              if (!found && !(E + acc <= thr)) found = true;
+            }
+            for (int q0 = SB_RB; q0 < nr && !found; q0 += SB_BATCH) {
+              uint32_t eb[SB_BATCH];
+#pragma unroll
+              for (int b = 0; b < SB_BATCH; ++b)
+                eb[b] = (q0 + b < nr) ? ent[off + (q0 + b) * 64 + lane] : 0u;
+#pragma unroll
+              for (int b = 0; b < SB_BATCH; ++b) {
+                if (q0 + b < nr && !found) {
+                  int tq;
+                  acc = acc + entry_b(eb[b], true, tq);
+                  tsel = tq;
+                  if (!(E + acc <= thr)) found = true;
+                }
+              }
             }
           }
           kn = readlane_i(tsel, lstar);
@@ -1038,13 +1060,19 @@ __global__ __launch_bounds__(256) void k_sample_sparse_big(SampleParams p) {
           if (lane == lstar) {
             int cnt = 0;
             float P_ = 0.0f;
+#pragma nounroll
             for (int g = 0; g < NG; ++g) {
               float a = 0.0f;
+#pragma nounroll
+              for (int q = 0; q < 16; q += 4) {
+                float cf[4];
+                quad_coefs(cf, lane * C + g * 16 + q, zc, invc);
 #pragma unroll
-              for (int j = 0; j < 16; ++j) {
-                a = __builtin_fmaf(coef[lane * C + g * 16 + j], beta, a);
-                const float x = g == 0 ? a : P_ + a;
-                cnt += (E + x <= thr2) ? 1 : 0;
+                for (int j = 0; j < 4; ++j) {
+                  a = __builtin_fmaf(cf[j], beta, a);
+                  const float x = g == 0 ? a : P_ + a;
+                  cnt += (E + x <= thr2) ? 1 : 0;
+                }
               }
               P_ = g == 0 ? a : P_ + a;
             }
@@ -1054,21 +1082,10 @@ __global__ __launch_bounds__(256) void k_sample_sparse_big(SampleParams p) {
         }
 
         // add the token back under its new topic
-        {
-          const int ndk = nd16_get(nd2, kn) + 1;
-          if (lane == 0) nd2[kn >> 1] += (kn & 1) ? 0x10000u : 1u;
-          wave_lds_fence();
-          const int ndz = (kn == zo) ? ndk : nd16_get(nd2, zo);
-          const float cfz = coef_of(zo, ndz, false, 0.0f);
-          const float cfk = coef_of(kn, ndk, false, 0.0f);
-          if (lane == 0) {
-            coef[zo] = cfz;
-            coef[kn] = cfk;
-          }
-          wave_lds_fence();
-          if (lane == lo) regroup(TG, go);
-          if (lane == kn / C) regroup(TG, (kn % C) / 16);
-        }
+        if (lane == 0) nd2[kn >> 1] += (kn & 1) ? 0x10000u : 1u;
+        wave_lds_fence();
+        if (lane == lo) regroup(TG, go, -1, 0.0f);
+        if (lane == kn / C) regroup(TG, (kn % C) / 16, -1, 0.0f);
         cn = (lane == idx) ? kn : cn;
         if (!FROZEN && kn != zo) {
           if (lane < 2) {
@@ -1423,8 +1440,8 @@ static int occupancy_sparse_t() {
 }
 template <int C, bool FROZEN>
 static size_t sparse_big_lds() {
-  // {alpha, inv} table + 4 waves x (nd pairs + coefficients); > 64 KiB at C = 64
-  const size_t lds = (2 * 64 * C + 4 * 3 * 32 * C) * sizeof(int32_t);
+  // {alpha, inv} table + per-wave 16-bit nd pairs; > 64 KiB at C = 64
+  const size_t lds = (2 * 64 * C + sb_waves<C>() * 32 * C) * sizeof(int32_t);
   static bool attr = [lds] {
     return hipFuncSetAttribute(reinterpret_cast<const void*>(&k_sample_sparse_big<C, SPARSE_P, FROZEN>),
                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) == hipSuccess;
@@ -1435,15 +1452,16 @@ static size_t sparse_big_lds() {
 template <int C, bool FROZEN>
 static hipError_t launch_sparse_big_t(const SampleParams& p, int blocks, hipStream_t st) {
   const size_t lds = sparse_big_lds<C, FROZEN>();
-  hipLaunchKernelGGL((k_sample_sparse_big<C, SPARSE_P, FROZEN>), dim3(blocks), dim3(256), lds, st, p);
+  hipLaunchKernelGGL((k_sample_sparse_big<C, SPARSE_P, FROZEN>), dim3(blocks), dim3(64 * sb_waves<C>()),
+                     lds, st, p);
   return hipGetLastError();
 }
 template <int C, bool FROZEN>
 static int occupancy_sparse_big_t() {
   int nb = 0;
   const size_t lds = sparse_big_lds<C, FROZEN>();
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_sample_sparse_big<C, SPARSE_P, FROZEN>, 256,
-                                                   lds) != hipSuccess)
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_sample_sparse_big<C, SPARSE_P, FROZEN>,
+                                                   64 * sb_waves<C>(), lds) != hipSuccess)
     return 1;
   return nb > 0 ? nb : 1;
 }
