@@ -153,6 +153,45 @@ lda_status lda_infer(lda_ctx* ctx, int64_t Dh, const int64_t* doc_off, const int
 lda_status lda_to_mallet_packed(lda_ctx* ctx, int32_t* rows, int64_t* row_off,
                                 int32_t* topic_bits);
 
+/* ---- hyperparameter optimisation ----------------------
+ * Mallet 2.0.7 ParallelTopicModel.optimizeAlpha / optimizeBeta, enabled by
+ * setOptimizeInterval(20) [src/cmu_ron/TrainAndPredict.java:163,
+ * src/cmu/TrainAndPredict.java:261].  The GPU builds the integer statistics;
+ * the fp64 fixed-point updates run on the host. */
+
+/* Longest document of this shard (sizes the histograms below). */
+lda_status lda_max_doc_length(lda_ctx* ctx, int32_t* max_len);
+/* WorkerRunnable's alpha statistics from the current z of this shard, ADDED
+ * into caller buffers (accumulate over the sampled sweeps, sum across ranks):
+ * doc_len_counts[max_len+1]: documents of each length (docLengthCounts);
+ * topic_doc_counts[K*(max_len+1)], row k: documents in which topic k has
+ * each count > 0 (topicDocCounts).  max_len >= lda_max_doc_length. */
+lda_status lda_doc_topic_histograms(lda_ctx* ctx, int32_t max_len, int32_t* doc_len_counts,
+                                    int32_t* topic_doc_counts);
+/* optimizeBeta's countHistogram, ADDED into count_hist[max_count+1]: cells
+ * (w, k) of the global nw holding each count c > 0 (identical on every rank:
+ * do not sum it across ranks).  LDA_ERR_INVALID_ARG if a cell exceeds
+ * max_count (the largest word total bounds every cell). */
+lda_status lda_count_histogram(lda_ctx* ctx, int64_t max_count, int32_t* count_hist);
+
+/* Dirichlet.learnParameters(params, observations, observationLengths, shape,
+ * scale, iterations): Minka's fixed point with a Gamma(shape, scale) prior;
+ * params[K] updated in place, params_sum = their new sum.  Host-only. */
+lda_status lda_learn_parameters(double* params, int32_t K, const int32_t* observations,
+                                const int32_t* observation_lengths, int32_t max_len, double shape,
+                                double scale, int32_t iterations, double* params_sum);
+/* Dirichlet.learnSymmetricConcentration(countHistogram, observationLengths,
+ * numDimensions, currentValue): 200 fixed-point steps for a symmetric
+ * Dirichlet's total concentration.  count_hist[max_count+1]; the observation
+ * length histogram is given sparsely as ascending (lengths[j], length_counts[j])
+ * pairs (topic sizes reach ~1e9 at C4).  Host-only. */
+lda_status lda_learn_symmetric_concentration(const int32_t* count_hist, int64_t max_count,
+                                             const int64_t* lengths, const int32_t* length_counts,
+                                             int64_t n_lengths, int32_t num_dims, double current,
+                                             double* out);
+/* Dirichlet.digamma (the series the estimators use).  Host-only. */
+double lda_digamma(double z);
+
 /* Kernel-level timing of the last lda_sample (ms, HIP events on the
  * context's stream). */
 lda_status lda_last_sample_ms(lda_ctx* ctx, float* ms);

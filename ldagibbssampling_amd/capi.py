@@ -80,6 +80,15 @@ SIGNATURES = {
     "lda_infer": (C.c_int32, [_vp, C.c_int64, _i64p, _i32p, C.c_int32, C.c_int32, C.c_int32,
                               C.c_uint64, _f64p]),
     "lda_to_mallet_packed": (C.c_int32, [_vp, _vp, _i64p, C.POINTER(C.c_int32)]),
+    "lda_max_doc_length": (C.c_int32, [_vp, C.POINTER(C.c_int32)]),
+    "lda_doc_topic_histograms": (C.c_int32, [_vp, C.c_int32, _i32p, _i32p]),
+    "lda_count_histogram": (C.c_int32, [_vp, C.c_int64, _i32p]),
+    "lda_learn_parameters": (C.c_int32, [_f64p, C.c_int32, _i32p, _i32p, C.c_int32, C.c_double,
+                                         C.c_double, C.c_int32, C.POINTER(C.c_double)]),
+    "lda_learn_symmetric_concentration": (C.c_int32, [_i32p, C.c_int64, _i64p, _i32p, C.c_int64,
+                                                      C.c_int32, C.c_double,
+                                                      C.POINTER(C.c_double)]),
+    "lda_digamma": (C.c_double, [C.c_double]),
     "lda_last_sample_ms": (C.c_int32, [_vp, C.POINTER(C.c_float)]),
     "lda_last_error": (C.c_char_p, []),
     "lda_version": (C.c_char_p, []),

@@ -598,6 +598,59 @@ lda_status lda_log_likelihood(lda_ctx* c, double* out) {
   return LDA_OK;
 }
 
+lda_status lda_max_doc_length(lda_ctx* c, int32_t* max_len) {
+  if (!c || !max_len) return fail(LDA_ERR_INVALID_ARG, "null argument");
+  int64_t m = 0;
+  for (int64_t d = 0; d < c->D; ++d) m = std::max(m, c->doc_off_h[d + 1] - c->doc_off_h[d]);
+  *max_len = (int32_t)m;
+  return LDA_OK;
+}
+
+lda_status lda_doc_topic_histograms(lda_ctx* c, int32_t max_len, int32_t* doc_len_counts,
+                                    int32_t* topic_doc_counts) {
+  if (!c || !doc_len_counts || !topic_doc_counts) return fail(LDA_ERR_INVALID_ARG, "null argument");
+  int32_t m = 0;
+  lda_max_doc_length(c, &m);
+  if (max_len < m) return fail(LDA_ERR_INVALID_ARG, "max_len below the longest document");
+  if (c->pending) return fail(LDA_ERR_STATE, "histograms with a pending delta: call lda_apply first");
+  HIP_TRY(hipSetDevice(c->device));
+  const int64_t L1 = (int64_t)max_len + 1;
+  const size_t n = (size_t)L1 + (size_t)c->K * L1;
+  int32_t* buf = nullptr;
+  HIP_TRY(dalloc(&buf, n));
+  std::vector<int32_t> h(n);
+  hipError_t e = hipMemsetAsync(buf, 0, n * sizeof(int32_t), c->stream);
+  if (e == hipSuccess)
+    e = lda::launch_doc_hist(c->z, c->doc_off, c->D, c->K, c->Kp, max_len, buf, buf + L1, c->stream);
+  if (e == hipSuccess) e = hipMemcpyAsync(h.data(), buf, n * sizeof(int32_t), hipMemcpyDeviceToHost, c->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+  (void)hipFree(buf);
+  HIP_TRY(e);
+  for (int64_t i = 0; i < L1; ++i) doc_len_counts[i] += h[i];
+  for (size_t i = 0; i < (size_t)c->K * L1; ++i) topic_doc_counts[i] += h[L1 + i];
+  return LDA_OK;
+}
+
+lda_status lda_count_histogram(lda_ctx* c, int64_t max_count, int32_t* count_hist) {
+  if (!c || !count_hist || max_count < 0) return fail(LDA_ERR_INVALID_ARG, "bad argument");
+  if (c->pending) return fail(LDA_ERR_STATE, "histogram with a pending delta: call lda_apply first");
+  HIP_TRY(hipSetDevice(c->device));
+  const size_t n = (size_t)max_count + 1;
+  int32_t* buf = nullptr;
+  HIP_TRY(dalloc(&buf, n + 1));
+  std::vector<int32_t> h(n + 1);
+  hipError_t e = hipMemsetAsync(buf, 0, (n + 1) * sizeof(int32_t), c->stream);
+  if (e == hipSuccess)
+    e = lda::launch_count_hist(c->nw, c->V, c->K, c->Kp, max_count, buf, buf + n, c->stream);
+  if (e == hipSuccess) e = hipMemcpyAsync(h.data(), buf, (n + 1) * sizeof(int32_t), hipMemcpyDeviceToHost, c->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+  (void)hipFree(buf);
+  HIP_TRY(e);
+  if (h[n]) return fail(LDA_ERR_INVALID_ARG, "an nw cell exceeds max_count");
+  for (size_t i = 0; i < n; ++i) count_hist[i] += h[i];
+  return LDA_OK;
+}
+
 lda_status lda_infer(lda_ctx* c, int64_t Dh, const int64_t* doc_off, const int32_t* words,
                      int32_t n_iter, int32_t burn_in, int32_t thin, uint64_t seed, double* theta) {
   if (!c || !doc_off || !theta) return fail(LDA_ERR_INVALID_ARG, "null argument");

@@ -83,6 +83,10 @@ hipError_t launch_ll_docs(const int32_t* z, const int64_t* doc_off, int64_t D, c
 hipError_t launch_ll_words(const int32_t* nw, int64_t V, int32_t K, int32_t Kp, double beta,
                            double* partial, unsigned long long* nonzero, int blocks,
                            hipStream_t st);
+hipError_t launch_doc_hist(const int32_t* z, const int64_t* doc_off, int64_t D, int32_t K, int32_t Kp,
+                           int32_t L, int32_t* len_hist, int32_t* topic_hist, hipStream_t st);
+hipError_t launch_count_hist(const int32_t* nw, int64_t V, int32_t K, int32_t Kp, int64_t max_count,
+                             int32_t* hist, int32_t* overflow, hipStream_t st);
 hipError_t launch_infer_init(const int32_t* words, int32_t* z, int64_t n, const int32_t* nw,
                              int32_t K, int32_t Kp, hipStream_t st);
 

@@ -1255,6 +1255,7 @@ __global__ __launch_bounds__(256) void k_doc_topics(const int32_t* __restrict__ 
   for (int i = lane; i < Kp; i += 64) hist[i] = 0;
   for (int64_t d = (int64_t)blockIdx.x * 4 + wid; d < D; d += (int64_t)gridDim.x * 4) {
     for (int64_t i = doc_off[d] + lane; i < doc_off[d + 1]; i += 64) atomicAdd(&hist[z[i]], 1);
+    wave_lds_fence();
     for (int k = lane; k < K; k += 64) {
       const int32_t c = hist[k];
       if (accumulate)
@@ -1263,6 +1264,7 @@ __global__ __launch_bounds__(256) void k_doc_topics(const int32_t* __restrict__ 
         out[d * K + k] = c;
     }
     for (int k = lane; k < Kp; k += 64) hist[k] = 0;
+    wave_lds_fence();
   }
 }
 
@@ -1303,12 +1305,14 @@ __global__ __launch_bounds__(256) void k_ll_docs(const int32_t* __restrict__ z,
   double acc = 0.0;
   for (int64_t d = (int64_t)blockIdx.x * 4 + wid; d < D; d += (int64_t)gridDim.x * 4) {
     for (int64_t i = doc_off[d] + lane; i < doc_off[d + 1]; i += 64) atomicAdd(&hist[z[i]], 1);
+    wave_lds_fence();
     for (int k = lane; k < K; k += 64) {
       const int32_t c = hist[k];
       if (c > 0) acc += log_gamma_stirling(alpha[k] + c) - log_gamma_stirling(alpha[k]);
       hist[k] = 0;
     }
     if (lane == 0) acc -= log_gamma_stirling(alpha_sum + (double)(doc_off[d + 1] - doc_off[d]));
+    wave_lds_fence();
   }
   acc = wave_sum_d(acc);
   if (lane == 0) wsum[wid] = acc;
@@ -1350,6 +1354,60 @@ __global__ __launch_bounds__(256) void k_ll_words(const int32_t* __restrict__ nw
 }
 
 // TopicInferencer init: most frequent topic of the word (ties -> larger id).
+// Mallet's alpha statistics (WorkerRunnable, shouldSaveState): per document
+// docLengthCounts[len]++ and topicDocCounts[k][n_dk]++ for every n_dk > 0;
+// one wavefront per document, the document's counts in LDS.
+__global__ __launch_bounds__(256) void k_doc_hist(const int32_t* __restrict__ z,
+                                                  const int64_t* __restrict__ doc_off, int64_t D,
+                                                  int32_t K, int32_t Kp, int32_t L,
+                                                  int32_t* __restrict__ len_hist,
+                                                  int32_t* __restrict__ topic_hist) {
+  extern __shared__ __attribute__((aligned(16))) int32_t h[];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  int32_t* hist = h + wid * Kp;
+  for (int i = lane; i < Kp; i += 64) hist[i] = 0;
+  wave_lds_fence();
+  for (int64_t d = (int64_t)blockIdx.x * 4 + wid; d < D; d += (int64_t)gridDim.x * 4) {
+    for (int64_t i = doc_off[d] + lane; i < doc_off[d + 1]; i += 64) atomicAdd(&hist[z[i]], 1);
+    wave_lds_fence();
+    if (lane == 0) atomicAdd(&len_hist[doc_off[d + 1] - doc_off[d]], 1);
+    for (int k = lane; k < K; k += 64) {
+      const int32_t c = hist[k];
+      if (c > 0) atomicAdd(&topic_hist[(int64_t)k * (L + 1) + c], 1);
+      hist[k] = 0;
+    }
+    wave_lds_fence();
+  }
+}
+
+// optimizeBeta's countHistogram: cells of nw (k < K) holding each count > 0.
+// Small counts are binned in LDS first (they are most of the cells).
+#define COUNT_HIST_LDS 4096
+__global__ __launch_bounds__(256) void k_count_hist(const int32_t* __restrict__ nw, int64_t V,
+                                                    int32_t K, int32_t Kp, int64_t max_count,
+                                                    int32_t* __restrict__ hist,
+                                                    int32_t* __restrict__ overflow) {
+  __shared__ int32_t sh[COUNT_HIST_LDS];
+  for (int i = threadIdx.x; i < COUNT_HIST_LDS; i += 256) sh[i] = 0;
+  __syncthreads();
+  const int64_t n = V * Kp;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    const int k = (int)(i & (Kp - 1));
+    const int32_t c = nw[i];
+    if (k < K && c > 0) {
+      if ((int64_t)c > max_count)
+        atomicOr(overflow, 1);
+      else if (c < COUNT_HIST_LDS)
+        atomicAdd(&sh[c], 1);
+      else
+        atomicAdd(&hist[c], 1);
+    }
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < COUNT_HIST_LDS && i <= max_count; i += 256)
+    if (sh[i]) atomicAdd(&hist[i], sh[i]);
+}
+
 __global__ __launch_bounds__(256) void k_infer_init(const int32_t* __restrict__ words,
                                                     int32_t* __restrict__ z, int64_t n,
                                                     const int32_t* __restrict__ nw, int32_t K,
@@ -1441,8 +1499,8 @@ static int occupancy_sparse_t() {
 template <int C, bool FROZEN>
 static size_t sparse_big_lds() {
   // {alpha, inv} table + per-wave 16-bit nd pairs; > 64 KiB at C = 64
-  const size_t lds = (2 * 64 * C + sb_waves<C>() * 32 * C) * sizeof(int32_t);
-  static bool attr = [lds] {
+  constexpr size_t lds = (2 * 64 * C + sb_waves<C>() * 32 * C) * sizeof(int32_t);
+  static bool attr = [] {
     return hipFuncSetAttribute(reinterpret_cast<const void*>(&k_sample_sparse_big<C, SPARSE_P, FROZEN>),
                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) == hipSuccess;
   }();
@@ -1591,6 +1649,24 @@ hipError_t launch_ll_words(const int32_t* nw, int64_t V, int32_t K, int32_t Kp, 
                            hipStream_t st) {
   hipLaunchKernelGGL(k_ll_words, dim3(blocks), dim3(256), 0, st, nw, V, K, Kp, beta, partial,
                      nonzero);
+  return hipGetLastError();
+}
+
+hipError_t launch_doc_hist(const int32_t* z, const int64_t* doc_off, int64_t D, int32_t K, int32_t Kp,
+                           int32_t L, int32_t* len_hist, int32_t* topic_hist, hipStream_t st) {
+  if (D <= 0) return hipSuccess;
+  const int blocks = (int)std::min<int64_t>((D + 3) / 4, 4096);
+  hipLaunchKernelGGL(k_doc_hist, dim3(blocks), dim3(256), 4 * Kp * sizeof(int32_t), st, z, doc_off, D,
+                     K, Kp, L, len_hist, topic_hist);
+  return hipGetLastError();
+}
+
+hipError_t launch_count_hist(const int32_t* nw, int64_t V, int32_t K, int32_t Kp, int64_t max_count,
+                             int32_t* hist, int32_t* overflow, hipStream_t st) {
+  if (V <= 0) return hipSuccess;
+  const int blocks = (int)std::min<int64_t>((V * Kp + 255) / 256, 4096);
+  hipLaunchKernelGGL(k_count_hist, dim3(blocks), dim3(256), 0, st, nw, V, K, Kp, max_count, hist,
+                     overflow);
   return hipGetLastError();
 }
 

@@ -183,6 +183,35 @@ class GibbsSampler:
                                      int(thin), int(seed) & (2**64 - 1), theta), "lda_infer")
         return theta
 
+    # ------------------------------------------- hyperparameter statistics
+    def max_doc_length(self) -> int:
+        m = C.c_int32()
+        capi.check(self._L.lda_max_doc_length(self._h, C.byref(m)), "lda_max_doc_length")
+        return m.value
+
+    def doc_topic_histograms(self, doc_len_counts=None, topic_doc_counts=None, max_len=None):
+        """Add this shard's (docLengthCounts, topicDocCounts) from the current z
+        into the given int32 arrays (allocated when None) and return them."""
+        if max_len is None:
+            max_len = self.max_doc_length() if doc_len_counts is None else len(doc_len_counts) - 1
+        if doc_len_counts is None:
+            doc_len_counts = np.zeros(max_len + 1, dtype=np.int32)
+        if topic_doc_counts is None:
+            topic_doc_counts = np.zeros((self.K, max_len + 1), dtype=np.int32)
+        assert doc_len_counts.dtype == np.int32 and topic_doc_counts.dtype == np.int32
+        assert doc_len_counts.shape == (max_len + 1,) and topic_doc_counts.shape == (self.K, max_len + 1)
+        capi.check(self._L.lda_doc_topic_histograms(self._h, int(max_len), doc_len_counts,
+                                                    topic_doc_counts), "lda_doc_topic_histograms")
+        return doc_len_counts, topic_doc_counts
+
+    def count_histogram(self, max_count: int, out=None):
+        """optimizeBeta's countHistogram of the global nw (added into `out`)."""
+        if out is None:
+            out = np.zeros(int(max_count) + 1, dtype=np.int32)
+        assert out.dtype == np.int32 and len(out) == int(max_count) + 1
+        capi.check(self._L.lda_count_histogram(self._h, int(max_count), out), "lda_count_histogram")
+        return out
+
     def mallet_packed(self):
         """typeTopicCounts in Mallet's packed layout: (rows, row_off, topic_bits)."""
         row_off = np.zeros(self.V + 1, dtype=np.int64)

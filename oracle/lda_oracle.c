@@ -115,6 +115,96 @@ double orc_log_gamma_stirling(double z) {
 }
 
 /* ======================================================================== */
+/* cc.mallet.types.Dirichlet: digamma, learnParameters,                      */
+/* learnSymmetricConcentration [M] (Minka's fixed-point iterations)          */
+/* ======================================================================== */
+double orc_digamma(double x) {
+  /* psi(x) = psi(x + n) - sum_{j<n} 1/(x + j); asymptotic series above 9.5 */
+  const double EULER = 0.5772156649015328606065121;
+  if (x < 1e-6) return -EULER - 1.0 / x;
+  double acc = 0.0;
+  for (; x < 9.5; x += 1.0) acc -= 1.0 / x;
+  const double r = 1.0 / x, r2 = r * r;
+  const double series =
+      1.0 / 12 - r2 * (1.0 / 120 - r2 * (1.0 / 252 - r2 * (1.0 / 240 - r2 * (1.0 / 132 -
+      r2 * (691.0 / 32760 - r2 * (1.0 / 12))))));
+  return acc + (log(x) - 0.5 * r - r2 * series);
+}
+
+double orc_learn_parameters(double* a, int32_t K, const int32_t* hist, const int32_t* lens,
+                            int32_t L, double shape, double scale, int32_t iters) {
+  const int64_t W = (int64_t)L + 1;
+  double A = 0.0;
+  int64_t* top = (int64_t*)malloc(sizeof(int64_t) * (K > 0 ? K : 1));
+  for (int32_t k = 0; k < K; ++k) {
+    A += a[k];
+    top[k] = -1;
+    for (int64_t i = W - 1; i >= 0; --i)
+      if (hist[k * W + i] > 0) {
+        top[k] = i;
+        break;
+      }
+  }
+  for (int32_t it = 0; it < iters; ++it) {
+    double den = 0.0, d = 0.0;
+    for (int64_t n = 1; n < W; ++n) {
+      d += 1.0 / (A + n - 1);
+      den += lens[n] * d;
+    }
+    den -= 1.0 / scale;
+    A = 0.0;
+    for (int32_t k = 0; k < K; ++k) {
+      const double ak = a[k];
+      double num = 0.0;
+      d = 0.0;
+      for (int64_t i = 1; i <= top[k]; ++i) {
+        d += 1.0 / (ak + i - 1);
+        num += hist[k * W + i] * d;
+      }
+      a[k] = ak * (num + shape) / den;
+      A += a[k];
+    }
+  }
+  free(top);
+  return A;
+}
+
+/* observation lengths as a DENSE histogram lens[0..max_len] (Mallet's form) */
+double orc_learn_symmetric_concentration(const int32_t* counts, int64_t max_count,
+                                         const int32_t* lens, int64_t max_len, int32_t dims,
+                                         double value) {
+  int64_t top = 0;
+  for (int64_t c = max_count; c > 0; --c)
+    if (counts[c] > 0) {
+      top = c;
+      break;
+    }
+  for (int it = 0; it < 200; ++it) {
+    const double p = value / dims;
+    double num = 0.0, d = 0.0;
+    for (int64_t c = 1; c <= top; ++c) {
+      d += 1.0 / (p + c - 1);
+      num += counts[c] * d;
+    }
+    const double psi0 = orc_digamma(value);
+    double den = 0.0;
+    int64_t last = 0;
+    d = 0.0;
+    for (int64_t n = 0; n <= max_len; ++n) {
+      if (lens[n] <= 0) continue;
+      if (n - last > 20)
+        d = orc_digamma(value + n) - psi0;
+      else
+        for (int64_t i = last; i < n; ++i) d += 1.0 / (value + i);
+      den += d * lens[n];
+      last = n;
+    }
+    value = p * num / den;
+  }
+  return value;
+}
+
+/* ======================================================================== */
 /* cpu_exact                                                                */
 /* ======================================================================== */
 struct orc_exact {
@@ -592,6 +682,9 @@ typedef struct {
   int64_t start_doc, num_docs;
   int32_t *local_counts, *local_index;
   double* term_scores;
+  int collect;                 /* shouldSaveState: record alpha statistics */
+  int32_t* doc_len_counts;     /* [max_len+1] */
+  int32_t* topic_doc_counts;   /* [K][max_len+1] */
 } mallet_worker;
 
 struct orc_mallet {
@@ -609,6 +702,9 @@ struct orc_mallet {
   int32_t* tpt;  /* global tokensPerTopic */
   mallet_worker* workers;
   int64_t seed;
+  /* hyperparameter optimisation (setOptimizeInterval / setBurninPeriod) */
+  int32_t optimize_interval, burnin, save_sample_interval, symmetric_alpha;
+  int32_t max_len;
 };
 
 static int32_t** ttc_alloc(const orc_mallet* m) {
@@ -723,7 +819,73 @@ orc_mallet* orc_mallet_create(int32_t K, double alpha_sum, double beta, int32_t 
     wk->term_scores = (double*)calloc(K, sizeof(double));
     orc_jrandom_seed(&wk->rng, seed);
   }
+  m->burnin = 200;
+  m->save_sample_interval = 10;
+  m->max_len = 0;
+  for (int64_t d = 0; d < D; ++d)
+    if (m->doc_off[d + 1] - m->doc_off[d] > m->max_len) m->max_len = (int32_t)(m->doc_off[d + 1] - m->doc_off[d]);
+  for (int t = 0; t < m->T; ++t) {
+    m->workers[t].doc_len_counts = (int32_t*)calloc(m->max_len + 1, sizeof(int32_t));
+    m->workers[t].topic_doc_counts = (int32_t*)calloc((size_t)K * (m->max_len + 1), sizeof(int32_t));
+  }
   return m;
+}
+
+void orc_mallet_set_optimize(orc_mallet* m, int32_t interval, int32_t burnin, int32_t symmetric) {
+  m->optimize_interval = interval;
+  m->burnin = burnin;
+  m->symmetric_alpha = symmetric;
+}
+
+void orc_mallet_get_hyper(const orc_mallet* m, double* alpha, double* beta) {
+  if (alpha) memcpy(alpha, m->alpha, sizeof(double) * m->K);
+  if (beta) *beta = m->beta;
+}
+
+/* ParallelTopicModel.optimizeAlpha [M] */
+static void mallet_optimize_alpha(orc_mallet* m) {
+  const int64_t W = (int64_t)m->max_len + 1;
+  int32_t* lens = (int32_t*)calloc(W, sizeof(int32_t));
+  int32_t* hist = (int32_t*)calloc((size_t)m->K * W, sizeof(int32_t));
+  for (int t = 0; t < m->T; ++t) {
+    mallet_worker* wk = &m->workers[t];
+    for (int64_t i = 0; i < W; ++i) {
+      lens[i] += wk->doc_len_counts[i];
+      wk->doc_len_counts[i] = 0;
+    }
+    for (int k = 0; k < m->K; ++k)
+      for (int64_t i = 0; i < W; ++i) {
+        /* symmetric alpha pools every topic into row 0 */
+        hist[(m->symmetric_alpha ? 0 : k) * W + i] += wk->topic_doc_counts[k * W + i];
+        wk->topic_doc_counts[k * W + i] = 0;
+      }
+  }
+  if (m->symmetric_alpha) {
+    m->alpha_sum = orc_learn_symmetric_concentration(hist, W - 1, lens, W - 1, m->K, m->alpha_sum);
+    for (int k = 0; k < m->K; ++k) m->alpha[k] = m->alpha_sum / m->K;
+  } else {
+    m->alpha_sum = orc_learn_parameters(m->alpha, m->K, hist, lens, m->max_len, 1.001, 1.0, 1);
+  }
+  free(lens);
+  free(hist);
+}
+
+/* ParallelTopicModel.optimizeBeta [M] */
+static void mallet_optimize_beta(orc_mallet* m) {
+  int32_t max_type = 0, max_topic = 0;
+  for (int w = 0; w < m->V; ++w)
+    if (m->type_totals[w] > max_type) max_type = m->type_totals[w];
+  for (int k = 0; k < m->K; ++k)
+    if (m->tpt[k] > max_topic) max_topic = m->tpt[k];
+  int32_t* counts = (int32_t*)calloc((size_t)max_type + 1, sizeof(int32_t));
+  int32_t* sizes = (int32_t*)calloc((size_t)max_topic + 1, sizeof(int32_t));
+  for (int w = 0; w < m->V; ++w)
+    for (int p = 0; p < m->row_len[w] && m->ttc[w][p] > 0; ++p) counts[m->ttc[w][p] >> m->topic_bits]++;
+  for (int k = 0; k < m->K; ++k) sizes[m->tpt[k]]++;
+  m->beta_sum = orc_learn_symmetric_concentration(counts, max_type, sizes, max_topic, m->V, m->beta_sum);
+  m->beta = m->beta_sum / m->V;
+  free(counts);
+  free(sizes);
 }
 
 void orc_mallet_destroy(orc_mallet* m) {
@@ -735,6 +897,7 @@ void orc_mallet_destroy(orc_mallet* m) {
       free(wk->tpt);
     }
     free(wk->cached); free(wk->local_counts); free(wk->local_index); free(wk->term_scores);
+    free(wk->doc_len_counts); free(wk->topic_doc_counts);
   }
   free(m->workers);
   ttc_free(m, m->ttc);
@@ -901,6 +1064,11 @@ static void mallet_sample_doc(const orc_mallet* m, mallet_worker* wk, int64_t d)
     wk->smoothing_only_mass += alpha[new_topic] * beta / (tpt[new_topic] + beta_sum);
     topic_beta_mass += beta * lc[new_topic] / (tpt[new_topic] + beta_sum);
   }
+  if (wk->collect) {
+    const int64_t W = (int64_t)m->max_len + 1;
+    wk->doc_len_counts[len]++;
+    for (dense = 0; dense < nonzero; ++dense) wk->topic_doc_counts[li[dense] * W + lc[li[dense]]]++;
+  }
   for (dense = 0; dense < nonzero; ++dense) {
     int k = li[dense];
     cached[k] = alpha[k] / (tpt[k] + beta_sum);
@@ -984,6 +1152,8 @@ void orc_mallet_estimate(orc_mallet* m, int32_t n_iter) {
   mallet_job* jobs = (mallet_job*)malloc(sizeof(mallet_job) * m->T);
   pthread_t* th = (pthread_t*)malloc(sizeof(pthread_t) * m->T);
   for (int it = 1; it <= n_iter; ++it) {
+    const int opt_on = it > m->burnin && m->optimize_interval != 0;
+    for (int t = 0; t < m->T; ++t) m->workers[t].collect = opt_on && it % m->save_sample_interval == 0;
     if (m->T > 1) {
       for (int t = 0; t < m->T; ++t) {
         jobs[t].m = m;
@@ -996,6 +1166,11 @@ void orc_mallet_estimate(orc_mallet* m, int32_t n_iter) {
       jobs[0].m = m;
       jobs[0].t = 0;
       mallet_worker_run(&jobs[0]);
+    }
+    for (int t = 0; t < m->T; ++t) m->workers[t].collect = 0;
+    if (opt_on && it % m->optimize_interval == 0) {
+      mallet_optimize_alpha(m);
+      mallet_optimize_beta(m);
     }
   }
   free(jobs);

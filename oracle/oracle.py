@@ -51,6 +51,14 @@ def lib():
     L.orc_jrandom_next_double.argtypes = [C.c_void_p]
     L.orc_log_gamma_stirling.restype = C.c_double
     L.orc_log_gamma_stirling.argtypes = [C.c_double]
+    L.orc_digamma.restype = C.c_double
+    L.orc_digamma.argtypes = [C.c_double]
+    L.orc_learn_parameters.restype = C.c_double
+    L.orc_learn_parameters.argtypes = [_f64p, C.c_int32, _i32p, _i32p, C.c_int32, C.c_double,
+                                       C.c_double, C.c_int32]
+    L.orc_learn_symmetric_concentration.restype = C.c_double
+    L.orc_learn_symmetric_concentration.argtypes = [_i32p, C.c_int64, _i32p, C.c_int64, C.c_int32,
+                                                    C.c_double]
 
     L.orc_exact_create.restype = C.c_void_p
     L.orc_exact_create.argtypes = [C.c_int32, C.c_int32, C.c_int64, _i64p, _i32p, C.c_void_p,
@@ -81,6 +89,8 @@ def lib():
                                     _i64p, _i32p, C.c_int64, C.c_int32]
     L.orc_mallet_destroy.argtypes = [C.c_void_p]
     L.orc_mallet_estimate.argtypes = [C.c_void_p, C.c_int32]
+    L.orc_mallet_set_optimize.argtypes = [C.c_void_p, C.c_int32, C.c_int32, C.c_int32]
+    L.orc_mallet_get_hyper.argtypes = [C.c_void_p, _f64p, C.POINTER(C.c_double)]
     L.orc_mallet_log_likelihood.restype = C.c_double
     L.orc_mallet_log_likelihood.argtypes = [C.c_void_p]
     L.orc_mallet_get_z.argtypes = [C.c_void_p, _i32p]
@@ -114,6 +124,29 @@ def u01(x: int) -> float:
 
 def log_gamma_stirling(z: float) -> float:
     return float(lib().orc_log_gamma_stirling(z))
+
+
+def digamma(x: float) -> float:
+    return float(lib().orc_digamma(x))
+
+
+def learn_parameters(alpha, topic_doc_counts, doc_len_counts, shape=1.001, scale=1.0, iters=1):
+    """Dirichlet.learnParameters: returns (new alpha, new alpha sum)."""
+    a = np.ascontiguousarray(alpha, dtype=np.float64).copy()
+    h = np.ascontiguousarray(topic_doc_counts, dtype=np.int32)
+    lens = np.ascontiguousarray(doc_len_counts, dtype=np.int32)
+    K, W = h.shape
+    assert len(lens) == W and len(a) == K
+    s = lib().orc_learn_parameters(a, K, h, lens, W - 1, shape, scale, iters)
+    return a, float(s)
+
+
+def learn_symmetric_concentration(count_hist, length_hist, dims, value) -> float:
+    """Dirichlet.learnSymmetricConcentration with DENSE histograms."""
+    c = np.ascontiguousarray(count_hist, dtype=np.int32)
+    lens = np.ascontiguousarray(length_hist, dtype=np.int32)
+    return float(lib().orc_learn_symmetric_concentration(c, len(c) - 1, lens, len(lens) - 1,
+                                                         dims, value))
 
 
 class JavaRandom:
@@ -245,6 +278,17 @@ class MalletModel:
 
     def estimate(self, n_iter):
         lib().orc_mallet_estimate(self._h, int(n_iter))
+
+    def set_optimize(self, interval: int, burnin: int = 200, symmetric: bool = False):
+        """setOptimizeInterval / setBurninPeriod / setSymmetricAlpha."""
+        lib().orc_mallet_set_optimize(self._h, int(interval), int(burnin), int(bool(symmetric)))
+
+    def hyper(self):
+        """(alpha[K], beta) after any optimisation."""
+        a = np.empty(self.K, dtype=np.float64)
+        b = C.c_double()
+        lib().orc_mallet_get_hyper(self._h, a, C.byref(b))
+        return a, b.value
 
     def log_likelihood(self) -> float:
         return float(lib().orc_mallet_log_likelihood(self._h))

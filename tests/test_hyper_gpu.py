@@ -1,0 +1,74 @@
+"""GPU statistics for hyperparameter optimisation: bit-exact integer
+histograms (Mallet's docLengthCounts / topicDocCounts / countHistogram)
+against numpy on the same state."""
+import numpy as np
+import pytest
+
+from ldagibbssampling_amd.corpus import synthetic_lda
+
+pytestmark = pytest.mark.gpu
+
+
+def _nd(z, doc_off, K):
+    D = len(doc_off) - 1
+    nd = np.zeros((D, K), np.int64)
+    doc = np.repeat(np.arange(D), np.diff(doc_off))
+    np.add.at(nd, (doc, z), 1)
+    return nd
+
+
+@pytest.mark.parametrize("kind,K", [("dense", 20), ("dense", 512), ("sparse", 2048)])
+def test_doc_topic_histograms(kind, K):
+    from ldagibbssampling_amd.sampler import GibbsSampler
+    c = synthetic_lda(num_docs=300, num_types=500, num_topics=min(K, 50), doc_len=None,
+                      mean_len=70, min_len=0, max_len=600, seed=K)
+    g = GibbsSampler(K, c.num_types, c.doc_off, c.words, 0.1, 0.01, seed=2, sampler=kind)
+    g.sweep(2)
+    lens = np.diff(c.doc_off)
+    L = g.max_doc_length()
+    assert L == lens.max()
+    dl, td = g.doc_topic_histograms()
+    g.doc_topic_histograms(dl, td)                        # accumulates
+    nd = _nd(g.z(), c.doc_off, K)
+    exp_dl = 2 * np.bincount(lens, minlength=L + 1)
+    exp_td = np.zeros((K, L + 1), np.int64)
+    for k in range(K):
+        v = nd[:, k]
+        exp_td[k] = 2 * np.bincount(v[v > 0], minlength=L + 1)
+    np.testing.assert_array_equal(dl, exp_dl)
+    np.testing.assert_array_equal(td, exp_td)
+    with pytest.raises(Exception):
+        g.doc_topic_histograms(max_len=L - 1)
+
+
+@pytest.mark.parametrize("K", [100, 4096])
+def test_count_histogram(K):
+    from ldagibbssampling_amd.sampler import GibbsSampler
+    c = synthetic_lda(num_docs=400, num_types=300, num_topics=20, doc_len=None, mean_len=300,
+                      min_len=1, max_len=900, seed=5)
+    g = GibbsSampler(K, c.num_types, c.doc_off, c.words, 0.1, 0.01, seed=3,
+                     sampler="sparse" if K > 1024 else "dense")
+    g.sweep(3)
+    nw = g.counts()[0]
+    top = int(np.bincount(c.words).max())
+    h = g.count_histogram(top)
+    v = nw[nw > 0]
+    np.testing.assert_array_equal(h, np.bincount(v, minlength=top + 1))
+    with pytest.raises(Exception):
+        g.count_histogram(int(v.max()) - 1)
+
+
+def test_count_histogram_large_cells():
+    """Cells >= 4096 take the global-atomic bins (small ones go through LDS)."""
+    from ldagibbssampling_amd.corpus import Corpus
+    from ldagibbssampling_amd.sampler import GibbsSampler
+    rng = np.random.default_rng(6)
+    D, L = 20, 3000
+    words = np.where(rng.random(D * L) < 0.6, 0, rng.integers(1, 40, D * L)).astype(np.int32)
+    c = Corpus(np.arange(D + 1, dtype=np.int64) * L, words, 40)
+    g = GibbsSampler(2, 40, c.doc_off, c.words, 0.1, 0.01, seed=1)
+    g.sweep(2)
+    nw = g.counts()[0]
+    assert nw.max() >= 4096
+    top = int(np.bincount(words).max())
+    np.testing.assert_array_equal(g.count_histogram(top), np.bincount(nw[nw > 0], minlength=top + 1))
