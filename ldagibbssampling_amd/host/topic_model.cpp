@@ -1,0 +1,682 @@
+// topic_model.cpp — ParallelTopicModel host mirror (see topic_model.hpp) and
+// the C ABI of include/lda_topic_model.h.
+//
+// Mallet 2.0.7 behaviour restated here (cc.mallet.topics.ParallelTopicModel,
+// not vendored; call sites src/cmu_ron/TrainAndPredict.java:159-177):
+//  * addInstances: new documents get random topics, earlier ones keep theirs;
+//    counts are rebuilt from every document.
+//  * estimate(): for iteration = 1..numIterations: topic display every
+//    showTopicsInterval; one parallel sweep (AD-LDA: every shard samples
+//    against the same nw snapshot, then the deltas are summed); alpha
+//    statistics on sweeps with iteration > burninPeriod and
+//    iteration % saveSampleInterval == 0; optimizeAlpha + optimizeBeta when
+//    iteration > burninPeriod and iteration % optimizeInterval == 0;
+//    "<iteration> LL/token: x" every 10 iterations.
+//  * optimizeAlpha: Dirichlet.learnParameters(alpha, topicDocCounts,
+//    docLengthCounts, 1.001, 1.0, 1), or learnSymmetricConcentration over the
+//    pooled histogram when usingSymmetricAlpha; histograms then cleared.
+//  * optimizeBeta: learnSymmetricConcentration(countHistogram,
+//    topicSizeHistogram, numTypes, betaSum); beta = betaSum / numTypes.
+#include "topic_model.hpp"
+
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <fstream>
+#include <numeric>
+#include <sstream>
+
+#include "../../include/lda_topic_model.h"
+#include "java_format.hpp"
+
+namespace lda_host {
+
+namespace {
+
+[[noreturn]] void raise(lda_status s, const std::string& msg) { throw Error{s, msg}; }
+
+void check(lda_status s, const char* where) {
+  if (s != LDA_OK) {
+    const char* m = lda_last_error();
+    raise(s, std::string(where) + ": " + (m ? m : ""));
+  }
+}
+
+}  // namespace
+
+// ----------------------------------------------------------------- shards
+// One lda_ctx per GPU over a contiguous, token-balanced document range; the
+// delta buffers are summed in place with one RCCL all-reduce per sweep
+// (ncclCommInitAll over the shards' devices, grouped calls from this thread).
+class ShardGroup {
+ public:
+  std::vector<lda_ctx*> ctx;
+  std::vector<int64_t> doc_begin;  // shard g owns documents [doc_begin[g], doc_begin[g+1])
+  std::vector<ncclComm_t> comms;
+
+  ~ShardGroup() {
+    for (auto c : comms) ncclCommDestroy(c);
+    for (auto c : ctx) lda_destroy(c);
+  }
+
+  void reduce() {
+    if (ctx.size() < 2) return;
+    std::vector<void*> ptr(ctx.size());
+    std::vector<hipStream_t> st(ctx.size());
+    size_t count = 0;
+    for (size_t g = 0; g < ctx.size(); ++g) {
+      check(lda_delta_buffer(ctx[g], &ptr[g], &count), "lda_delta_buffer");
+      void* s = nullptr;
+      check(lda_get_stream(ctx[g], &s), "lda_get_stream");
+      st[g] = static_cast<hipStream_t>(s);
+    }
+    ncclResult_t r = ncclGroupStart();
+    for (size_t g = 0; g < ctx.size() && r == ncclSuccess; ++g)
+      r = ncclAllReduce(ptr[g], ptr[g], count, ncclInt32, ncclSum, comms[g], st[g]);
+    const ncclResult_t r2 = ncclGroupEnd();
+    if (r != ncclSuccess || r2 != ncclSuccess)
+      raise(LDA_ERR_DEVICE, std::string("ncclAllReduce: ") + ncclGetErrorString(r != ncclSuccess ? r : r2));
+  }
+  void sample() {
+    for (auto c : ctx) check(lda_sample(c), "lda_sample");
+  }
+  void apply() {
+    for (auto c : ctx) check(lda_apply(c), "lda_apply");
+  }
+};
+
+// ------------------------------------------------------------------ model
+ParallelTopicModel::ParallelTopicModel(int32_t num_topics, double alpha_sum, double beta)
+    : K_(num_topics), alpha_sum_(alpha_sum), beta_(beta) {
+  if (num_topics < 1 || num_topics > LDA_MAX_TOPICS) raise(LDA_ERR_UNSUPPORTED, "num_topics out of range");
+  if (!(alpha_sum > 0.0) || !(beta > 0.0)) raise(LDA_ERR_INVALID_ARG, "alphaSum and beta must be > 0");
+  alpha_.assign((size_t)K_, alpha_sum / K_);
+}
+
+ParallelTopicModel::~ParallelTopicModel() = default;
+
+// Anything that invalidates the GPU shards first saves the current topic
+// assignments (documents keep their z across re-sharding / addInstances).
+void ParallelTopicModel::markDirty() {
+  if (shards_ && !shards_dirty_) z_cache_ = topics();
+  shards_dirty_ = true;
+}
+
+void ParallelTopicModel::setRandomSeed(int64_t seed) {
+  markDirty();
+  seed_ = (uint64_t)seed;
+}
+
+void ParallelTopicModel::setNumThreads(int32_t n) {
+  if (n < 1) raise(LDA_ERR_INVALID_ARG, "numThreads must be >= 1");
+  markDirty();
+  num_threads_ = n;
+}
+
+void ParallelTopicModel::setSampler(int32_t sampler) {
+  if (sampler != LDA_SAMPLER_DENSE && sampler != LDA_SAMPLER_SPARSE)
+    raise(LDA_ERR_INVALID_ARG, "unknown sampler");
+  markDirty();
+  sampler_ = sampler;
+}
+
+void ParallelTopicModel::setAlphabet(std::vector<std::string> words, int32_t num_types) {
+  if (num_types < V_) raise(LDA_ERR_INVALID_ARG, "the alphabet cannot shrink");
+  if (!words.empty() && (int32_t)words.size() != num_types)
+    raise(LDA_ERR_INVALID_ARG, "alphabet size mismatch");
+  if (num_types != V_) markDirty();
+  alphabet_ = std::move(words);
+  V_ = num_types;
+}
+
+void ParallelTopicModel::addInstances(int64_t D, const int64_t* doc_off, const int32_t* words,
+                                      const char* const* sources) {
+  if (D < 0 || (D > 0 && !doc_off)) raise(LDA_ERR_INVALID_ARG, "bad documents");
+  if (V_ < 1) raise(LDA_ERR_STATE, "set the alphabet before addInstances");
+  markDirty();  // documents already in the model keep their z
+  const int64_t base = doc_off_.back();
+  for (int64_t d = 0; d < D; ++d) {
+    const int64_t a = doc_off[d] - doc_off[0], b = doc_off[d + 1] - doc_off[0];
+    if (b < a) raise(LDA_ERR_INVALID_ARG, "doc_off not monotone");
+    for (int64_t i = a; i < b; ++i) {
+      if (words[i] < 0 || words[i] >= V_) raise(LDA_ERR_INVALID_ARG, "word id outside the alphabet");
+      words_.push_back(words[i]);
+    }
+    doc_off_.push_back(base + b);
+    const bool has = sources && sources[d];
+    sources_.push_back(has ? sources[d] : "");
+    has_source_.push_back(has ? 1 : 0);
+  }
+}
+
+void ParallelTopicModel::log(const std::string& line) const {
+  if (verbosity_ > 0) {
+    std::fputs(line.c_str(), stderr);
+    std::fputc('\n', stderr);
+  }
+}
+
+void ParallelTopicModel::ensureShards() {
+  if (shards_ && !shards_dirty_) return;
+  if (V_ < 1) raise(LDA_ERR_STATE, "no alphabet: call addInstances first");
+  const std::vector<int32_t> keep = z_cache_;  // saved by markDirty (may be shorter than N)
+  shards_.reset();
+  const int64_t D = numDocs(), N = numTokens();
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev < 1) raise(LDA_ERR_DEVICE, "no HIP device");
+  const int G = (int)std::max<int64_t>(1, std::min<int64_t>({(int64_t)num_threads_, (int64_t)ndev, std::max<int64_t>(D, 1)}));
+  auto sg = std::make_unique<ShardGroup>();
+  // token-balanced contiguous document ranges (the cuts Mallet makes by
+  // document count; tokens balance the GPUs' work)
+  sg->doc_begin.push_back(0);
+  for (int g = 1; g < G; ++g) {
+    const int64_t target = N * g / G;
+    int64_t d = std::lower_bound(doc_off_.begin(), doc_off_.end(), target) - doc_off_.begin();
+    d = std::max(d, sg->doc_begin.back());
+    sg->doc_begin.push_back(std::min(d, D));
+  }
+  sg->doc_begin.push_back(D);
+  for (int g = 0; g < G; ++g) {
+    const int64_t d0 = sg->doc_begin[g], d1 = sg->doc_begin[g + 1];
+    lda_config cfg{};
+    cfg.num_topics = K_;
+    cfg.num_types = V_;
+    cfg.num_docs = d1 - d0;
+    cfg.alpha = alpha_.data();
+    cfg.beta = beta_;
+    cfg.seed = seed_;
+    cfg.device = g;
+    cfg.sampler = sampler_;
+    cfg.token_base = doc_off_[d0];
+    cfg.tokens_per_range = 0;
+    lda_ctx* c = nullptr;
+    const int32_t* w = words_.empty() ? nullptr : words_.data() + doc_off_[d0];
+    check(lda_create(&c, &cfg, doc_off_.data() + d0, w, nullptr), "lda_create");
+    sg->ctx.push_back(c);
+  }
+  // documents already in the model keep their topics
+  if (!keep.empty()) {
+    for (int g = 0; g < G; ++g) {
+      const int64_t t0 = doc_off_[sg->doc_begin[g]], t1 = doc_off_[sg->doc_begin[g + 1]];
+      if (t0 >= (int64_t)keep.size() || t1 == t0) continue;
+      std::vector<int32_t> z((size_t)(t1 - t0));
+      check(lda_get_z(sg->ctx[g], z.data()), "lda_get_z");
+      const int64_t m = std::min<int64_t>(t1, (int64_t)keep.size());
+      std::copy(keep.begin() + t0, keep.begin() + m, z.begin());
+      check(lda_set_z(sg->ctx[g], z.data()), "lda_set_z");
+    }
+  }
+  if (G > 1) {
+    std::vector<int> devs(G);
+    std::iota(devs.begin(), devs.end(), 0);
+    sg->comms.resize(G);
+    const ncclResult_t r = ncclCommInitAll(sg->comms.data(), G, devs.data());
+    if (r != ncclSuccess) {
+      sg->comms.clear();
+      raise(LDA_ERR_DEVICE, std::string("ncclCommInitAll: ") + ncclGetErrorString(r));
+    }
+  }
+  // the shards' local counts are the pending delta: sum them, apply
+  sg->reduce();
+  sg->apply();
+  shards_ = std::move(sg);
+  shards_dirty_ = false;
+  z_dirty_ = true;
+  max_doc_len_ = 0;
+  for (int64_t d = 0; d < D; ++d)
+    max_doc_len_ = std::max<int32_t>(max_doc_len_, (int32_t)(doc_off_[d + 1] - doc_off_[d]));
+  doc_len_counts_.assign((size_t)max_doc_len_ + 1, 0);
+  topic_doc_counts_.assign((size_t)K_ * (max_doc_len_ + 1), 0);
+}
+
+std::vector<int32_t> ParallelTopicModel::topics() {
+  ensureShards();  // documents added since the last sweep get their initial topics
+  if (z_dirty_) {
+    z_cache_.assign((size_t)numTokens(), 0);
+    for (size_t g = 0; g < shards_->ctx.size(); ++g) {
+      const int64_t t0 = doc_off_[shards_->doc_begin[g]];
+      check(lda_get_z(shards_->ctx[g], z_cache_.data() + t0), "lda_get_z");
+    }
+    z_dirty_ = false;
+  }
+  return z_cache_;
+}
+
+void ParallelTopicModel::counts(int32_t* nw, int32_t* nwsum) {
+  ensureShards();
+  check(lda_get_counts(shards_->ctx[0], nw, nwsum, nullptr, nullptr), "lda_get_counts");
+}
+
+double ParallelTopicModel::modelLogLikelihood() {
+  ensureShards();
+  double doc_total = 0.0, word_part = 0.0;
+  for (size_t g = 0; g < shards_->ctx.size(); ++g) {
+    double dp = 0.0, wp = 0.0;
+    check(lda_log_likelihood_parts(shards_->ctx[g], &dp, &wp), "lda_log_likelihood_parts");
+    doc_total += dp;
+    if (g == 0) word_part = wp;
+  }
+  return doc_total + word_part;
+}
+
+void ParallelTopicModel::optimizeAlpha() {
+  const int64_t W = (int64_t)max_doc_len_ + 1;
+  if (symmetric_alpha_) {
+    // every topic's histogram pooled into one (Mallet keeps it in topic 0's row)
+    std::vector<int32_t> pooled((size_t)W, 0);
+    for (int k = 0; k < K_; ++k)
+      for (int64_t i = 0; i < W; ++i) pooled[(size_t)i] += topic_doc_counts_[(size_t)(k * W + i)];
+    std::vector<int64_t> lens;
+    std::vector<int32_t> cnt;
+    for (int64_t n = 0; n < W; ++n)
+      if (doc_len_counts_[(size_t)n] > 0) {
+        lens.push_back(n);
+        cnt.push_back(doc_len_counts_[(size_t)n]);
+      }
+    double a = 0.0;
+    check(lda_learn_symmetric_concentration(pooled.data(), W - 1, lens.data(), cnt.data(),
+                                            (int64_t)lens.size(), K_, alpha_sum_, &a),
+          "lda_learn_symmetric_concentration");
+    alpha_sum_ = a;
+    std::fill(alpha_.begin(), alpha_.end(), alpha_sum_ / K_);
+  } else {
+    double s = 0.0;
+    check(lda_learn_parameters(alpha_.data(), K_, topic_doc_counts_.data(), doc_len_counts_.data(),
+                               max_doc_len_, 1.001, 1.0, 1, &s),
+          "lda_learn_parameters");
+    alpha_sum_ = s;
+  }
+  std::fill(doc_len_counts_.begin(), doc_len_counts_.end(), 0);
+  std::fill(topic_doc_counts_.begin(), topic_doc_counts_.end(), 0);
+}
+
+void ParallelTopicModel::optimizeBeta() {
+  // countHistogram: nw cells by count, up to the largest word total
+  std::vector<int32_t> totals((size_t)V_, 0);
+  for (int32_t w : words_) totals[(size_t)w]++;
+  const int64_t max_count = totals.empty() ? 0 : *std::max_element(totals.begin(), totals.end());
+  std::vector<int32_t> hist((size_t)max_count + 1, 0);
+  check(lda_count_histogram(shards_->ctx[0], max_count, hist.data()), "lda_count_histogram");
+  // topicSizeHistogram, sparse: (tokens in topic, number of topics)
+  std::vector<int32_t> nwsum((size_t)K_);
+  check(lda_get_counts(shards_->ctx[0], nullptr, nwsum.data(), nullptr, nullptr), "lda_get_counts");
+  std::vector<int64_t> sizes(nwsum.begin(), nwsum.end());
+  std::sort(sizes.begin(), sizes.end());
+  std::vector<int64_t> lens;
+  std::vector<int32_t> cnt;
+  for (int64_t s : sizes) {
+    if (!lens.empty() && lens.back() == s) {
+      cnt.back()++;
+    } else {
+      lens.push_back(s);
+      cnt.push_back(1);
+    }
+  }
+  double beta_sum = beta_ * V_;
+  check(lda_learn_symmetric_concentration(hist.data(), max_count, lens.data(), cnt.data(),
+                                          (int64_t)lens.size(), V_, beta_sum, &beta_sum),
+        "lda_learn_symmetric_concentration");
+  beta_ = beta_sum / V_;
+}
+
+void ParallelTopicModel::estimate() {
+  ensureShards();
+  ll_trace_.clear();
+  const double total_tokens = (double)numTokens();
+  for (int32_t it = 1; it <= num_iterations_; ++it) {
+    if (show_topics_interval_ != 0 && it % show_topics_interval_ == 0)
+      log("\n" + displayTopWords(words_per_topic_, false));
+    shards_->sample();
+    shards_->reduce();
+    shards_->apply();
+    z_dirty_ = true;
+    const bool opt = it > burnin_period_ && optimize_interval_ != 0;
+    if (opt && it % save_sample_interval_ == 0)
+      for (auto c : shards_->ctx)
+        check(lda_doc_topic_histograms(c, max_doc_len_, doc_len_counts_.data(),
+                                       topic_doc_counts_.data()),
+              "lda_doc_topic_histograms");
+    if (opt && it % optimize_interval_ == 0) {
+      optimizeAlpha();
+      optimizeBeta();
+      for (auto c : shards_->ctx) check(lda_set_alpha_beta(c, alpha_.data(), beta_), "lda_set_alpha_beta");
+    }
+    if (it % 10 == 0) {
+      if (print_log_likelihood_) {
+        const double ll = modelLogLikelihood() / total_tokens;
+        ll_trace_.emplace_back(it, ll);
+        log("<" + std::to_string(it) + "> LL/token: " + java_number5(ll));
+      } else {
+        log("<" + std::to_string(it) + ">");
+      }
+    }
+  }
+}
+
+std::vector<double> ParallelTopicModel::getTopicProbabilities(int64_t doc) {
+  if (doc < 0 || doc >= numDocs()) raise(LDA_ERR_INVALID_ARG, "document index out of range");
+  ensureShards();
+  const std::vector<int32_t> z = topics();
+  std::vector<double> dist((size_t)K_, 0.0);
+  for (int64_t i = doc_off_[doc]; i < doc_off_[doc + 1]; ++i) dist[(size_t)z[(size_t)i]] += 1.0;
+  double sum = 0.0;
+  for (int k = 0; k < K_; ++k) {
+    dist[(size_t)k] += alpha_[(size_t)k];
+    sum += dist[(size_t)k];
+  }
+  for (int k = 0; k < K_; ++k) dist[(size_t)k] /= sum;
+  return dist;
+}
+
+// IDSorter order: weight descending; equal weights by ascending id (Mallet's
+// stable sort of an array already in id order; parity unpinned)
+static void sort_ids(std::vector<std::pair<int32_t, double>>& v) {
+  std::stable_sort(v.begin(), v.end(), [](const auto& a, const auto& b) { return a.second > b.second; });
+}
+
+std::string ParallelTopicModel::documentTopics(double threshold, int32_t max) {
+  ensureShards();
+  const std::vector<int32_t> z = topics();
+  if (max < 0 || max > K_) max = K_;
+  std::string out = "#doc source topic proportion ...\n";
+  std::vector<int32_t> cnt((size_t)K_);
+  std::vector<std::pair<int32_t, double>> sorted((size_t)K_);
+  for (int64_t d = 0; d < numDocs(); ++d) {
+    out += std::to_string(d);
+    out += ' ';
+    out += has_source_[(size_t)d] ? sources_[(size_t)d] : std::string("null-source");
+    out += ' ';
+    std::fill(cnt.begin(), cnt.end(), 0);
+    const int64_t len = doc_off_[d + 1] - doc_off_[d];
+    for (int64_t i = doc_off_[d]; i < doc_off_[d + 1]; ++i) cnt[(size_t)z[(size_t)i]]++;
+    for (int k = 0; k < K_; ++k)
+      sorted[(size_t)k] = {k, (alpha_[(size_t)k] + cnt[(size_t)k]) / ((double)len + alpha_sum_)};
+    sort_ids(sorted);
+    for (int i = 0; i < max; ++i) {
+      if (sorted[(size_t)i].second < threshold) break;
+      out += std::to_string(sorted[(size_t)i].first) + " " + java_double(sorted[(size_t)i].second) + " ";
+    }
+    out += " \n";
+  }
+  return out;
+}
+
+std::string ParallelTopicModel::displayTopWords(int32_t num_words, bool using_new_lines) {
+  ensureShards();
+  std::vector<int32_t> nw((size_t)V_ * K_);
+  check(lda_get_counts(shards_->ctx[0], nw.data(), nullptr, nullptr, nullptr), "lda_get_counts");
+  std::string out;
+  std::vector<std::pair<int32_t, double>> words;
+  for (int k = 0; k < K_; ++k) {
+    words.clear();
+    for (int32_t w = 0; w < V_; ++w) {
+      const int32_t c = nw[(size_t)w * K_ + k];
+      if (c > 0) words.emplace_back(w, (double)c);
+    }
+    sort_ids(words);
+    auto name = [&](int32_t w) { return alphabet_.empty() ? std::to_string(w) : alphabet_[(size_t)w]; };
+    // Mallet's loop starts its word counter at 1 and stops before numWords
+    const size_t n = (size_t)std::max(0, std::min<int32_t>(num_words - 1, (int32_t)words.size()));
+    if (using_new_lines) {
+      out += std::to_string(k) + "\t" + java_number5(alpha_[(size_t)k]) + "\n";
+      for (size_t i = 0; i < n; ++i)
+        out += name(words[i].first) + "\t" + java_number5(words[i].second) + "\n";
+    } else {
+      out += std::to_string(k) + "\t" + java_number5(alpha_[(size_t)k]) + "\t";
+      for (size_t i = 0; i < n; ++i) out += name(words[i].first) + " ";
+      out += "\n";
+    }
+  }
+  return out;
+}
+
+void ParallelTopicModel::infer(int64_t Dh, const int64_t* doc_off, const int32_t* words,
+                               int32_t num_iterations, int32_t thinning, int32_t burn_in,
+                               uint64_t seed, double* theta) {
+  ensureShards();
+  if (Dh < 0 || (Dh > 0 && (!doc_off || !theta))) raise(LDA_ERR_INVALID_ARG, "bad documents");
+  // tokens of types unknown to the model are dropped (Mallet's inferencer
+  // skips type indices beyond its typeTopicCounts)
+  std::vector<int64_t> off((size_t)Dh + 1, 0);
+  std::vector<int32_t> kept;
+  for (int64_t d = 0; d < Dh; ++d) {
+    for (int64_t i = doc_off[d] - doc_off[0]; i < doc_off[d + 1] - doc_off[0]; ++i)
+      if (words[i] >= 0 && words[i] < V_) kept.push_back(words[i]);
+    off[(size_t)d + 1] = (int64_t)kept.size();
+  }
+  check(lda_infer(shards_->ctx[0], Dh, off.data(), kept.empty() ? nullptr : kept.data(),
+                  num_iterations, burn_in, thinning, seed, theta),
+        "lda_infer");
+}
+
+}  // namespace lda_host
+
+// ------------------------------------------------------------------ C ABI
+struct ldatm {
+  lda_host::ParallelTopicModel model;
+  ldatm(int32_t K, double a, double b) : model(K, a, b) {}
+};
+
+namespace {
+thread_local std::string g_tm_error;
+
+template <typename F>
+lda_status guard(F&& f) {
+  try {
+    f();
+    return LDA_OK;
+  } catch (const lda_host::Error& e) {
+    g_tm_error = e.message;
+    return e.status;
+  } catch (const std::bad_alloc&) {
+    g_tm_error = "host allocation failed";
+    return LDA_ERR_OUT_OF_MEMORY;
+  } catch (const std::exception& e) {
+    g_tm_error = e.what();
+    return LDA_ERR_INVALID_ARG;
+  }
+}
+
+lda_status copy_text(const std::string& s, char* buf, size_t cap, size_t* len) {
+  if (len) *len = s.size();
+  if (buf) {
+    if (cap < s.size() + 1) {
+      g_tm_error = "buffer too small";
+      return LDA_ERR_INVALID_ARG;
+    }
+    std::memcpy(buf, s.c_str(), s.size() + 1);
+  }
+  return LDA_OK;
+}
+
+lda_status write_file(const char* path, const std::string& s) {
+  if (!path) {
+    g_tm_error = "null path";
+    return LDA_ERR_INVALID_ARG;
+  }
+  std::ofstream f(path, std::ios::binary);
+  if (!f) {
+    g_tm_error = std::string("cannot open ") + path;
+    return LDA_ERR_INVALID_ARG;
+  }
+  f << s;
+  return f.good() ? LDA_OK : LDA_ERR_INVALID_ARG;
+}
+
+#define TM_CHECK(m)                 \
+  if (!(m)) {                       \
+    g_tm_error = "null model";      \
+    return LDA_ERR_INVALID_ARG;     \
+  }
+}  // namespace
+
+extern "C" {
+
+const char* ldatm_last_error(void) { return g_tm_error.c_str(); }
+
+lda_status ldatm_format_double(double x, int32_t style, char* buf, size_t cap) {
+  if (style != 0 && style != 1) {
+    g_tm_error = "style must be 0 or 1";
+    return LDA_ERR_INVALID_ARG;
+  }
+  return copy_text(style == 0 ? lda_host::java_double(x) : lda_host::java_number5(x), buf, cap, nullptr);
+}
+
+lda_status ldatm_create(ldatm** out, int32_t num_topics, double alpha_sum, double beta) {
+  if (!out) return LDA_ERR_INVALID_ARG;
+  *out = nullptr;
+  return guard([&] { *out = new ldatm(num_topics, alpha_sum, beta); });
+}
+
+void ldatm_destroy(ldatm* m) { delete m; }
+
+lda_status ldatm_set_alphabet(ldatm* m, int32_t num_types, const char* const* words) {
+  TM_CHECK(m);
+  return guard([&] {
+    std::vector<std::string> w;
+    if (words)
+      for (int32_t i = 0; i < num_types; ++i) w.emplace_back(words[i] ? words[i] : "");
+    m->model.setAlphabet(std::move(w), num_types);
+  });
+}
+
+lda_status ldatm_add_instances(ldatm* m, int64_t D, const int64_t* doc_off, const int32_t* words,
+                               const char* const* sources) {
+  TM_CHECK(m);
+  return guard([&] { m->model.addInstances(D, doc_off, words, sources); });
+}
+
+#define TM_SETTER(name, call)                          \
+  lda_status name(ldatm* m, int32_t n) {               \
+    TM_CHECK(m);                                       \
+    return guard([&] { m->model.call; });              \
+  }
+TM_SETTER(ldatm_set_num_iterations, setNumIterations(n))
+TM_SETTER(ldatm_set_optimize_interval, setOptimizeInterval(n))
+TM_SETTER(ldatm_set_burnin_period, setBurninPeriod(n))
+TM_SETTER(ldatm_set_symmetric_alpha, setSymmetricAlpha(n != 0))
+TM_SETTER(ldatm_set_num_threads, setNumThreads(n))
+TM_SETTER(ldatm_set_sampler, setSampler(n))
+TM_SETTER(ldatm_set_verbosity, setVerbosity(n))
+TM_SETTER(ldatm_set_print_log_likelihood, setPrintLogLikelihood(n != 0))
+
+lda_status ldatm_set_save_sample_interval(ldatm* m, int32_t n) {
+  TM_CHECK(m);
+  if (n < 1) {
+    g_tm_error = "saveSampleInterval must be >= 1";
+    return LDA_ERR_INVALID_ARG;
+  }
+  return guard([&] { m->model.setSaveSampleInterval(n); });
+}
+
+lda_status ldatm_set_topic_display(ldatm* m, int32_t interval, int32_t n) {
+  TM_CHECK(m);
+  return guard([&] { m->model.setTopicDisplay(interval, n); });
+}
+
+lda_status ldatm_set_random_seed(ldatm* m, int64_t seed) {
+  TM_CHECK(m);
+  return guard([&] { m->model.setRandomSeed(seed); });
+}
+
+lda_status ldatm_estimate(ldatm* m) {
+  TM_CHECK(m);
+  return guard([&] { m->model.estimate(); });
+}
+
+lda_status ldatm_get_ll_trace(ldatm* m, int32_t* iterations, double* ll, int32_t cap, int32_t* n) {
+  TM_CHECK(m);
+  const auto& t = m->model.llTrace();
+  if (n) *n = (int32_t)t.size();
+  for (int32_t i = 0; i < cap && i < (int32_t)t.size(); ++i) {
+    if (iterations) iterations[i] = t[(size_t)i].first;
+    if (ll) ll[i] = t[(size_t)i].second;
+  }
+  return LDA_OK;
+}
+
+lda_status ldatm_model_log_likelihood(ldatm* m, double* out) {
+  TM_CHECK(m);
+  return guard([&] { *out = m->model.modelLogLikelihood(); });
+}
+
+lda_status ldatm_get_shape(ldatm* m, int32_t* K, int32_t* V, int64_t* D, int64_t* N) {
+  TM_CHECK(m);
+  if (K) *K = m->model.numTopics();
+  if (V) *V = m->model.numTypes();
+  if (D) *D = m->model.numDocs();
+  if (N) *N = m->model.numTokens();
+  return LDA_OK;
+}
+
+lda_status ldatm_get_hyper(ldatm* m, double* alpha, double* alpha_sum, double* beta) {
+  TM_CHECK(m);
+  if (alpha) std::copy(m->model.alpha().begin(), m->model.alpha().end(), alpha);
+  if (alpha_sum) *alpha_sum = m->model.alphaSum();
+  if (beta) *beta = m->model.beta();
+  return LDA_OK;
+}
+
+lda_status ldatm_get_z(ldatm* m, int32_t* z) {
+  TM_CHECK(m);
+  return guard([&] {
+    const std::vector<int32_t> t = m->model.topics();
+    if ((int64_t)t.size() != m->model.numTokens()) throw lda_host::Error{LDA_ERR_STATE, "no topic assignments yet"};
+    std::copy(t.begin(), t.end(), z);
+  });
+}
+
+lda_status ldatm_get_counts(ldatm* m, int32_t* nw, int32_t* nwsum) {
+  TM_CHECK(m);
+  return guard([&] { m->model.counts(nw, nwsum); });
+}
+
+lda_status ldatm_get_topic_probabilities(ldatm* m, int64_t doc, double* out) {
+  TM_CHECK(m);
+  return guard([&] {
+    const std::vector<double> p = m->model.getTopicProbabilities(doc);
+    std::copy(p.begin(), p.end(), out);
+  });
+}
+
+lda_status ldatm_document_topics_text(ldatm* m, double threshold, int32_t max, char* buf, size_t cap,
+                                      size_t* len) {
+  TM_CHECK(m);
+  std::string s;
+  lda_status st = guard([&] { s = m->model.documentTopics(threshold, max); });
+  return st ? st : copy_text(s, buf, cap, len);
+}
+
+lda_status ldatm_print_document_topics(ldatm* m, const char* path, double threshold, int32_t max) {
+  TM_CHECK(m);
+  std::string s;
+  lda_status st = guard([&] { s = m->model.documentTopics(threshold, max); });
+  return st ? st : write_file(path, s);
+}
+
+lda_status ldatm_top_words_text(ldatm* m, int32_t num_words, int32_t using_new_lines, char* buf,
+                                size_t cap, size_t* len) {
+  TM_CHECK(m);
+  std::string s;
+  lda_status st = guard([&] { s = m->model.displayTopWords(num_words, using_new_lines != 0); });
+  return st ? st : copy_text(s, buf, cap, len);
+}
+
+lda_status ldatm_print_top_words(ldatm* m, const char* path, int32_t num_words, int32_t using_new_lines) {
+  TM_CHECK(m);
+  std::string s;
+  lda_status st = guard([&] { s = m->model.displayTopWords(num_words, using_new_lines != 0); });
+  return st ? st : write_file(path, s);
+}
+
+lda_status ldatm_infer(ldatm* m, int64_t Dh, const int64_t* doc_off, const int32_t* words,
+                       int32_t num_iterations, int32_t thinning, int32_t burn_in, uint64_t seed,
+                       double* theta) {
+  TM_CHECK(m);
+  return guard([&] { m->model.infer(Dh, doc_off, words, num_iterations, thinning, burn_in, seed, theta); });
+}
+
+}  // extern "C"

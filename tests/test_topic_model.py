@@ -1,0 +1,98 @@
+"""CPU checks of the ParallelTopicModel host mirror (liblda_topic_model.so):
+header <-> binding <-> exports, Mallet's number renderings, the reference's
+ingest pipe, and loud errors without a GPU.  Sampling itself is covered by
+tests/test_topic_model_gpu.py."""
+import ctypes as C
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+from ldagibbssampling_amd import capi, topic_model as tm
+
+HEADER = os.path.join(os.path.dirname(capi.HEADER_PATH), "lda_topic_model.h")
+
+
+def declared():
+    text = re.sub(r"/\*.*?\*/", "", open(HEADER).read(), flags=re.S)
+    return sorted(set(re.findall(r"\b(ldatm_[a-z_0-9]+)\s*\(", text)))
+
+
+@pytest.fixture(scope="module")
+def L():
+    return tm.load_tm()
+
+
+def test_header_binding_exports_agree(L):
+    assert declared() == sorted(tm.TM_SIGNATURES)
+    out = subprocess.run(["nm", "-D", "--defined-only", tm.TM_LIB_PATH], capture_output=True,
+                         text=True, check=True).stdout
+    exported = set(re.findall(r"\bT (ldatm_\w+)", out))
+    assert set(declared()) <= exported
+    # the mirror sits above the sampler ABI: it links liblda_mi355x.so and RCCL
+    dyn = subprocess.run(["readelf", "-d", tm.TM_LIB_PATH], capture_output=True, text=True).stdout
+    assert "liblda_mi355x.so" in dyn and "librccl.so" in dyn
+
+
+@pytest.mark.parametrize("x,java", [
+    (1.0, "1.0"), (100.0, "100.0"), (0.001, "0.001"), (1e-4, "1.0E-4"), (1e7, "1.0E7"),
+    (9999999.0, "9999999.0"), (123456789.0, "1.23456789E8"), (0.1 + 0.2, "0.30000000000000004"),
+    (0.6308917995984609, "0.6308917995984609"), (0.0010402955565968202, "0.0010402955565968202"),
+    (-2.5e-5, "-2.5E-5"), (0.0, "0.0"), (-0.0, "-0.0"), (1.5e300, "1.5E300"),
+    (float("nan"), "NaN"), (float("inf"), "Infinity"),
+])
+def test_java_double_to_string(L, x, java):
+    assert tm.format_double(x, 0) == java
+
+
+@pytest.mark.parametrize("x,fmt", [
+    (0.00868, "0.00868"), (2.0, "2"), (0.123456, "0.12346"), (1234.56789, "1,234.56789"),
+    (1234567.0, "1,234,567"), (-7.123456789, "-7.12346"), (0.1, "0.1"), (5e-324, "0"),
+    (0.000015, "0.00002"), (0.000025, "0.00003"),   # HALF_EVEN on the exact binary value
+    (0.125, "0.125"), (2.5e-6, "0"),
+])
+def test_mallet_number_format(L, x, fmt):
+    assert tm.format_double(x, 1) == fmt
+
+
+def test_format_errors_are_loud(L):
+    with pytest.raises(capi.LdaError):
+        tm.format_double(1.0, 7)
+
+
+def test_instance_list_from_inverse_docs():
+    text = "t1\tFoo/Bar.java\tbaz.java\n t2\tfoo/bar.java\n\tBAZ.java\tnew.java\n"
+    il = tm.InstanceList.fromInverseDocs(text)
+    a = il.getDataAlphabet()
+    assert a.toArray() == ["foo/bar.java", "baz.java", "new.java"]
+    assert [list(i.data) for i in il] == [[0, 1], [0], [1, 2]]
+    assert [i.target for i in il] == ["t1", " t2", ""]
+    # a second list over the same (growing) alphabet, as updateModel does
+    il2 = tm.InstanceList.fromInverseDocs("t9\tnew.java\tzzz.java\n", alphabet=a)
+    assert a.size() == 4 and list(il2[0].data) == [2, 3]
+    # inference-style: no growth, unknown tokens dropped
+    il3 = tm.InstanceList.fromInverseDocs("t9\tqqq.java\tbaz.java\n", alphabet=a, grow=False)
+    assert a.size() == 4 and list(il3[0].data) == [1]
+
+
+def test_model_options_without_gpu(L):
+    """Creating a model and setting options is host-only; the first use of
+    the GPU (estimate) fails loudly when there is none."""
+    m = tm.ParallelTopicModel(20, 10.0, 0.01)
+    m.setOptimizeInterval(20)
+    m.setNumThreads(4)
+    m.setNumIterations(5)
+    m.setTopicDisplay(0, 0)
+    assert m.alphaSum == 10.0 and m.beta == 0.01 and np.allclose(m.alpha, 0.5)
+    with pytest.raises(capi.LdaError):
+        m.setNumThreads(0)
+    with pytest.raises(capi.LdaError):
+        tm.ParallelTopicModel(5000, 1.0, 0.01)
+    il = tm.InstanceList.fromInverseDocs("a\tx\ty\nb\ty\tz\n")
+    m.addInstances(il)
+    import torch
+    if not torch.cuda.is_available():
+        with pytest.raises(capi.LdaError):
+            m.estimate()
