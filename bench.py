@@ -60,6 +60,26 @@ def pmc_traffic(K: int, tokens_per_launch: int, kernel_prefix: str):
     return None, None
 
 
+def stream_copy_gbs(device: int, nbytes: int = 2 << 30, reps: int = 10) -> float:
+    """Measured device-to-device copy rate (read + write bytes / s) on this
+    box: SURVEY.md §8d's "measured stream-copy peak" beside the 8 TB/s spec."""
+    import torch
+    x = torch.empty(nbytes // 4, dtype=torch.int32, device=f"cuda:{device}")
+    y = torch.empty_like(x)
+    y.copy_(x)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        y.copy_(x)
+    e1.record()
+    torch.cuda.synchronize()
+    gbs = 2 * nbytes * reps / (e0.elapsed_time(e1) * 1e-3) / 1e9
+    del x, y
+    torch.cuda.empty_cache()
+    return gbs
+
+
 def cpu_baseline(corpus, K, alpha_sum, beta, budget_s=15.0, threads=4):
     """cpu_mallet (oracle/, the Mallet 2.0.7 SparseLDA restatement) timed on a
     bounded sample of the same workload on this host's cores."""
@@ -158,14 +178,13 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
-    # per-launch kernel duration of the sampler (HIP events on its stream):
-    # a separate, identical pass so that the timed loop carries no host syncs.
-    ks = []
-    for _ in range(3):
-        step()
-        ks.append(sampler.last_sample_ms())
-    torch.cuda.synchronize()
+    # per-launch duration of the sampler kernel over the timed region: HIP
+    # events recorded around every launch on the sampler's stream, read back
+    # after the closing synchronize (no host sync inside the timed loop)
+    ks = sampler.sample_times(args.steps)
+    assert len(ks) == min(args.steps, 256)
     kern_ms = float(np.mean(ks))
+    copy_gbs = stream_copy_gbs(local_rank) if rank == 0 else None
 
     t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local_rank}")
     if world > 1:
@@ -211,6 +230,8 @@ def main():
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBS,
+                "measured_copy_gbs": copy_gbs,
+                "kernel_ms_timed_region": kern_ms,
                 "traffic": traffic_gb,
                 "traffic_unit": "GB per launch (rocprofv3 PMC, gfx950-corrected)",
                 "traffic_source": traffic_src,

@@ -195,6 +195,9 @@ double lda_digamma(double z);
 /* Kernel-level timing of the last lda_sample (ms, HIP events on the
  * context's stream). */
 lda_status lda_last_sample_ms(lda_ctx* ctx, float* ms);
+/* Kernel durations (ms, oldest first) of the last n = min(max, launches, 256)
+ * lda_sample calls: bench.py reads the launches of its timed region. */
+lda_status lda_sample_times(lda_ctx* ctx, int32_t max, float* ms, int32_t* n);
 
 const char* lda_last_error(void);
 const char* lda_version(void);

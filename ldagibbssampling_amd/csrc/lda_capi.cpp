@@ -129,8 +129,10 @@ struct lda_ctx {
   double* partial = nullptr;
   unsigned long long* nonzero = nullptr;
   int partial_blocks = 1024;
-  hipEvent_t ev0 = nullptr, ev1 = nullptr;
-  bool timed = false;
+  // event pairs around the last LDA_TIME_RING sampler launches (lda_sample_times)
+  static constexpr int LDA_TIME_RING = 256;
+  hipEvent_t ev0[LDA_TIME_RING] = {}, ev1[LDA_TIME_RING] = {};
+  int64_t launches = 0;
 
   ~lda_ctx() {
     if (device >= 0) (void)hipSetDevice(device);
@@ -139,8 +141,10 @@ struct lda_ctx {
                     (void*)inv, (void*)inv_m1, (void*)partial, (void*)nonzero, (void*)ent,
                     (void*)row_off, (void*)row_nnz, (void*)nw16, (void*)wide})
       if (p) (void)hipFree(p);
-    if (ev0) (void)hipEventDestroy(ev0);
-    if (ev1) (void)hipEventDestroy(ev1);
+    for (int i = 0; i < LDA_TIME_RING; ++i) {
+      if (ev0[i]) (void)hipEventDestroy(ev0[i]);
+      if (ev1[i]) (void)hipEventDestroy(ev1[i]);
+    }
     if (own_stream) (void)hipStreamDestroy(own_stream);
   }
 
@@ -338,8 +342,10 @@ lda_status lda_create(lda_ctx** out, const lda_config* cfg, const int64_t* doc_o
   CT(dalloc(&c->inv_m1, c->Kp));
   CT(dalloc(&c->partial, c->partial_blocks));
   CT(dalloc(&c->nonzero, c->partial_blocks));
-  CT(hipEventCreate(&c->ev0));
-  CT(hipEventCreate(&c->ev1));
+  for (int i = 0; i < lda_ctx::LDA_TIME_RING; ++i) {
+    CT(hipEventCreate(&c->ev0[i]));
+    CT(hipEventCreate(&c->ev1[i]));
+  }
 
   if (N > 0) CT(hipMemcpyAsync(c->words, words, sizeof(int32_t) * N, hipMemcpyHostToDevice, c->stream));
   CT(hipMemcpyAsync(c->doc_off, off.data(), sizeof(int64_t) * (D + 1), hipMemcpyHostToDevice, c->stream));
@@ -419,13 +425,14 @@ lda_status lda_sample(lda_ctx* c) {
     HIP_TRY(hipMemsetAsync(c->queue, 0, sizeof(int32_t), c->stream));
     const lda::SampleParams p = c->params(false);
     const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>(c->sample_blocks, (c->R + 3) / 4));
-    HIP_TRY(hipEventRecord(c->ev0, c->stream));
+    const int slot = (int)(c->launches % lda_ctx::LDA_TIME_RING);
+    HIP_TRY(hipEventRecord(c->ev0[slot], c->stream));
     if (c->sampler == LDA_SAMPLER_SPARSE)
       HIP_TRY(lda::launch_sample_sparse(c->C, false, p, blocks, c->stream));
     else
       HIP_TRY(lda::launch_sample(c->C, false, p, blocks, c->stream));
-    HIP_TRY(hipEventRecord(c->ev1, c->stream));
-    c->timed = true;
+    HIP_TRY(hipEventRecord(c->ev1[slot], c->stream));
+    c->launches++;
   }
   c->sweep++;
   c->pending = true;
@@ -458,9 +465,23 @@ lda_status lda_debug_sample_trace(lda_ctx* c, float* host_trace) {
 lda_status lda_last_sample_ms(lda_ctx* c, float* ms) {
   if (!c || !ms) return fail(LDA_ERR_INVALID_ARG, "null argument");
   *ms = 0.0f;
-  if (!c->timed) return LDA_OK;
-  HIP_TRY(hipEventSynchronize(c->ev1));
-  HIP_TRY(hipEventElapsedTime(ms, c->ev0, c->ev1));
+  if (c->launches == 0) return LDA_OK;
+  const int slot = (int)((c->launches - 1) % lda_ctx::LDA_TIME_RING);
+  HIP_TRY(hipEventSynchronize(c->ev1[slot]));
+  HIP_TRY(hipEventElapsedTime(ms, c->ev0[slot], c->ev1[slot]));
+  return LDA_OK;
+}
+
+lda_status lda_sample_times(lda_ctx* c, int32_t max, float* ms, int32_t* n) {
+  if (!c || !n || max < 0 || (max > 0 && !ms)) return fail(LDA_ERR_INVALID_ARG, "bad argument");
+  const int64_t avail = std::min<int64_t>(c->launches, lda_ctx::LDA_TIME_RING);
+  const int32_t k = (int32_t)std::min<int64_t>(avail, max);
+  *n = k;
+  for (int32_t i = 0; i < k; ++i) {
+    const int slot = (int)((c->launches - k + i) % lda_ctx::LDA_TIME_RING);
+    HIP_TRY(hipEventSynchronize(c->ev1[slot]));
+    HIP_TRY(hipEventElapsedTime(&ms[i], c->ev0[slot], c->ev1[slot]));
+  }
   return LDA_OK;
 }
 

@@ -132,6 +132,14 @@ class GibbsSampler:
         capi.check(self._L.lda_last_sample_ms(self._h, C.byref(ms)), "lda_last_sample_ms")
         return float(ms.value)
 
+    def sample_times(self, last: int) -> np.ndarray:
+        """Kernel durations (ms) of the last `last` lda_sample launches."""
+        ms = np.zeros(max(int(last), 0), dtype=np.float32)
+        n = C.c_int32()
+        capi.check(self._L.lda_sample_times(self._h, len(ms), ms.ctypes.data if len(ms) else None,
+                                            C.byref(n)), "lda_sample_times")
+        return ms[:n.value]
+
     # ---------------------------------------------------------------- state
     def z(self) -> np.ndarray:
         out = np.empty(self.N, dtype=np.int32)

@@ -1,0 +1,50 @@
+#!/usr/bin/env python3
+"""Write profiles/rNN/traffic_k{K}.json (what bench.py reports as
+roofline.traffic) from the rocprofv3 summaries of one profile run.
+
+  make_traffic.py <summary_dir> <kernel> <tokens_per_launch> <workload> <out.json>
+
+summary_dir holds summary_kt.json (--kernel-trace --stats), summary_fetch.json
+(--pmc FETCH_SIZE) and summary_write.json (--pmc WRITE_SIZE), each its own
+rocprofv3 pass over the same bench command (tools/profile.sh).  Bytes follow
+MI355X_MICROARCH.md §HBM for gfx950: FETCH_SIZE/WRITE_SIZE are KiB and
+FETCH_SIZE counts half of a 16 B/lane coalesced read stream (the sampler's row
+gathers), so hbm = (2*FETCH_SIZE + WRITE_SIZE) * 1024.
+"""
+import json
+import os
+import sys
+
+
+def main(d, kernel, tokens, workload, out):
+    kt = json.load(open(os.path.join(d, "summary_kt.json")))
+    fe = json.load(open(os.path.join(d, "summary_fetch.json")))["counters"][kernel]["FETCH_SIZE"]
+    wr = json.load(open(os.path.join(d, "summary_write.json")))["counters"][kernel]["WRITE_SIZE"]
+    t = {
+        "workload": workload,
+        "kernel": kernel,
+        "tokens_per_launch": int(tokens),
+        "avg_ns_kernel_trace": kt["kernels"][kernel]["avg_ns"],
+        "FETCH_SIZE_KiB": fe["avg_per_dispatch"],
+        "WRITE_SIZE_KiB": wr["avg_per_dispatch"],
+        "hbm_bytes_per_launch": (2 * fe["avg_per_dispatch"] + wr["avg_per_dispatch"]) * 1024,
+        "hbm_bytes_per_launch_uncorrected": (fe["avg_per_dispatch"] + wr["avg_per_dispatch"]) * 1024,
+        "correction": "MI355X_MICROARCH.md §HBM: FETCH_SIZE (KiB) reads 1/2 of a 16 B/lane "
+                      "coalesced stream on gfx950 -> bytes = (2*FETCH_SIZE + WRITE_SIZE)*1024; "
+                      "FETCH_SIZE also counts Infinity-Cache hits",
+        "source": f"tools/profile.sh passes summarised in {d}",
+    }
+    tcc = os.path.join(d, "summary_tcc.json")
+    if os.path.exists(tcc):
+        c = json.load(open(tcc))["counters"].get(kernel, {})
+        if "TCC_HIT_sum" in c and "TCC_MISS_sum" in c:
+            h, m = c["TCC_HIT_sum"]["avg_per_dispatch"], c["TCC_MISS_sum"]["avg_per_dispatch"]
+            t["l2_hit_rate"] = h / (h + m) if h + m else None
+    t["bytes_per_token"] = t["hbm_bytes_per_launch"] / t["tokens_per_launch"]
+    with open(out, "w") as f:
+        json.dump(t, f, indent=1)
+    print(json.dumps(t, indent=1))
+
+
+if __name__ == "__main__":
+    main(*sys.argv[1:6])

@@ -13,12 +13,19 @@ run() {  # name, rocprof args...
   python3 tools/summarize_prof.py $P/$name $P/summary_$name.json && cp $P/$name/*kernel_stats.csv $P/ 2>/dev/null; rm -rf $P/$name
   echo "$name ok"
 }
-run kt --kernel-trace --stats &&
-run fetch $SEL --pmc FETCH_SIZE &&
-run write $SEL --pmc WRITE_SIZE &&
-run sq $SEL --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU &&
-run lat $SEL --pmc SQ_INSTS_VMEM_RD SQ_INST_LEVEL_VMEM SQ_ACCUM_PREV_HIRES &&
-run tcc $SEL --pmc TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_DRAM_sum &&
-run ea $SEL --pmc TCC_EA0_RDREQ_LEVEL_sum TCC_EA0_RDREQ_DRAM_CREDIT_STALL_sum TCC_BUSY_avr &&
-run lds $SEL --pmc SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_VMEM_WR SQ_WAIT_INST_LDS
+PASSES=${PASSES:-"kt fetch write sq lat tcc ea lds"}
+ok=0
+for p in $PASSES; do
+  case $p in
+    kt) run kt --kernel-trace --stats ;;
+    fetch) run fetch $SEL --pmc FETCH_SIZE ;;
+    write) run write $SEL --pmc WRITE_SIZE ;;
+    sq) run sq $SEL --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU ;;
+    lat) run lat $SEL --pmc SQ_INSTS_VMEM_RD SQ_INST_LEVEL_VMEM SQ_ACCUM_PREV_HIRES ;;
+    tcc) run tcc $SEL --pmc TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_DRAM_sum ;;
+    ea) run ea $SEL --pmc TCC_EA0_RDREQ_LEVEL_sum TCC_EA0_RDREQ_DRAM_CREDIT_STALL_sum TCC_BUSY_avr ;;
+    lds) run lds $SEL --pmc SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_VMEM_WR SQ_WAIT_INST_LDS ;;
+  esac || { ok=1; break; }
+done
 ls $P
+exit $ok
