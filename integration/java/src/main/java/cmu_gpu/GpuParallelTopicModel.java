@@ -5,6 +5,7 @@ import java.util.logging.Logger;
 
 import cc.mallet.topics.ParallelTopicModel;
 import cc.mallet.topics.TopicAssignment;
+import cc.mallet.types.Dirichlet;
 import cc.mallet.types.FeatureSequence;
 import cc.mallet.types.LabelSequence;
 
@@ -44,6 +45,11 @@ public class GpuParallelTopicModel extends ParallelTopicModel {
   /** packed rows (count << topicBits | topic), row offsets [V+1] */
   private static native void nativeMalletPacked(long ctx, int[] rows, long[] rowOff);
   private static native void nativeGetTokensPerTopic(long ctx, int[] tokensPerTopic);
+  /** adds docLengthCounts[maxLen+1] and topicDocCounts[K*(maxLen+1)] (flattened) */
+  private static native void nativeDocTopicHistograms(long ctx, int maxLen, int[] docLen,
+                                                      int[] topicDocFlat);
+  /** adds countHistogram[maxCount+1] of the nw cells */
+  private static native void nativeCountHistogram(long ctx, long maxCount, int[] hist);
   private static native void nativeDestroy(long ctx);
 
   @Override
@@ -68,11 +74,46 @@ public class GpuParallelTopicModel extends ParallelTopicModel {
     }
     long seed = randomSeed == -1 ? System.nanoTime() : randomSeed;
     long ctx = nativeCreate(numTopics, numTypes, docOff, words, z, alpha, beta, seed, device);
+    int maxLen = 0;
+    for (int d = 0; d < D; d++) maxLen = Math.max(maxLen, (int) (docOff[d + 1] - docOff[d]));
+    int[] docLen = new int[maxLen + 1];
+    int[] topicDocFlat = new int[numTopics * (maxLen + 1)];
+    int maxTypeCount = 0;
+    for (int w = 0; w < numTypes; w++) maxTypeCount = Math.max(maxTypeCount, typeTotals[w]);
     try {
       for (int iteration = 1; iteration <= numIterations; iteration++) {
         nativeSweep(ctx, 1);
-        if (iteration > burninPeriod && optimizeInterval != 0 && iteration % optimizeInterval == 0) {
-          // host-side Minka updates of alpha/beta go here (DESIGN.md §8), then:
+        boolean opt = iteration > burninPeriod && optimizeInterval != 0;
+        if (opt && iteration % saveSampleInterval == 0) {
+          nativeDocTopicHistograms(ctx, maxLen, docLen, topicDocFlat);   // collectAlphaStatistics
+        }
+        if (opt && iteration % optimizeInterval == 0) {
+          // optimizeAlpha: Mallet's own estimator on the GPU's histograms
+          int[][] topicDoc = new int[numTopics][];
+          for (int k = 0; k < numTopics; k++) {
+            topicDoc[k] = java.util.Arrays.copyOfRange(topicDocFlat, k * (maxLen + 1), (k + 1) * (maxLen + 1));
+          }
+          if (usingSymmetricAlpha) {
+            int[] pooled = new int[maxLen + 1];
+            for (int k = 0; k < numTopics; k++)
+              for (int i = 0; i <= maxLen; i++) pooled[i] += topicDoc[k][i];
+            alphaSum = Dirichlet.learnSymmetricConcentration(pooled, docLen, numTopics, alphaSum);
+            java.util.Arrays.fill(alpha, alphaSum / numTopics);
+          } else {
+            alphaSum = Dirichlet.learnParameters(alpha, topicDoc, docLen, 1.001, 1.0, 1);
+          }
+          java.util.Arrays.fill(docLen, 0);
+          java.util.Arrays.fill(topicDocFlat, 0);
+          // optimizeBeta: countHistogram from the GPU, topic sizes from tokensPerTopic
+          int[] countHistogram = new int[maxTypeCount + 1];
+          nativeCountHistogram(ctx, maxTypeCount, countHistogram);
+          nativeGetTokensPerTopic(ctx, tokensPerTopic);
+          int maxTopicSize = 0;
+          for (int k = 0; k < numTopics; k++) maxTopicSize = Math.max(maxTopicSize, tokensPerTopic[k]);
+          int[] topicSizeHistogram = new int[maxTopicSize + 1];
+          for (int k = 0; k < numTopics; k++) topicSizeHistogram[tokensPerTopic[k]]++;
+          betaSum = Dirichlet.learnSymmetricConcentration(countHistogram, topicSizeHistogram, numTypes, betaSum);
+          beta = betaSum / numTypes;
           nativeSetAlphaBeta(ctx, alpha, beta);
         }
         if (iteration % 10 == 0) {

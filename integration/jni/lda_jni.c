@@ -94,6 +94,27 @@ JNIEXPORT void JNICALL Java_cmu_1gpu_GpuParallelTopicModel_nativeGetTokensPerTop
   check(env, s);
 }
 
+/* alpha statistics: docLengthCounts[maxLen+1] and topicDocCounts flattened
+ * [K*(maxLen+1)] are ADDED into (WorkerRunnable's collectAlphaStatistics) */
+JNIEXPORT void JNICALL Java_cmu_1gpu_GpuParallelTopicModel_nativeDocTopicHistograms(
+    JNIEnv* env, jclass cls, jlong ctx, jint maxLen, jintArray docLen, jintArray topicDoc) {
+  jint* dl = (*env)->GetIntArrayElements(env, docLen, NULL);
+  jint* td = (*env)->GetIntArrayElements(env, topicDoc, NULL);
+  lda_status s = lda_doc_topic_histograms((lda_ctx*)(intptr_t)ctx, maxLen, (int32_t*)dl, (int32_t*)td);
+  (*env)->ReleaseIntArrayElements(env, topicDoc, td, 0);
+  (*env)->ReleaseIntArrayElements(env, docLen, dl, 0);
+  check(env, s);
+}
+
+/* optimizeBeta's countHistogram[maxCount+1] (added into) */
+JNIEXPORT void JNICALL Java_cmu_1gpu_GpuParallelTopicModel_nativeCountHistogram(
+    JNIEnv* env, jclass cls, jlong ctx, jlong maxCount, jintArray hist) {
+  jint* h = (*env)->GetIntArrayElements(env, hist, NULL);
+  lda_status s = lda_count_histogram((lda_ctx*)(intptr_t)ctx, maxCount, (int32_t*)h);
+  (*env)->ReleaseIntArrayElements(env, hist, h, 0);
+  check(env, s);
+}
+
 JNIEXPORT void JNICALL Java_cmu_1gpu_GpuParallelTopicModel_nativeDestroy(JNIEnv* env, jclass cls,
                                                                           jlong ctx) {
   lda_destroy((lda_ctx*)(intptr_t)ctx);
