@@ -784,22 +784,34 @@ __global__ __launch_bounds__(256) void k_sample_sparse(SampleParams p) {
 }
 
 // ------------------------------------------- the large-K sparse sampler
-// K up to 4096 (C = 32, 64): the same draw as k_sample_sparse with the doc
-// part's lane partials in groups of 16 topics (TG registers; see
-// oracle/lda_oracle.c:lane_partial_grouped), so a changed topic re-sums 16
-// coefficients, not C.  LDS holds only a per-block float2 {alpha, inv} table
-// and per-wave 16-bit document counts (documents < 65536 tokens); every
-// coefficient (nd + alpha) * inv is recomputed where it is used, which keeps
-// SB_WAVES waves per CU resident.  The word part streams its rounds of 64
-// entries (the first SB_RB of the next P tokens prefetched, the rest in
-// batches of SB_BATCH loads); the selected lane re-walks its entries.
+// K up to 4096 (C = 32, 64): the draw of k_sample_sparse with the doc part's
+// lane partials split into groups of 16 topics.  A group's partial is the
+// Hillis-Steele inclusive scan of coef*beta across one 16-lane DPP row
+// (oracle/lda_oracle.c:group_rowscan16), so re-evaluating a changed group is
+// one row pass for the whole wave, and the A-part search over the selected
+// lane's C topics is one pass over NG rows plus a ballot.  LDS holds a
+// per-block float2 {alpha, inv} table and per-wave 16-bit document counts
+// (documents < 65536 tokens); coefficients are recomputed where used, which
+// keeps SB_WAVES waves per CU resident.  The word part streams its rounds of
+// 64 entries (the first SB_RB of the next P tokens prefetched, the rest in
+// batches); the selected lane's rounds are re-walked one per lane, followed
+// by a serial readlane chain that reproduces the sum pass's order.
 #define SB_RB 2
 #define SB_BATCH 4
 template <int C>
 constexpr int sb_waves() { return 12; }
 
 __device__ __forceinline__ int nd16_get(const uint32_t* nd2, int k) {
-  return (int)((nd2[k >> 1] >> ((k & 1) * 16)) & 0xFFFFu);
+  return (int)reinterpret_cast<const uint16_t*>(nd2)[k];
+}
+
+// inclusive scan inside each 16-lane row (sources outside the row add 0)
+__device__ __forceinline__ float row_scan16(float x) {
+  x = dpp_mov<0x111, 0xf, true>(x) + x;
+  x = dpp_mov<0x112, 0xf, true>(x) + x;
+  x = dpp_mov<0x114, 0xf, true>(x) + x;
+  x = dpp_mov<0x118, 0xf, true>(x) + x;
+  return x;
 }
 
 template <int C, int P, bool FROZEN>
@@ -810,6 +822,7 @@ __global__ __launch_bounds__(64 * sb_waves<C>()) void k_sample_sparse_big(Sample
   constexpr int WB = sb_waves<C>();
   const int lane = threadIdx.x & 63;
   const int wid = threadIdx.x >> 6;
+  const int row = lane >> 4, col = lane & 15;
   float2* tab = reinterpret_cast<float2*>(smem);                              // [KP] {alpha, inv}
   uint32_t* nd2 = reinterpret_cast<uint32_t*>(smem + 2 * KP) + wid * (KP / 2); // [KP/2]
 
@@ -819,42 +832,32 @@ __global__ __launch_bounds__(64 * sb_waves<C>()) void k_sample_sparse_big(Sample
 
   const float beta = p.beta;
   const int last_lane = (p.K - 1) / C;
-  const int last_j = (lane < last_lane) ? C - 1 : (p.K - 1) % C;
   const int32_t* __restrict__ nw = p.nw;
   const uint32_t* __restrict__ ent = p.ent;
   const int64_t* __restrict__ row_off = p.row_off;
   const int32_t* __restrict__ row_nnz = p.row_nnz;
   const float* __restrict__ inv_m1 = p.inv_m1;
 
-  // Coefficients of group g of this lane, 4 topics per step (few live
-  // registers); topic zc (if in the group) uses the own-token-removed invc.
-  auto quad_coefs = [&](float (&cf)[4], int k0, int zc, float invc) {
-    const uint2 nn = *reinterpret_cast<const uint2*>(nd2 + k0 / 2);
-    const float4 t0 = *reinterpret_cast<const float4*>(tab + k0);
-    const float4 t1 = *reinterpret_cast<const float4*>(tab + k0 + 2);
-    cf[0] = ((float)(nn.x & 0xFFFFu) + t0.x) * ((k0 == zc) ? invc : t0.y);
-    cf[1] = ((float)(nn.x >> 16) + t0.z) * ((k0 + 1 == zc) ? invc : t0.w);
-    cf[2] = ((float)(nn.y & 0xFFFFu) + t1.x) * ((k0 + 2 == zc) ? invc : t1.y);
-    cf[3] = ((float)(nn.y >> 16) + t1.z) * ((k0 + 3 == zc) ? invc : t1.w);
+  auto coef_at = [&](int k, int zc, float invc) -> float {
+    const float2 t = tab[k];
+    return ((float)nd16_get(nd2, k) + t.x) * ((k == zc) ? invc : t.y);
   };
-  auto group_sum = [&](int g, int zc, float invc) -> float {
-    float a = 0.0f;
-#pragma nounroll
-    for (int q = 0; q < 16; q += 4) {
-      float cf[4];
-      quad_coefs(cf, lane * C + g * 16 + q, zc, invc);
-      a = __builtin_fmaf(cf[0], beta, a);
-      a = __builtin_fmaf(cf[1], beta, a);
-      a = __builtin_fmaf(cf[2], beta, a);
-      a = __builtin_fmaf(cf[3], beta, a);
-    }
-    return a;
+  // one row pass: lane (row r, col j) evaluates topic owner*C + g*16 + j of
+  // the (owner, g) its row was given; returns the in-row inclusive scan
+  auto row_pass = [&](int owner, int g, int zc, float invc) -> float {
+    return row_scan16(coef_at(owner * C + g * 16 + col, zc, invc) * beta);
   };
-  auto regroup = [&](float (&TG)[NG], int g, int zc, float invc) {
-    const float v = group_sum(g, zc, invc);
+  auto set_tg = [&](float (&TG)[NG], int owner, int g, float v) {
 #pragma unroll
     for (int q = 0; q < NG; ++q)
-      if (q == g) TG[q] = v;
+      if (q == g) TG[q] = (lane == owner) ? v : TG[q];
+  };
+  auto get_tg = [&](const float (&TG)[NG], int g) -> float {
+    float v = TG[0];
+#pragma unroll
+    for (int q = 1; q < NG; ++q)
+      if (q == g) v = TG[q];
+    return v;
   };
   auto lane_total = [&](const float (&TG)[NG]) -> float {
     float t = TG[0];
@@ -892,6 +895,8 @@ __global__ __launch_bounds__(64 * sb_waves<C>()) void k_sample_sparse_big(Sample
     float cu = u01(draw_u32((uint64_t)(p.token_base + t0 + lane), p.c2, p.c3, p.k0, p.k1));
 
     float TG[NG];
+    // document start: every lane evaluates its own NG group trees serially
+    // (the same additions as the row scan, element by element)
     auto build_doc = [&](int64_t ts, int64_t te) {
       for (int64_t i = ts + lane; i < te; i += 64) {
         const int k = p.z[i];
@@ -899,7 +904,16 @@ __global__ __launch_bounds__(64 * sb_waves<C>()) void k_sample_sparse_big(Sample
       }
       wave_lds_fence();
 #pragma unroll
-      for (int g = 0; g < NG; ++g) TG[g] = group_sum(g, -1, 0.0f);
+      for (int g = 0; g < NG; ++g) {
+        float x[16];
+#pragma unroll
+        for (int j = 0; j < 16; ++j) x[j] = coef_at(lane * C + g * 16 + j, -1, 0.0f) * beta;
+#pragma unroll
+        for (int d = 1; d < 16; d <<= 1)
+#pragma unroll
+          for (int j = 15; j >= d; --j) x[j] = x[j - d] + x[j];
+        TG[g] = x[15];
+      }
     };
     auto clear_doc = [&]() {
 #pragma unroll
@@ -969,11 +983,12 @@ __global__ __launch_bounds__(64 * sb_waves<C>()) void k_sample_sparse_big(Sample
         // while the token is out: topic zc's coefficient uses invc (inv_m1[zo])
         const int zc = FROZEN ? -1 : zo;
         const float invc = FROZEN ? 0.0f : cinv[s];
+        const float g_saved = readlane_f(get_tg(TG, go), lo);
 
-        // remove the token from its document
+        // remove the token from its document; re-evaluate its group
         if (lane == 0) nd2[zo >> 1] -= (zo & 1) ? 0x10000u : 1u;
         wave_lds_fence();
-        if (lane == lo) regroup(TG, go, zc, invc);
+        set_tg(TG, lo, go, readlane_f(row_pass(lo, go, zc, invc), 15));
 
         // word part: rounds of 64 entries, lane l holds e = l + 64 r
         const int nr_all = (n + 63) >> 6;
@@ -982,9 +997,7 @@ __global__ __launch_bounds__(64 * sb_waves<C>()) void k_sample_sparse_big(Sample
           int cq = (int)(e >> ENT_TOPIC_BITS);
           if (valid && (uint32_t)cq == ENT_COUNT_SAT) cq = nw[(int64_t)w * KP + tq];
           if (!FROZEN) cq -= (tq == zo) ? 1 : 0;
-          const float2 t = tab[tq];
-          const float cf = ((float)nd16_get(nd2, tq) + t.x) * ((tq == zc) ? invc : t.y);
-          return valid ? cf * (float)cq : 0.0f;
+          return valid ? coef_at(tq, zc, invc) * (float)cq : 0.0f;
         };
         float accB = 0.0f;
 #pragma unroll
@@ -1020,72 +1033,62 @@ __global__ __launch_bounds__(64 * sb_waves<C>()) void k_sample_sparse_big(Sample
           const uint64_t m = __ballot((TB > thr) && (lane < nl));
           const int lstar = m ? (int)__builtin_ctzll(m) : nl - 1;
           const float E = lstar > 0 ? readlane_f(TB, lstar - 1) : 0.0f;
-          int tsel = 0;
-          if (lane == lstar) {
-            const int nr = (n - lane + 63) / 64;
-            float acc = 0.0f;
-            bool found = false;
+          // lane q takes round q of lane lstar (entry lstar + 64 q)
+          const int nr = (n - lstar + 63) >> 6;
+          uint32_t e = 0u;
 #pragma unroll
-            for (int q = 0; q < SB_RB; ++q) {
-              if (q < nr) {
-                int tq;
-                acc = acc + entry_b(ring[s][q], true, tq);
-                if (!found) tsel = tq;
-                if (!found && !(E + acc <= thr)) found = true;
-              }
-            }
-            for (int q0 = SB_RB; q0 < nr && !found; q0 += SB_BATCH) {
-              uint32_t eb[SB_BATCH];
-#pragma unroll
-              for (int b = 0; b < SB_BATCH; ++b)
-                eb[b] = (q0 + b < nr) ? ent[off + (q0 + b) * 64 + lane] : 0u;
-#pragma unroll
-              for (int b = 0; b < SB_BATCH; ++b) {
-                if (q0 + b < nr && !found) {
-                  int tq;
-                  acc = acc + entry_b(eb[b], true, tq);
-                  tsel = tq;
-                  if (!(E + acc <= thr)) found = true;
-                }
-              }
+          for (int q = 0; q < SB_RB; ++q) {
+            const uint32_t rq = (uint32_t)readlane_i((int)ring[s][q], lstar);
+            if (lane == q) e = rq;
+          }
+          if (lane >= SB_RB && lane < nr) e = ent[off + lstar + 64 * lane];
+          int tq;
+          const float term = entry_b(e, lane < nr, tq);
+          // the sum pass's serial order: acc = ((t0 + t1) + t2) + ...
+          float acc = 0.0f;
+          int sel = nr - 1;
+          for (int q = 0; q < nr; ++q) {
+            acc = acc + readlane_f(term, q);
+            if (!(E + acc <= thr)) {
+              sel = q;
+              break;
             }
           }
-          kn = readlane_i(tsel, lstar);
+          kn = readlane_i(tq, sel);
         } else {
           const float thr2 = thr - sumB;
           const uint64_t m = __ballot((TAs > thr2) && (lane <= last_lane));
           const int lstar = m ? (int)__builtin_ctzll(m) : last_lane;
           const float E = lstar > 0 ? readlane_f(TAs, lstar - 1) : 0.0f;
-          int jsel = 0;
-          if (lane == lstar) {
-            int cnt = 0;
-            float P_ = 0.0f;
-#pragma nounroll
-            for (int g = 0; g < NG; ++g) {
-              float a = 0.0f;
-#pragma nounroll
-              for (int q = 0; q < 16; q += 4) {
-                float cf[4];
-                quad_coefs(cf, lane * C + g * 16 + q, zc, invc);
+          // row r takes group r of lane lstar; group prefix P_{r-1} added on top
+          const float x = row_pass(lstar, row % NG, zc, invc);
+          float G[NG];
 #pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                  a = __builtin_fmaf(cf[j], beta, a);
-                  const float x = g == 0 ? a : P_ + a;
-                  cnt += (E + x <= thr2) ? 1 : 0;
-                }
-              }
-              P_ = g == 0 ? a : P_ + a;
-            }
-            jsel = cnt < C ? cnt : last_j;
+          for (int q = 0; q < NG; ++q) G[q] = readlane_f(x, 16 * q + 15);
+          float base = 0.0f, Pq = G[0];
+#pragma unroll
+          for (int q = 1; q < NG; ++q) {
+            if (row == q) base = Pq;
+            Pq = Pq + G[q];
           }
-          kn = lstar * C + readlane_i(jsel, lstar);
+          const float val = row == 0 ? x : base + x;
+          const int cnt = __builtin_popcountll(__ballot((E + val <= thr2) && lane < C));
+          const int last_j = (lstar < last_lane) ? C - 1 : (p.K - 1) % C;
+          kn = lstar * C + (cnt < C ? cnt : last_j);
         }
 
         // add the token back under its new topic
         if (lane == 0) nd2[kn >> 1] += (kn & 1) ? 0x10000u : 1u;
         wave_lds_fence();
-        if (lane == lo) regroup(TG, go, -1, 0.0f);
-        if (lane == kn / C) regroup(TG, (kn % C) / 16, -1, 0.0f);
+        if (kn == zo) {
+          set_tg(TG, lo, go, g_saved);        // the document is as before the removal
+        } else {
+          const int ln = kn / C, gn = (kn % C) / 16;
+          const float x = row_pass(row == 0 ? lo : ln, row == 0 ? go : gn, -1, 0.0f);
+          const float gl = readlane_f(x, 15), gk = readlane_f(x, 31);
+          set_tg(TG, lo, go, gl);
+          set_tg(TG, ln, gn, gk);
+        }
         cn = (lane == idx) ? kn : cn;
         if (!FROZEN && kn != zo) {
           if (lane < 2) {

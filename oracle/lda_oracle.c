@@ -407,14 +407,32 @@ static int exact_draw(const orc_exact* s, const int32_t* nwrow, const int32_t* n
  * TA_l = ((G_0 + G_1) + G_2) + ...; the prefix at element j of group g is
  * x_j = (G_0 + ... + G_{g-1}) + s_{g,j}  (s = serial fma inside the group).
  * For C <= 16 (one group) this is the plain serial fma chain. */
-static float lane_partial_grouped(const float* coef_lane, int C, float beta, float* G /*C/GS*/) {
-  const int GS = C < 16 ? C : 16;
-  float tot = 0.0f;
-  for (int g = 0; g < C / GS; ++g) {
+/* Doc-part partials of the sparse draw.  C <= 16: one serial fma chain of
+ * coef*beta per lane.  C >= 32 (k_sample_sparse_big): groups of 16 topics,
+ * each the Hillis-Steele inclusive scan of p_j = coef_j*beta across a 16-lane
+ * DPP row (row_shr 1,2,4,8; out-of-row sources add 0); x[] = the in-group
+ * prefix, G = x[15]; the lane partial is ((G0 + G1) + G2) + ... */
+static float group_rowscan16(const float* coef16, float beta, float x[16]) {
+  for (int j = 0; j < 16; ++j) x[j] = coef16[j] * beta;
+  for (int d = 1; d < 16; d <<= 1) {
+    float y[16];
+    for (int j = 0; j < 16; ++j) y[j] = j >= d ? x[j - d] : 0.0f;
+    for (int j = 0; j < 16; ++j) x[j] = x[j] + y[j];
+  }
+  return x[15];
+}
+
+static float lane_partial_grouped(const float* coef_lane, int C, float beta, float* G) {
+  if (C <= 16) {
     float a = 0.0f;
-    for (int j = 0; j < GS; ++j) a = fmaf(coef_lane[g * GS + j], beta, a);
-    G[g] = a;
-    tot = g == 0 ? a : tot + a;
+    for (int j = 0; j < C; ++j) a = fmaf(coef_lane[j], beta, a);
+    G[0] = a;
+    return a;
+  }
+  float tot = 0.0f, x[16];
+  for (int g = 0; g < C / 16; ++g) {
+    G[g] = group_rowscan16(coef_lane + 16 * g, beta, x);
+    tot = g == 0 ? G[g] : tot + G[g];
   }
   return tot;
 }
@@ -422,7 +440,6 @@ static float lane_partial_grouped(const float* coef_lane, int C, float beta, flo
 static int exact_draw_sparse(const orc_exact* s, const int32_t* nwrow, const int32_t* nd, int zo,
                              float u, float* coef, int32_t* et, int32_t* ec) {
   const int C = s->C, K = s->K, Kp = s->Kp;
-  const int GS = C < 16 ? C : 16;
   for (int k = 0; k < Kp; ++k)
     coef[k] = ((float)nd[k] + s->alpha_f[k]) * (k == zo ? s->inv_m1[k] : s->inv[k]);
   int n = 0;
@@ -471,17 +488,20 @@ static int exact_draw_sparse(const orc_exact* s, const int32_t* nwrow, const int
       break;
     }
   const float E = lstar > 0 ? TA[lstar - 1] : 0.0f;
-  lane_partial_grouped(coef + lstar * C, C, s->beta_f, G);
   int cnt = 0;
-  float P = 0.0f;
-  for (int g = 0; g < C / GS; ++g) {
+  if (C <= 16) {
     float a = 0.0f;
-    for (int j = 0; j < GS; ++j) {
-      a = fmaf(coef[lstar * C + g * GS + j], s->beta_f, a);
-      const float x = g == 0 ? a : P + a;
-      cnt += (E + x <= thr2) ? 1 : 0;
+    for (int j = 0; j < C; ++j) {
+      a = fmaf(coef[lstar * C + j], s->beta_f, a);
+      cnt += (E + a <= thr2) ? 1 : 0;
     }
-    P = g == 0 ? G[0] : P + G[g];
+  } else {
+    float P = 0.0f, x[16];
+    for (int g = 0; g < C / 16; ++g) {
+      const float Gg = group_rowscan16(coef + lstar * C + 16 * g, s->beta_f, x);
+      for (int j = 0; j < 16; ++j) cnt += (E + (g == 0 ? x[j] : P + x[j]) <= thr2) ? 1 : 0;
+      P = g == 0 ? Gg : P + Gg;
+    }
   }
   const int jsel = cnt < C ? cnt : ((lstar < last_lane) ? C - 1 : (K - 1) % C);
   return lstar * C + jsel;
