@@ -799,7 +799,7 @@ __global__ __launch_bounds__(256) void k_sample_sparse(SampleParams p) {
 #define SB_RB 2
 #define SB_BATCH 4
 template <int C>
-constexpr int sb_waves() { return 12; }
+constexpr int sb_waves() { return 16; }
 
 __device__ __forceinline__ int nd16_get(const uint32_t* nd2, int k) {
   return (int)reinterpret_cast<const uint16_t*>(nd2)[k];
@@ -903,7 +903,7 @@ __global__ __launch_bounds__(64 * sb_waves<C>()) void k_sample_sparse_big(Sample
         atomicAdd(&nd2[k >> 1], (k & 1) ? 0x10000u : 1u);
       }
       wave_lds_fence();
-#pragma unroll
+#pragma nounroll
       for (int g = 0; g < NG; ++g) {
         float x[16];
 #pragma unroll
@@ -912,7 +912,9 @@ __global__ __launch_bounds__(64 * sb_waves<C>()) void k_sample_sparse_big(Sample
         for (int d = 1; d < 16; d <<= 1)
 #pragma unroll
           for (int j = 15; j >= d; --j) x[j] = x[j - d] + x[j];
-        TG[g] = x[15];
+#pragma unroll
+        for (int q = 0; q < NG; ++q)
+          if (q == g) TG[q] = x[15];
       }
     };
     auto clear_doc = [&]() {
