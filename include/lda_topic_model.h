@@ -96,6 +96,14 @@ lda_status ldatm_print_top_words(ldatm* m, const char* path, int32_t num_words,
 lda_status ldatm_top_words_text(ldatm* m, int32_t num_words, int32_t using_new_lines, char* buf,
                                 size_t cap, size_t* len);
 
+/* Checkpoint / resume: the reference's save()/load() of its model
+ * (src/cmu_ron/TrainAndPredict.java:179-200) as a native binary file holding
+ * every field needed to continue bit for bit (documents, alphabet, sources,
+ * topics, alpha/beta, options, pending optimisation statistics and the
+ * Philox sweep counter).  ldatm_load creates a new model. */
+lda_status ldatm_save(ldatm* m, const char* path);
+lda_status ldatm_load(ldatm** out, const char* path);
+
 /* getInferencer().getSampledDistribution(instance, numIterations, thinning,
  * burnIn) [src/cmu_ron/TrainAndPredict.java:144], batched over Dh documents
  * (word ids of the model alphabet; ids >= V are dropped like Mallet's

@@ -101,7 +101,10 @@ ParallelTopicModel::~ParallelTopicModel() = default;
 // Anything that invalidates the GPU shards first saves the current topic
 // assignments (documents keep their z across re-sharding / addInstances).
 void ParallelTopicModel::markDirty() {
-  if (shards_ && !shards_dirty_) z_cache_ = topics();
+  if (shards_ && !shards_dirty_) {
+    z_cache_ = topics();
+    check(lda_get_sweep(shards_->ctx[0], &sweep_), "lda_get_sweep");
+  }
   shards_dirty_ = true;
 }
 
@@ -222,14 +225,17 @@ void ParallelTopicModel::ensureShards() {
   // the shards' local counts are the pending delta: sum them, apply
   sg->reduce();
   sg->apply();
+  for (auto c : sg->ctx) check(lda_set_sweep(c, sweep_), "lda_set_sweep");
   shards_ = std::move(sg);
   shards_dirty_ = false;
   z_dirty_ = true;
-  max_doc_len_ = 0;
-  for (int64_t d = 0; d < D; ++d)
-    max_doc_len_ = std::max<int32_t>(max_doc_len_, (int32_t)(doc_off_[d + 1] - doc_off_[d]));
-  doc_len_counts_.assign((size_t)max_doc_len_ + 1, 0);
-  topic_doc_counts_.assign((size_t)K_ * (max_doc_len_ + 1), 0);
+  int32_t m = 0;
+  for (int64_t d = 0; d < D; ++d) m = std::max<int32_t>(m, (int32_t)(doc_off_[d + 1] - doc_off_[d]));
+  if (m != max_doc_len_) {  // statistics gathered so far stay valid unless the shape changes
+    max_doc_len_ = m;
+    doc_len_counts_.assign((size_t)max_doc_len_ + 1, 0);
+    topic_doc_counts_.assign((size_t)K_ * (max_doc_len_ + 1), 0);
+  }
 }
 
 std::vector<int32_t> ParallelTopicModel::topics() {
@@ -433,6 +439,144 @@ std::string ParallelTopicModel::displayTopWords(int32_t num_words, bool using_ne
   return out;
 }
 
+// ---- checkpoint: little-endian binary, every field needed to continue the
+// run bit for bit (topics, hyperparameters, options, the statistics gathered
+// since the last optimisation, and the Philox sweep counter).
+namespace {
+constexpr char kMagic[8] = {'L', 'D', 'A', 'T', 'M', 0, 'v', '1'};
+
+struct Writer {
+  std::ofstream f;
+  template <typename T>
+  void pod(const T& v) { f.write(reinterpret_cast<const char*>(&v), sizeof(T)); }
+  template <typename T>
+  void vec(const std::vector<T>& v) {
+    pod<int64_t>((int64_t)v.size());
+    if (!v.empty()) f.write(reinterpret_cast<const char*>(v.data()), (std::streamsize)(v.size() * sizeof(T)));
+  }
+  void str(const std::string& s) {
+    pod<int64_t>((int64_t)s.size());
+    f.write(s.data(), (std::streamsize)s.size());
+  }
+};
+
+struct Reader {
+  std::ifstream f;
+  template <typename T>
+  T pod() {
+    T v{};
+    f.read(reinterpret_cast<char*>(&v), sizeof(T));
+    if (!f) raise(LDA_ERR_INVALID_ARG, "checkpoint truncated");
+    return v;
+  }
+  int64_t count(int64_t limit) {
+    const int64_t n = pod<int64_t>();
+    if (n < 0 || n > limit) raise(LDA_ERR_INVALID_ARG, "checkpoint corrupt (bad length)");
+    return n;
+  }
+  template <typename T>
+  std::vector<T> vec(int64_t limit) {
+    std::vector<T> v((size_t)count(limit));
+    if (!v.empty()) f.read(reinterpret_cast<char*>(v.data()), (std::streamsize)(v.size() * sizeof(T)));
+    if (!f) raise(LDA_ERR_INVALID_ARG, "checkpoint truncated");
+    return v;
+  }
+  std::string str() {
+    std::string s((size_t)count(1 << 30), '\0');
+    f.read(&s[0], (std::streamsize)s.size());
+    if (!f) raise(LDA_ERR_INVALID_ARG, "checkpoint truncated");
+    return s;
+  }
+};
+}  // namespace
+
+void ParallelTopicModel::save(const std::string& path) {
+  // live shards: their state; otherwise the snapshot (possibly no topics yet:
+  // a model saved before its first use re-initialises them on load)
+  const bool live = shards_ && !shards_dirty_;
+  const std::vector<int32_t> z = live ? topics() : z_cache_;
+  if (live) check(lda_get_sweep(shards_->ctx[0], &sweep_), "lda_get_sweep");
+  Writer w{std::ofstream(path, std::ios::binary)};
+  if (!w.f) raise(LDA_ERR_INVALID_ARG, "cannot open " + path);
+  w.f.write(kMagic, 8);
+  w.pod(K_);
+  w.pod(V_);
+  w.pod(alpha_sum_);
+  w.pod(beta_);
+  w.vec(alpha_);
+  w.pod(seed_);
+  w.pod(sweep_);
+  for (int32_t v : {num_iterations_, optimize_interval_, burnin_period_, save_sample_interval_,
+                    show_topics_interval_, words_per_topic_, (int32_t)symmetric_alpha_,
+                    (int32_t)print_log_likelihood_, num_threads_, sampler_})
+    w.pod(v);
+  w.vec(doc_off_);
+  w.vec(words_);
+  w.vec(z);
+  w.pod<int64_t>((int64_t)alphabet_.size());
+  for (const auto& a : alphabet_) w.str(a);
+  w.vec(has_source_);
+  for (const auto& src : sources_) w.str(src);
+  w.pod(max_doc_len_);
+  w.vec(doc_len_counts_);
+  w.vec(topic_doc_counts_);
+  w.f.flush();
+  if (!w.f) raise(LDA_ERR_INVALID_ARG, "write failed: " + path);
+}
+
+std::unique_ptr<ParallelTopicModel> ParallelTopicModel::load(const std::string& path) {
+  Reader r{std::ifstream(path, std::ios::binary)};
+  if (!r.f) raise(LDA_ERR_INVALID_ARG, "cannot open " + path);
+  char magic[8];
+  r.f.read(magic, 8);
+  if (!r.f || std::memcmp(magic, kMagic, 8) != 0) raise(LDA_ERR_INVALID_ARG, "not an lda_topic_model checkpoint");
+  const int32_t K = r.pod<int32_t>(), V = r.pod<int32_t>();
+  const double alpha_sum = r.pod<double>(), beta = r.pod<double>();
+  auto m = std::make_unique<ParallelTopicModel>(K, alpha_sum, beta);
+  m->V_ = V;
+  m->alpha_ = r.vec<double>(K);
+  if ((int32_t)m->alpha_.size() != K) raise(LDA_ERR_INVALID_ARG, "checkpoint corrupt (alpha)");
+  m->seed_ = r.pod<uint64_t>();
+  m->sweep_ = r.pod<uint32_t>();
+  int32_t opt[10];
+  for (int32_t& v : opt) v = r.pod<int32_t>();
+  m->num_iterations_ = opt[0];
+  m->optimize_interval_ = opt[1];
+  m->burnin_period_ = opt[2];
+  m->save_sample_interval_ = opt[3];
+  m->show_topics_interval_ = opt[4];
+  m->words_per_topic_ = opt[5];
+  m->symmetric_alpha_ = opt[6] != 0;
+  m->print_log_likelihood_ = opt[7] != 0;
+  m->num_threads_ = opt[8];
+  m->sampler_ = opt[9];
+  const int64_t big = (int64_t)1 << 40;
+  m->doc_off_ = r.vec<int64_t>(big);
+  m->words_ = r.vec<int32_t>(big);
+  m->z_cache_ = r.vec<int32_t>(big);
+  const int64_t D = (int64_t)m->doc_off_.size() - 1;
+  if (D < 0 || m->doc_off_[0] != 0 || m->doc_off_.back() != (int64_t)m->words_.size() ||
+      (!m->z_cache_.empty() && m->z_cache_.size() != m->words_.size()))
+    raise(LDA_ERR_INVALID_ARG, "checkpoint corrupt (documents)");
+  for (int32_t wid : m->words_)
+    if (wid < 0 || wid >= V) raise(LDA_ERR_INVALID_ARG, "checkpoint corrupt (word id)");
+  for (int32_t t : m->z_cache_)
+    if (t < 0 || t >= K) raise(LDA_ERR_INVALID_ARG, "checkpoint corrupt (topic)");
+  const int64_t na = r.count(V);
+  for (int64_t i = 0; i < na; ++i) m->alphabet_.push_back(r.str());
+  m->has_source_ = r.vec<uint8_t>(D);
+  for (int64_t d = 0; d < (int64_t)m->has_source_.size(); ++d) m->sources_.push_back(r.str());
+  m->max_doc_len_ = r.pod<int32_t>();
+  m->doc_len_counts_ = r.vec<int32_t>(big);
+  m->topic_doc_counts_ = r.vec<int32_t>(big);
+  if ((int64_t)m->has_source_.size() != D ||
+      (m->max_doc_len_ >= 0 && (m->doc_len_counts_.size() != (size_t)m->max_doc_len_ + 1 ||
+                                m->topic_doc_counts_.size() != (size_t)K * (m->max_doc_len_ + 1))))
+    raise(LDA_ERR_INVALID_ARG, "checkpoint corrupt (statistics)");
+  m->shards_dirty_ = true;
+  return m;
+}
+
 void ParallelTopicModel::infer(int64_t Dh, const int64_t* doc_off, const int32_t* words,
                                int32_t num_iterations, int32_t thinning, int32_t burn_in,
                                uint64_t seed, double* theta) {
@@ -456,8 +600,11 @@ void ParallelTopicModel::infer(int64_t Dh, const int64_t* doc_off, const int32_t
 
 // ------------------------------------------------------------------ C ABI
 struct ldatm {
-  lda_host::ParallelTopicModel model;
-  ldatm(int32_t K, double a, double b) : model(K, a, b) {}
+  std::unique_ptr<lda_host::ParallelTopicModel> owned;
+  lda_host::ParallelTopicModel& model;
+  ldatm(int32_t K, double a, double b)
+      : owned(std::make_unique<lda_host::ParallelTopicModel>(K, a, b)), model(*owned) {}
+  explicit ldatm(std::unique_ptr<lda_host::ParallelTopicModel> m) : owned(std::move(m)), model(*owned) {}
 };
 
 namespace {
@@ -670,6 +817,27 @@ lda_status ldatm_print_top_words(ldatm* m, const char* path, int32_t num_words, 
   std::string s;
   lda_status st = guard([&] { s = m->model.displayTopWords(num_words, using_new_lines != 0); });
   return st ? st : write_file(path, s);
+}
+
+lda_status ldatm_save(ldatm* m, const char* path) {
+  TM_CHECK(m);
+  if (!path) {
+    g_tm_error = "null path";
+    return LDA_ERR_INVALID_ARG;
+  }
+  return guard([&] { m->model.save(path); });
+}
+
+lda_status ldatm_load(ldatm** out, const char* path) {
+  if (!out || !path) {
+    g_tm_error = "null argument";
+    return LDA_ERR_INVALID_ARG;
+  }
+  *out = nullptr;
+  return guard([&] {
+    auto loaded = lda_host::ParallelTopicModel::load(path);
+    *out = new ldatm(std::move(loaded));
+  });
 }
 
 lda_status ldatm_infer(ldatm* m, int64_t Dh, const int64_t* doc_off, const int32_t* words,

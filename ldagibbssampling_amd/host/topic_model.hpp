@@ -72,6 +72,11 @@ class ParallelTopicModel {
   std::string documentTopics(double threshold, int32_t max);
   std::string displayTopWords(int32_t num_words, bool using_new_lines);
 
+  // ---- checkpoint / resume (the reference's save()/load(),
+  //      src/cmu_ron/TrainAndPredict.java:179-200, as a native format) ----
+  void save(const std::string& path);
+  static std::unique_ptr<ParallelTopicModel> load(const std::string& path);
+
   // ---- inference (TopicInferencer.getSampledDistribution, batched) ---
   void infer(int64_t Dh, const int64_t* doc_off, const int32_t* words, int32_t num_iterations,
              int32_t thinning, int32_t burn_in, uint64_t seed, double* theta);
@@ -103,7 +108,8 @@ class ParallelTopicModel {
 
   std::unique_ptr<ShardGroup> shards_;
   bool shards_dirty_ = true;
-  int32_t max_doc_len_ = 0;
+  int32_t max_doc_len_ = -1;
+  uint32_t sweep_ = 0;  // Philox sweep counter carried across re-sharding
   std::vector<int32_t> doc_len_counts_, topic_doc_counts_;  // alpha statistics
   std::vector<std::pair<int32_t, double>> ll_trace_;
 };

@@ -66,6 +66,8 @@ TM_SIGNATURES = {
                                           C.POINTER(C.c_size_t)]),
     "ldatm_print_top_words": (_i32, [_vp, C.c_char_p, _i32, _i32]),
     "ldatm_top_words_text": (_i32, [_vp, _i32, _i32, _vp, C.c_size_t, C.POINTER(C.c_size_t)]),
+    "ldatm_save": (_i32, [_vp, C.c_char_p]),
+    "ldatm_load": (_i32, [C.POINTER(_vp), C.c_char_p]),
     "ldatm_infer": (_i32, [_vp, C.c_int64, _i64p, _vp, _i32, _i32, _i32, C.c_uint64, _f64p]),
     "ldatm_format_double": (_i32, [C.c_double, _i32, C.c_char_p, C.c_size_t]),
     "ldatm_last_error": (C.c_char_p, []),
@@ -356,6 +358,23 @@ class ParallelTopicModel:
     def printTopWords(self, path, numWords: int, usingNewLines: bool = False):
         _check(self._L.ldatm_print_top_words(self._h, os.fsencode(path), int(numWords),
                                              int(bool(usingNewLines))), "printTopWords")
+
+    # ------------------------------------------------ checkpoint / resume
+    def save(self, path):
+        """Everything needed to continue this run bit for bit."""
+        _check(self._L.ldatm_save(self._h, os.fsencode(path)), "ldatm_save")
+
+    @classmethod
+    def load(cls, path) -> "ParallelTopicModel":
+        L = load_tm()
+        h = C.c_void_p()
+        _check(L.ldatm_load(C.byref(h), os.fsencode(path)), "ldatm_load")
+        m = cls.__new__(cls)
+        m._h, m._L = h, L
+        m.numTopics = m._shape()[0]
+        m.alphabet = None
+        m.data = []
+        return m
 
     # -------------------------------------------------------- inference
     def getInferencer(self) -> "TopicInferencer":

@@ -96,3 +96,27 @@ def test_model_options_without_gpu(L):
     if not torch.cuda.is_available():
         with pytest.raises(capi.LdaError):
             m.estimate()
+
+
+def test_checkpoint_round_trip_without_gpu(L, tmp_path):
+    """save()/load() of a model that has not sampled yet is host-only."""
+    il = tm.InstanceList.fromInverseDocs("a\tx\ty\tz\nb\ty\tz\nc\tq\n")
+    m = tm.ParallelTopicModel(7, 3.5, 0.02)
+    m.setOptimizeInterval(20)
+    m.setBurninPeriod(50)
+    m.setRandomSeed(11)
+    m.addInstances(il)
+    p = tmp_path / "model.ldatm"
+    m.save(str(p))
+    r = tm.ParallelTopicModel.load(str(p))
+    assert r._shape() == m._shape() == (7, 4, 3, 6)
+    np.testing.assert_array_equal(r.alpha, m.alpha)
+    assert r.beta == 0.02 and r.alphaSum == 3.5
+    bad = tmp_path / "bad.ldatm"
+    bad.write_bytes(b"not a checkpoint")
+    with pytest.raises(capi.LdaError):
+        tm.ParallelTopicModel.load(str(bad))
+    trunc = tmp_path / "trunc.ldatm"
+    trunc.write_bytes(p.read_bytes()[:60])
+    with pytest.raises(capi.LdaError):
+        tm.ParallelTopicModel.load(str(trunc))

@@ -207,3 +207,23 @@ def test_inferencer_matches_sampler_inference():
     np.testing.assert_allclose(theta, exp, rtol=0, atol=0)
     one = inf.getSampledDistribution(held_il[0], 40, 5, 10, seed=3)
     assert one.shape == (32,) and abs(one.sum() - 1) < 1e-12
+
+
+def test_checkpoint_resume_is_bit_exact(tmp_path):
+    """estimate(); save; estimate() == load; estimate(): topics, alpha, beta,
+    with the optimisation schedule and statistics crossing the checkpoint."""
+    from ldagibbssampling_amd import topic_model as tm
+    c = synthetic_lda(num_docs=150, num_types=500, num_topics=10, doc_len=None, mean_len=40,
+                      min_len=1, max_len=120, seed=13)
+    m, _ = _model(c, 16, 8.0, 0.05, 4, setNumIterations=25, setOptimizeInterval=10,
+                  setBurninPeriod=5, setSaveSampleInterval=5)
+    m.estimate()
+    path = tmp_path / "ckpt.ldatm"
+    m.save(str(path))
+    m.estimate()
+    r = tm.ParallelTopicModel.load(str(path))
+    r.estimate()
+    np.testing.assert_array_equal(r.topicAssignments(), m.topicAssignments())
+    np.testing.assert_array_equal(r.alpha, m.alpha)
+    assert r.beta == m.beta
+    assert r.modelLogLikelihood() == m.modelLogLikelihood()
