@@ -56,3 +56,61 @@ def test_heldout_perplexity_within_1pct(oracle, K, alpha_sum, beta):
     print(f"K={K}: gpu {pg} mean {mg:.3f} | cpu_mallet {pm} mean {mm:.3f} | "
           f"rel diff {(mg - mm) / mm:+.4%}")
     assert abs(mg - mm) <= 0.01 * mm
+
+
+def _corpus_split(K):
+    from ldagibbssampling_amd.corpus import synthetic_lda, document_completion_split
+    c = synthetic_lda(num_docs=2200, num_types=3000, num_topics=K, doc_len=None, mean_len=80,
+                      min_len=10, max_len=300, seed=20261015, k_true=min(K, 50))
+    rng = np.random.default_rng(0)
+    perm = rng.permutation(c.num_docs)
+    n_held = c.num_docs // 10
+    train = c.subset(np.sort(perm[n_held:]))
+    held_obs, held_sc = document_completion_split(c.subset(np.sort(perm[:n_held])))
+    return c, train, held_obs, held_sc
+
+
+@pytest.mark.parametrize("K,alpha_sum,beta", [
+    (100, 10.0, 0.001),     # src/cmu/TrainAndPredict.java:259
+    (500, 100.0, 1.0),      # src/cmu_ron/TrainAndPredict.java:160
+])
+def test_heldout_perplexity_reference_settings(oracle, K, alpha_sum, beta):
+    """The reference's own training configuration, hyperparameter optimisation
+    on (setOptimizeInterval(20), Mallet's default burn-in 200, 4 threads,
+    1000 sweeps): the native ParallelTopicModel on the GPU vs cpu_mallet.
+    Each model is scored with its own learned alpha/beta."""
+    from ldagibbssampling_amd import topic_model as tm
+    from ldagibbssampling_amd.sampler import GibbsSampler
+    c, train, held_obs, held_sc = _corpus_split(K)
+    alphabet = tm.Alphabet(range(c.num_types))
+    held_il = tm.InstanceList.fromCorpus(held_obs, alphabet)
+    pg, pm, hyper = [], [], []
+    for seed in (1, 2, 3):
+        m = tm.ParallelTopicModel(K, alpha_sum, beta)
+        m.addInstances(tm.InstanceList.fromCorpus(train, alphabet))
+        m.setRandomSeed(seed)
+        m.setTopicDisplay(0, 0)
+        m.setOptimizeInterval(20)
+        m.setNumThreads(4)
+        m.setNumIterations(1000)
+        m.estimate()
+        theta = m.getInferencer().getSampledDistributions(held_il, 100, 10, 10, seed=7)
+        nw, nwsum = m.typeTopicCounts()
+        ll = oracle.doc_completion_loglik(K, c.num_types, nw, nwsum, m.beta, theta,
+                                          held_sc.doc_off, held_sc.words)
+        pg.append(float(np.exp(-ll / held_sc.num_tokens)))
+        mm = oracle.MalletModel(K, alpha_sum, beta, c.num_types, train.doc_off, train.words,
+                                seed=seed, num_threads=4)
+        mm.set_optimize(20, burnin=200)
+        mm.estimate(1000)
+        a_m, b_m = mm.hyper()
+        gm = GibbsSampler(K, c.num_types, train.doc_off, train.words, a_m, b_m, seed=seed,
+                          z_init=mm.z())
+        gm.sweep(0)
+        pm.append(_perplexity(gm, held_obs, held_sc, oracle))
+        hyper.append((float(m.alphaSum), float(m.beta), float(a_m.sum()), float(b_m)))
+    mg, mmn = float(np.mean(pg)), float(np.mean(pm))
+    print(f"K={K} (alphaSum {alpha_sum}, beta {beta}, optimizeInterval 20): gpu {pg} mean "
+          f"{mg:.3f} | cpu_mallet {pm} mean {mmn:.3f} | rel diff {(mg - mmn) / mmn:+.4%} | "
+          f"learned (alphaSum, beta) gpu/mallet {hyper}")
+    assert abs(mg - mmn) <= 0.01 * mmn
