@@ -15,6 +15,7 @@
 // lda_count_histogram); this file is the fp64 arithmetic, restated from the
 // published algorithm.  Its independent restatement for the tests lives in
 // oracle/lda_oracle.c (orc_learn_parameters, orc_learn_symmetric_concentration).
+#include <algorithm>
 #include <cmath>
 #include <cstdint>
 #include <string>
@@ -44,6 +45,15 @@ double digamma(double z) {
   return psi;
 }
 
+// Two deliberate departures from Mallet's literal arithmetic (both no-ops for
+// ordinary values): the digamma steps add the integer offset first,
+// 1/(a + (i-1)), because Java's (a + i) - 1 cancels to 0 once a < 1.1e-16 --
+// which happens to topics that die under optimisation (K = 500, alphaSum =
+// 100 on a small corpus) -- and turns alpha into inf/NaN; and an updated
+// alpha_k is floored at 1e-300 so that a dead topic cannot underflow to 0
+// over thousands of sweeps (0 * inf again).
+constexpr double kMinParameter = 1e-300;
+
 }  // namespace
 
 extern "C" {
@@ -68,7 +78,7 @@ lda_status lda_learn_parameters(double* params, int32_t K, const int32_t* observ
     // the digamma difference accumulated term by term, minus 1/scale
     double denom = 0.0, dig = 0.0;
     for (int64_t n = 1; n < L1; ++n) {
-      dig += 1.0 / (psum + (double)n - 1.0);
+      dig += 1.0 / (psum + (double)(n - 1));
       denom += (double)observation_lengths[n] * dig;
     }
     denom -= 1.0 / scale;
@@ -78,10 +88,10 @@ lda_status lda_learn_parameters(double* params, int32_t K, const int32_t* observ
       double num = 0.0;
       dig = 0.0;
       for (int64_t i = 1; i <= last[k]; ++i) {
-        dig += 1.0 / (old + (double)i - 1.0);
+        dig += 1.0 / (old + (double)(i - 1));
         num += (double)observations[k * L1 + i] * dig;
       }
-      params[k] = old * (num + shape) / denom;
+      params[k] = std::max(old * (num + shape) / denom, kMinParameter);
       psum += params[k];
     }
   }
@@ -114,7 +124,7 @@ lda_status lda_learn_symmetric_concentration(const int32_t* count_hist, int64_t 
     const double per_dim = value / num_dims;
     double dig = 0.0, num = 0.0;
     for (int64_t c = 1; c <= top; ++c) {
-      dig += 1.0 / (per_dim + (double)c - 1.0);
+      dig += 1.0 / (per_dim + (double)(c - 1));
       num += (double)count_hist[c] * dig;
     }
     // sum over lengths n of count(n) * (psi(value + n) - psi(value)); far

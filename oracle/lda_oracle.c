@@ -148,7 +148,7 @@ double orc_learn_parameters(double* a, int32_t K, const int32_t* hist, const int
   for (int32_t it = 0; it < iters; ++it) {
     double den = 0.0, d = 0.0;
     for (int64_t n = 1; n < W; ++n) {
-      d += 1.0 / (A + n - 1);
+      d += 1.0 / (A + (double)(n - 1));
       den += lens[n] * d;
     }
     den -= 1.0 / scale;
@@ -158,10 +158,11 @@ double orc_learn_parameters(double* a, int32_t K, const int32_t* hist, const int
       double num = 0.0;
       d = 0.0;
       for (int64_t i = 1; i <= top[k]; ++i) {
-        d += 1.0 / (ak + i - 1);
+        d += 1.0 / (ak + (double)(i - 1));   /* not (ak + i) - 1: cancels for ak < 1.1e-16 */
         num += hist[k * W + i] * d;
       }
       a[k] = ak * (num + shape) / den;
+      if (a[k] < 1e-300) a[k] = 1e-300;     /* a dead topic must not underflow to 0 */
       A += a[k];
     }
   }
@@ -183,7 +184,7 @@ double orc_learn_symmetric_concentration(const int32_t* counts, int64_t max_coun
     const double p = value / dims;
     double num = 0.0, d = 0.0;
     for (int64_t c = 1; c <= top; ++c) {
-      d += 1.0 / (p + c - 1);
+      d += 1.0 / (p + (double)(c - 1));
       num += counts[c] * d;
     }
     const double psi0 = orc_digamma(value);

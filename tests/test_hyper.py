@@ -118,3 +118,23 @@ def test_mallet_oracle_optimisation_moves_hyperparameters(oracle):
     a, b = m.hyper()
     assert not np.allclose(a, 1.0) and b != 0.01
     assert np.all(a > 0) and b > 0
+
+
+def test_dead_topics_stay_finite(oracle):
+    """A topic whose alpha has decayed below 1.1e-16 and then reappears in a
+    document: Mallet's literal (a + i) - 1 cancels to 0 there (1/0 -> inf ->
+    NaN alpha).  Both restatements add the integer offset first and floor
+    alpha at 1e-300, so the update stays finite and positive."""
+    K, L = 4, 10
+    hist = np.zeros((K, L + 1), np.int32)
+    lens = np.zeros(L + 1, np.int32)
+    lens[10] = 50
+    hist[0, 1] = 3
+    hist[0, 2] = 1
+    hist[1, 10] = 40
+    for a0 in (1e-17, 1e-200, 1e-300):
+        alpha = np.array([a0, 0.5, 1e-250, 0.3])
+        ap, sp = _learn_parameters_product(alpha, hist, lens)
+        ao, so = oracle.learn_parameters(alpha, hist, lens)
+        np.testing.assert_array_equal(ap, ao)
+        assert np.all(np.isfinite(ap)) and np.all(ap >= 1e-300) and np.isfinite(sp)
