@@ -201,6 +201,8 @@ __device__ __forceinline__ int32_t row16_count(const uint32_t (&r)[(C + 1) / 2],
   else return (int32_t)((j & 1) ? (r[j >> 1] >> 16) : (r[j >> 1] & 0xFFFFu));
 }
 
+typedef float pkf32 __attribute__((ext_vector_type(2)));
+
 template <int C, int P, bool FROZEN>
 __global__ __launch_bounds__(256) void k_sample(SampleParams p) {
   extern __shared__ __attribute__((aligned(16))) int32_t smem[];
@@ -237,35 +239,40 @@ __global__ __launch_bounds__(256) void k_sample(SampleParams p) {
     r = uniform_i(__shfl(r, 0));
     if (r >= p.num_ranges) break;
     const int64_t d0 = p.range_doc[r], d1 = p.range_doc[r + 1];
-    const int64_t t0 = p.doc_off[d0], t1 = p.doc_off[d1];
-    if (t1 <= t0) continue;
+    const int64_t t0 = p.doc_off[d0];
+    // token positions below are 32-bit offsets from the range start
+    const int nt = (int)(p.doc_off[d1] - t0);
+    if (nt <= 0) continue;
+    const int32_t* __restrict__ wrd = p.words + t0;
+    int32_t* __restrict__ zr = p.z + t0;
+    const uint64_t gbase = (uint64_t)(p.token_base + t0);
 
     // --- chunk registers: chunk c (cw, cz, cu, cn, cf), c+1 (w1, z1, f1), c+2 (w2, z2);
     // f = 1 when the word's row holds a count > 65535 (read the int32 row)
-    int64_t cbase = t0;
+    int cbase = 0;
     int cw = 0, cz = 0, w1 = 0, z1 = 0, w2 = 0, z2 = 0;
-    if (t0 + lane < t1) {
-      cw = p.words[t0 + lane];
-      cz = p.z[t0 + lane];
+    if (lane < nt) {
+      cw = wrd[lane];
+      cz = zr[lane];
     }
-    if (t0 + 64 + lane < t1) {
-      w1 = p.words[t0 + 64 + lane];
-      z1 = p.z[t0 + 64 + lane];
+    if (64 + lane < nt) {
+      w1 = wrd[64 + lane];
+      z1 = zr[64 + lane];
     }
-    if (t0 + 128 + lane < t1) {
-      w2 = p.words[t0 + 128 + lane];
-      z2 = p.z[t0 + 128 + lane];
+    if (128 + lane < nt) {
+      w2 = wrd[128 + lane];
+      z2 = zr[128 + lane];
     }
     int cf = (int)wide_of[cw], f1 = (int)wide_of[w1];
     int cn = cz;
-    float cu = u01(draw_u32((uint64_t)(p.token_base + t0 + lane), p.c2, p.c3, p.k0, p.k1));
+    float cu = u01(draw_u32(gbase + (uint64_t)lane, p.c2, p.c3, p.k0, p.k1));
 
     // --- first document of the range (nd is all zero here)
     int64_t doc = d0;
     while (p.doc_off[doc + 1] <= t0) ++doc;
-    int64_t doc_end = p.doc_off[doc + 1];
+    int doc_end = (int)(p.doc_off[doc + 1] - t0);
     {
-      for (int64_t i = t0 + lane; i < doc_end; i += 64) atomicAdd(&nd[p.z[i]], 1);
+      for (int i = lane; i < doc_end; i += 64) atomicAdd(&nd[zr[i]], 1);
       wave_lds_fence();
 #pragma unroll
       for (int j = 0; j < C; ++j) av[lane * C + j] = (float)nd[lane * C + j] + t_alpha[lane * C + j];
@@ -278,9 +285,8 @@ __global__ __launch_bounds__(256) void k_sample(SampleParams p) {
     float cinv[P];
 #pragma unroll
     for (int s = 0; s < P; ++s) {
-      const int64_t tp = t0 + s;
-      const int wp = (tp < t1) ? readlane_i(cw, s) : 0;
-      const int zp = (tp < t1) ? readlane_i(cz, s) : 0;
+      const int wp = (s < nt) ? readlane_i(cw, s) : 0;
+      const int zp = (s < nt) ? readlane_i(cz, s) : 0;
       load_row16<C>(rows[s], nw16 + (int64_t)wp * KP, lane);
       if (!FROZEN) {
         ccnt[s] = nw[(int64_t)wp * KP + zp];
@@ -288,15 +294,15 @@ __global__ __launch_bounds__(256) void k_sample(SampleParams p) {
       }
     }
 
-    for (int64_t tb = t0; tb < t1; tb += P) {
+    for (int tb = 0; tb < nt; tb += P) {
 #pragma unroll
       for (int s = 0; s < P; ++s) {
-        const int64_t t = tb + s;
-        if (t >= t1) break;
-        int idx = (int)(t - cbase);
+        const int t = tb + s;
+        if (t >= nt) break;
+        int idx = t - cbase;
         if (idx == 64) {
           // chunk switch: publish the finished chunk's new z, shift
-          p.z[cbase + lane] = cn;
+          zr[cbase + lane] = cn;
           cbase += 64;
           idx = 0;
           cw = w1;
@@ -306,10 +312,10 @@ __global__ __launch_bounds__(256) void k_sample(SampleParams p) {
           z1 = z2;
           f1 = (int)wide_of[w1];
           cn = cz;
-          cu = u01(draw_u32((uint64_t)(p.token_base + cbase + lane), p.c2, p.c3, p.k0, p.k1));
-          if (cbase + 128 + lane < t1) {
-            w2 = p.words[cbase + 128 + lane];
-            z2 = p.z[cbase + 128 + lane];
+          cu = u01(draw_u32(gbase + (uint64_t)(cbase + lane), p.c2, p.c3, p.k0, p.k1));
+          if (cbase + 128 + lane < nt) {
+            w2 = wrd[cbase + 128 + lane];
+            z2 = zr[cbase + 128 + lane];
           }
         }
         if (t == doc_end) {
@@ -317,9 +323,9 @@ __global__ __launch_bounds__(256) void k_sample(SampleParams p) {
           for (int j = 0; j < C; ++j) nd[lane * C + j] = 0;
           wave_lds_fence();
           ++doc;
-          while (p.doc_off[doc + 1] <= t) ++doc;
-          doc_end = p.doc_off[doc + 1];
-          for (int64_t i = t + lane; i < doc_end; i += 64) atomicAdd(&nd[p.z[i]], 1);
+          while (p.doc_off[doc + 1] - t0 <= t) ++doc;
+          doc_end = (int)(p.doc_off[doc + 1] - t0);
+          for (int i = t + lane; i < doc_end; i += 64) atomicAdd(&nd[zr[i]], 1);
           wave_lds_fence();
 #pragma unroll
           for (int j = 0; j < C; ++j) av[lane * C + j] = (float)nd[lane * C + j] + t_alpha[lane * C + j];
@@ -347,8 +353,9 @@ __global__ __launch_bounds__(256) void k_sample(SampleParams p) {
         const float bc = FROZEN ? 0.0f : ((float)(ccnt[s] - 1) + beta) * cinv[s];
         const bool own_old = (lane == lo);
 
-        // word factors b = (float(c) + beta) * inv; rows with a count > 65535
-        // come from the int32 row instead (rare: uniform branch, not prefetched)
+        // word factors b = (float(c) + beta) * inv (packed fp32 pairs, each
+        // half an ordinary IEEE add / mul); rows with a count > 65535 come
+        // from the int32 row instead (rare: uniform branch, not prefetched)
         int32_t cfull[C];
         if (wide) {
           const int32_t* wr = nw + (int64_t)w * KP + lane * C;
@@ -358,14 +365,25 @@ __global__ __launch_bounds__(256) void k_sample(SampleParams p) {
 #pragma unroll
           for (int j = 0; j < C; ++j) cfull[j] = row16_count<C>(rows[s], j);
         }
+        float bw[C];
+        if constexpr (C >= 2) {
+#pragma unroll
+          for (int j = 0; j < C; j += 2) {
+            pkf32 c2v = {(float)cfull[j], (float)cfull[j + 1]};
+            const pkf32 b2 = (c2v + beta) * (pkf32){inv_r[j], inv_r[j + 1]};
+            bw[j] = b2.x;
+            bw[j + 1] = b2.y;
+          }
+        } else {
+          bw[0] = ((float)cfull[0] + beta) * inv_r[0];
+        }
 
         // lane-serial fma prefix (the z_old element of lane lo uses bc)
         float S[C];
         float acc = 0.0f;
 #pragma unroll
         for (int j = 0; j < C; ++j) {
-          const float bj = ((float)cfull[j] + beta) * inv_r[j];
-          const float b = (!FROZEN && j == jo && own_old) ? bc : bj;
+          const float b = (!FROZEN && j == jo && own_old) ? bc : bw[j];
           acc = __builtin_fmaf(a[j], b, acc);
           S[j] = acc;
         }
@@ -377,9 +395,11 @@ __global__ __launch_bounds__(256) void k_sample(SampleParams p) {
         const uint64_t m = __ballot((T > thr) && (lane <= last_lane));
         const int lstar = m ? (int)__builtin_ctzll(m) : last_lane;
         const float E = lstar > 0 ? readlane_f(T, lstar - 1) : 0.0f;
-        int cnt = 0;
+        // every lane counts its own prefix against lane lstar's E; lstar's count is the one used
+        int cl = 0;
 #pragma unroll
-        for (int j = 0; j < C; ++j) cnt += (int)((__ballot(E + S[j] <= thr) >> lstar) & 1ull);
+        for (int j = 0; j < C; ++j) cl += (E + S[j] <= thr) ? 1 : 0;
+        const int cnt = readlane_i(cl, lstar);
         const int jsel = cnt < C ? cnt : (lstar < last_lane ? C - 1 : last_j_tail);
         const int kn = lstar * C + jsel;
 
@@ -404,9 +424,9 @@ __global__ __launch_bounds__(256) void k_sample(SampleParams p) {
         }
 
         // keep the pipeline full: token t+P
-        const int64_t tp = t + P;
-        if (tp < t1) {
-          const int pidx = (int)(tp - cbase);
+        const int tp = t + P;
+        if (tp < nt) {
+          const int pidx = tp - cbase;
           const int wp = pidx < 64 ? readlane_i(cw, pidx) : readlane_i(w1, pidx - 64);
           load_row16<C>(rows[s], nw16 + (int64_t)wp * KP, lane);
           if (!FROZEN) {
@@ -417,7 +437,7 @@ __global__ __launch_bounds__(256) void k_sample(SampleParams p) {
         }
       }
     }
-    if (cbase + lane < t1) p.z[cbase + lane] = cn;
+    if (cbase + lane < nt) zr[cbase + lane] = cn;
 #pragma unroll
     for (int j = 0; j < C; ++j) nd[lane * C + j] = 0;
     wave_lds_fence();
