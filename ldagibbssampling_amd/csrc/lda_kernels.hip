@@ -208,18 +208,24 @@ __global__ __launch_bounds__(256) void k_sample(SampleParams p) {
   extern __shared__ __attribute__((aligned(16))) int32_t smem[];
   constexpr int KP = C * 64;
   constexpr int H = (C + 1) / 2;                     // dwords of a 16-bit row per lane
+  // inv_m1 as a per-block LDS table for C <= 8; for C = 16 the extra table
+  // would cost a block per CU, so inv_m1[z_old] is prefetched from memory
+  constexpr bool kInvLds = C <= 8;
+  constexpr int TB = kInvLds ? 3 : 2;                // per-block tables before the per-wave area
   const int lane = threadIdx.x & 63;
   const int wid = threadIdx.x >> 6;
   float* t_alpha = reinterpret_cast<float*>(smem);   // [KP] per block
   int32_t* bsum = smem + KP;                         // [KP] per-block nwsum delta
-  int32_t* nd = smem + 2 * KP + wid * 2 * KP;        // [KP] per-wave live doc counts
+  float* t_invm1 = reinterpret_cast<float*>(smem + 2 * KP);  // [KP] per block (kInvLds)
+  int32_t* nd = smem + TB * KP + wid * 2 * KP;       // [KP] per-wave live doc counts
   float* av = reinterpret_cast<float*>(nd + KP);     // [KP] per-wave a_k = float(nd_k) + alpha_k
 
   for (int i = threadIdx.x; i < KP; i += 256) {
     t_alpha[i] = p.alpha[i];
     bsum[i] = 0;
+    if (kInvLds) t_invm1[i] = FROZEN ? 0.0f : p.inv_m1[i];
   }
-  for (int i = threadIdx.x; i < 8 * KP; i += 256) smem[2 * KP + i] = 0;
+  for (int i = threadIdx.x; i < 8 * KP; i += 256) smem[TB * KP + i] = 0;
   __syncthreads();
 
   float inv_r[C];
@@ -279,19 +285,14 @@ __global__ __launch_bounds__(256) void k_sample(SampleParams p) {
       wave_lds_fence();
     }
 
-    // --- prime the pipeline: 16-bit rows (+ z_old count and inv_m1) of P tokens
+    // --- prime the pipeline: 16-bit rows of the next P tokens
     uint32_t rows[P][H];
-    int ccnt[P];
-    float cinv[P];
+    float cinv_r[P];
 #pragma unroll
     for (int s = 0; s < P; ++s) {
       const int wp = (s < nt) ? readlane_i(cw, s) : 0;
-      const int zp = (s < nt) ? readlane_i(cz, s) : 0;
       load_row16<C>(rows[s], nw16 + (int64_t)wp * KP, lane);
-      if (!FROZEN) {
-        ccnt[s] = nw[(int64_t)wp * KP + zp];
-        cinv[s] = inv_m1[zp];
-      }
+      if (!FROZEN && !kInvLds) cinv_r[s] = inv_m1[(s < nt) ? readlane_i(cz, s) : 0];
     }
 
     for (int tb = 0; tb < nt; tb += P) {
@@ -350,7 +351,7 @@ __global__ __launch_bounds__(256) void k_sample(SampleParams p) {
         }
         float a[C];
         load_lds_f<C>(a, av + lane * C);
-        const float bc = FROZEN ? 0.0f : ((float)(ccnt[s] - 1) + beta) * cinv[s];
+        const float cinv = FROZEN ? 0.0f : (kInvLds ? t_invm1[zo] : cinv_r[s]);
         const bool own_old = (lane == lo);
 
         // word factors b = (float(c) + beta) * inv (packed fp32 pairs, each
@@ -365,6 +366,12 @@ __global__ __launch_bounds__(256) void k_sample(SampleParams p) {
 #pragma unroll
           for (int j = 0; j < C; ++j) cfull[j] = row16_count<C>(rows[s], j);
         }
+        // the own-token-corrected factor of z_old, from lane lo's own row
+        // element (exact: a 16-bit row holds every count below 65536)
+        int32_t c_old = cfull[0];
+#pragma unroll
+        for (int j = 1; j < C; ++j) c_old = (j == jo) ? cfull[j] : c_old;
+        const float bc = FROZEN ? 0.0f : ((float)(c_old - 1) + beta) * cinv;
         float bw[C];
         if constexpr (C >= 2) {
 #pragma unroll
@@ -429,11 +436,8 @@ __global__ __launch_bounds__(256) void k_sample(SampleParams p) {
           const int pidx = tp - cbase;
           const int wp = pidx < 64 ? readlane_i(cw, pidx) : readlane_i(w1, pidx - 64);
           load_row16<C>(rows[s], nw16 + (int64_t)wp * KP, lane);
-          if (!FROZEN) {
-            const int zp = pidx < 64 ? readlane_i(cz, pidx) : readlane_i(z1, pidx - 64);
-            ccnt[s] = nw[(int64_t)wp * KP + zp];
-            cinv[s] = inv_m1[zp];
-          }
+          if (!FROZEN && !kInvLds)
+            cinv_r[s] = inv_m1[pidx < 64 ? readlane_i(cz, pidx) : readlane_i(z1, pidx - 64)];
         }
       }
     }
@@ -1461,9 +1465,11 @@ __global__ __launch_bounds__(256) void k_infer_init(const int32_t* __restrict__ 
 }
 
 // ------------------------------------------------------------- launchers
+template <int C>
+static constexpr size_t sample_lds() { return (C <= 8 ? 11 : 10) * 64 * C * sizeof(int32_t); }
 template <int C, int P, bool FROZEN>
 static hipError_t launch_sample_t(const SampleParams& p, int blocks, hipStream_t st) {
-  const size_t lds = 10 * 64 * C * sizeof(int32_t);
+  const size_t lds = sample_lds<C>();
   hipLaunchKernelGGL((k_sample<C, P, FROZEN>), dim3(blocks), dim3(256), lds, st, p);
   return hipGetLastError();
 }
@@ -1471,7 +1477,7 @@ static hipError_t launch_sample_t(const SampleParams& p, int blocks, hipStream_t
 template <int C, int P, bool FROZEN>
 static int occupancy_t() {
   int nb = 0;
-  const size_t lds = 10 * 64 * C * sizeof(int32_t);
+  const size_t lds = sample_lds<C>();
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_sample<C, P, FROZEN>, 256, lds) !=
       hipSuccess)
     return 1;
