@@ -98,11 +98,13 @@ SIGNATURES = {
 _lib = None
 
 
-def load(path: str = LIB_PATH):
-    """Load liblda_mi355x.so; raises if it is missing (no CPU fallback)."""
+def load(path: str | None = None):
+    """Load liblda_mi355x.so; raises if it is missing (no CPU fallback).
+    LDA_MI355X_LIB overrides the in-tree path (A/B runs of kernel variants)."""
     global _lib
     if _lib is not None:
         return _lib
+    path = path or os.environ.get("LDA_MI355X_LIB") or LIB_PATH
     if not os.path.exists(path):
         raise ImportError(
             f"{path} not found: build the HIP extension first "

@@ -15,9 +15,15 @@ constexpr uint32_t STREAM_INFER = 2u;
 // Row-prefetch depth of the sampler per C = Kp/64 (tokens in flight per wave).
 #define SAMPLE_P1 4
 #define SAMPLE_P2 4
+#ifndef SAMPLE_P4
 #define SAMPLE_P4 4
+#endif
+#ifndef SAMPLE_P8
 #define SAMPLE_P8 4
+#endif
+#ifndef SAMPLE_P16
 #define SAMPLE_P16 2
+#endif
 // sparse sampler: tokens in flight, 64-entry rounds prefetched per token
 #define SPARSE_P 4
 #define SPARSE_R0 2
