@@ -233,6 +233,9 @@ def main():
                 "measured_copy_gbs": copy_gbs,
                 "kernel_ms_timed_region": kern_ms,
                 "traffic": traffic_gb,
+                # the bandwidth the kernel really moves (PMC bytes / its time)
+                "traffic_gbs": (traffic_gb / (kern_ms * 1e-3)) if traffic_gb else None,
+                "traffic_frac": (traffic_gb / (kern_ms * 1e-3) / HBM_PEAK_GBS) if traffic_gb else None,
                 "traffic_unit": "GB per launch (rocprofv3 PMC, gfx950-corrected)",
                 "traffic_source": traffic_src,
                 "algorithmic_gb_per_launch": n_local * bpt / 1e9,
