@@ -155,7 +155,12 @@ def main():
     sampler = GibbsSampler(K, V, corpus.doc_off, corpus.words, np.full(K, alpha_sum / K), beta,
                            seed=1, device=local_rank, token_base=rank * n_local,
                            sampler=args.sampler)
-    stream = torch.cuda.current_stream()
+    # one non-default stream carries the sampler kernels and (as torch's
+    # current stream) orders the all-reduce behind them: no host sync per sweep.
+    # (handle 0 = the legacy default stream would mean "the context's own
+    # stream" to lda_set_stream, which the collective would not wait for)
+    stream = torch.cuda.Stream(device=local_rank)
+    torch.cuda.set_stream(stream)
     sampler.set_stream(stream.cuda_stream)
     # AD-LDA: sample; all-reduce (SUM) of every rank's int32 nw/nwsum delta; apply
     trainer = ADLDATrainer(sampler, sync_before_reduce=False)

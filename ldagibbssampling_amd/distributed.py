@@ -67,6 +67,22 @@ class ADLDATrainer:
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
         self._delta = engine.delta_tensor() if self.world > 1 else None
         self._initialised = False
+        if self.world > 1 and not sync_before_reduce:
+            self._check_stream_order()
+
+    def _check_stream_order(self):
+        """Without a host sync the collective is ordered behind the sampler
+        only if both run on torch's current stream, and that stream is a real
+        one (handle 0 would make lda_set_stream pick the context's own)."""
+        import torch
+        if not hasattr(self.engine, "stream_handle") or self._delta is None or \
+                self._delta.device.type != "cuda":
+            return
+        cur = torch.cuda.current_stream(self._delta.device).cuda_stream
+        if cur == 0 or self.engine.stream_handle() != cur:
+            raise ValueError("sync_before_reduce=False needs the engine on torch's current, "
+                             "non-default stream: torch.cuda.set_stream(s); "
+                             "engine.set_stream(s.cuda_stream)")
 
     def _reduce(self):
         if self.world > 1:

@@ -114,6 +114,12 @@ class GibbsSampler:
     def set_stream(self, stream_handle: int | None):
         capi.check(self._L.lda_set_stream(self._h, stream_handle), "lda_set_stream")
 
+    def stream_handle(self) -> int:
+        """The hipStream_t every call of this context is ordered on."""
+        h = C.c_void_p()
+        capi.check(self._L.lda_get_stream(self._h, C.byref(h)), "lda_get_stream")
+        return int(h.value or 0)
+
     def synchronize(self):
         capi.check(self._L.lda_synchronize(self._h), "lda_synchronize")
 

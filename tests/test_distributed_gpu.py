@@ -21,7 +21,7 @@ def _corpus():
                          min_len=0, max_len=300, seed=31)
 
 
-def _worker(rank, world, port, outdir):
+def _worker(rank, world, port, outdir, stream_ordered=False):
     sys.path.insert(0, ROOT)
     import torch
     import torch.distributed as dist
@@ -34,7 +34,22 @@ def _worker(rank, world, port, outdir):
     sh = shard_corpus(c.doc_off, c.words, world, rank)
     g = GibbsSampler(K, c.num_types, sh.doc_off, sh.words, 0.1, 0.01, seed=SEED,
                      token_base=sh.token_base)
-    tr = ADLDATrainer(g)
+    if stream_ordered:
+        # bench.py's arrangement: sampler and collective on one torch stream, no host sync
+        st = torch.cuda.Stream()
+        torch.cuda.set_stream(st)
+        g.set_stream(st.cuda_stream)
+        tr = ADLDATrainer(g, sync_before_reduce=False)
+        # the default stream is refused (handle 0 would not order the collective)
+        torch.cuda.set_stream(torch.cuda.default_stream())
+        try:
+            ADLDATrainer(g, sync_before_reduce=False)
+            raise AssertionError("default stream accepted")
+        except ValueError:
+            pass
+        torch.cuda.set_stream(st)
+    else:
+        tr = ADLDATrainer(g)
     tr.sweep(SWEEPS)
     ll = tr.log_likelihood()
     nw, nwsum, _, _ = g.counts()
@@ -44,7 +59,8 @@ def _worker(rank, world, port, outdir):
     dist.destroy_process_group()
 
 
-def test_two_ranks_one_gpu(oracle):
+@pytest.mark.parametrize("stream_ordered", [False, True])
+def test_two_ranks_one_gpu(oracle, stream_ordered):
     import socket
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
@@ -52,7 +68,8 @@ def test_two_ranks_one_gpu(oracle):
     s.close()
     world = 2
     with tempfile.TemporaryDirectory() as d:
-        mp.start_processes(_worker, args=(world, port, d), nprocs=world, start_method="spawn")
+        mp.start_processes(_worker, args=(world, port, d, stream_ordered), nprocs=world,
+                           start_method="spawn")
         res = [np.load(os.path.join(d, f"r{r}.npz")) for r in range(world)]
     c = _corpus()
     o = oracle.ExactSampler(K, c.num_types, c.doc_off, c.words, 0.1, 0.01, SEED)
