@@ -122,6 +122,9 @@ def main():
     ap.add_argument("--burnin", type=int, default=0,
                     help="extra untimed sweeps before the warm-up (steady-state measurement)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
+                    help="collective backend for N > 1 (nccl = RCCL over xGMI; gloo only to "
+                         "rehearse several ranks on one GPU)")
     ap.add_argument("--cpu-budget", type=float, default=15.0)
     args = ap.parse_args()
 
@@ -133,9 +136,14 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
-    torch.cuda.set_device(local_rank)
+    ndev = torch.cuda.device_count()
+    device = local_rank % ndev                 # == local_rank with one GPU per rank
+    torch.cuda.set_device(device)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", device))
+        else:
+            dist.init_process_group("gloo")
 
     from ldagibbssampling_amd.corpus import synthetic_lda_torch
     from ldagibbssampling_amd.distributed import ADLDATrainer
@@ -149,17 +157,17 @@ def main():
     alpha_sum, beta = 0.1 * K, 0.01
     t_gen = time.perf_counter()
     corpus = synthetic_lda_torch(docs, V, K, doc_len=L, seed=20261015 + rank,
-                                 device=f"cuda:{local_rank}")
+                                 device=f"cuda:{device}")
     t_gen = time.perf_counter() - t_gen
     n_local = corpus.num_tokens
     sampler = GibbsSampler(K, V, corpus.doc_off, corpus.words, np.full(K, alpha_sum / K), beta,
-                           seed=1, device=local_rank, token_base=rank * n_local,
+                           seed=1, device=device, token_base=rank * n_local,
                            sampler=args.sampler)
     # one non-default stream carries the sampler kernels and (as torch's
     # current stream) orders the all-reduce behind them: no host sync per sweep.
     # (handle 0 = the legacy default stream would mean "the context's own
     # stream" to lda_set_stream, which the collective would not wait for)
-    stream = torch.cuda.Stream(device=local_rank)
+    stream = torch.cuda.Stream(device=device)
     torch.cuda.set_stream(stream)
     sampler.set_stream(stream.cuda_stream)
     # AD-LDA: sample; all-reduce (SUM) of every rank's int32 nw/nwsum delta; apply
@@ -189,9 +197,9 @@ def main():
     ks = sampler.sample_times(args.steps)
     assert len(ks) == min(args.steps, 256)
     kern_ms = float(np.mean(ks))
-    copy_gbs = stream_copy_gbs(local_rank) if rank == 0 else None
+    copy_gbs = stream_copy_gbs(device) if rank == 0 else None
 
-    t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local_rank}")
+    t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{device}")
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = float(t.item())
@@ -227,7 +235,8 @@ def main():
                 "num_topics": K,
                 "alpha_sum": alpha_sum,
                 "beta": beta,
-                "parallelism": f"dp{world} (AD-LDA doc shards, RCCL all-reduce of int32 delta)",
+                "parallelism": f"dp{world} (AD-LDA doc shards, "
+                               f"{'RCCL' if args.backend == 'nccl' else 'gloo'} all-reduce of int32 delta)",
             },
             "roofline": {
                 "bound": "hbm",
