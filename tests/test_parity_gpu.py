@@ -294,3 +294,22 @@ def test_wide_rows_escape(oracle, kind):
     o.sweep(2)
     assert g.counts()[0].max() > 65535
     _assert_same_state(g, o, with_nd=False)
+
+
+@pytest.mark.parametrize("K", [20, 512, 1024])
+def test_dense_escaped_counts(oracle, K):
+    """Counts from 255 up: the dense sampler's 8-bit rows mark them 255 and
+    the lane reads its exact int32 slice (mixed escaped / plain lanes)."""
+    from ldagibbssampling_amd.corpus import Corpus
+    D, L = 60, 500
+    rng = np.random.default_rng(K)
+    words = np.where(rng.random(D * L) < 0.5, rng.integers(0, 3, D * L),
+                     rng.integers(3, 200, D * L)).astype(np.int32)
+    c = Corpus(np.arange(D + 1, dtype=np.int64) * L, words, 200)
+    z0 = np.where(rng.random(D * L) < 0.7, 7, rng.integers(0, K, D * L)).astype(np.int32)
+    g, o = _pair(oracle, c, K, np.full(K, 0.1), 0.01, seed=K + 5, z_init=z0)
+    g.sweep(3)
+    o.sweep(3)
+    nw = g.counts()[0]
+    assert (nw >= 255).sum() >= 1 and ((nw > 0) & (nw < 255)).sum() > 100
+    _assert_same_state(g, o)
