@@ -125,34 +125,14 @@ __device__ __forceinline__ void load_row(int32_t (&r)[C], const int32_t* __restr
 // One wavefront walks one work range (a run of whole documents) at a time,
 // pulling ranges from a device queue.  The wave keeps a 64-token chunk of the
 // token stream in registers (lane i <-> token i of the chunk: word, old z,
-// Philox uniform, new z), the next chunk's words/z one chunk ahead, and for
-// the next P tokens: the word's row of Bt = (float(nw) + beta) * inv (built
-// per sweep by k_build_btable), the int count nw[w][z_old] and inv_m1[z_old]
-// (the snapshot makes all of them independent of the draws, so they pipeline
-// across tokens and documents).  Per lane and topic the draw is one fma:
-//   S_j = fma(a_j, b_j, S_{j-1}),  a_j = float(nd_j) + alpha_j kept in
-// registers and refreshed only at the topic that changed; the z_old element
-// of lane z_old/C uses the corrected b computed once per token.
-
-template <int C>
-__device__ __forceinline__ void load_brow(float (&r)[C], const float* __restrict__ p) {
-  if constexpr (C >= 4) {
-#pragma unroll
-    for (int q = 0; q < C / 4; ++q) {
-      const float4 v = reinterpret_cast<const float4*>(p)[q];
-      r[4 * q + 0] = v.x;
-      r[4 * q + 1] = v.y;
-      r[4 * q + 2] = v.z;
-      r[4 * q + 3] = v.w;
-    }
-  } else if constexpr (C == 2) {
-    const float2 v = *reinterpret_cast<const float2*>(p);
-    r[0] = v.x;
-    r[1] = v.y;
-  } else {
-    r[0] = p[0];
-  }
-}
+// Philox uniform, new z), the next two chunks' words/z ahead of it, and the
+// 16-bit rows of nw for the next P tokens in flight (the snapshot makes them
+// independent of the draws, so they pipeline across tokens and documents).
+// Per lane and topic the draw is one fma:
+//   S_j = fma(a_j, b_j, S_{j-1}),  a_j = float(nd_j) + alpha_j (LDS, per wave)
+//   b_j = (float(c_j) + beta) * inv_j  (c_j from the row; packed fp32 pairs)
+// and the z_old element of lane z_old/C uses the own-token-corrected factor
+// ((float)(c_zold - 1) + beta) * inv_m1[z_old], c_zold taken from the row.
 
 template <int C>
 __device__ __forceinline__ void load_lds_f(float (&r)[C], const float* p) {
