@@ -80,33 +80,53 @@ def stream_copy_gbs(device: int, nbytes: int = 2 << 30, reps: int = 10) -> float
     return gbs
 
 
+def _cpu_model() -> str:
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return platform.processor() or platform.machine()
+
+
 def cpu_baseline(corpus, K, alpha_sum, beta, budget_s=15.0, threads=4):
     """cpu_mallet (oracle/, the Mallet 2.0.7 SparseLDA restatement) timed on a
-    bounded sample of the same workload on this host's cores."""
+    bounded sample of the same workload on this host's cores: `threads`
+    workers (the reference's setNumThreads(4)) for ~budget_s, plus a short
+    single-thread run (T = 1 and T = threads)."""
     from oracle import oracle as O
     O.build()
     ndocs = min(corpus.num_docs, 20_000)
     sub = corpus.subset(np.arange(ndocs))
-    m = O.MalletModel(K, alpha_sum, beta, corpus.num_types, sub.doc_off, sub.words, seed=1,
-                      num_threads=threads)
-    m.estimate(2)                                    # warm-up sweeps
-    t0 = time.perf_counter()
-    sweeps = 0
-    while True:
-        m.estimate(1)
-        sweeps += 1
-        if time.perf_counter() - t0 >= budget_s or sweeps >= 50:
-            break
-    dt = time.perf_counter() - t0
+
+    def timed(T, budget, max_sweeps):
+        m = O.MalletModel(K, alpha_sum, beta, corpus.num_types, sub.doc_off, sub.words, seed=1,
+                          num_threads=T)
+        m.estimate(2)                                    # warm-up sweeps
+        t0 = time.perf_counter()
+        sweeps = 0
+        while True:
+            m.estimate(1)
+            sweeps += 1
+            if time.perf_counter() - t0 >= budget or sweeps >= max_sweeps:
+                break
+        return sub.num_tokens * sweeps / (time.perf_counter() - t0), sweeps
+
+    v, sweeps = timed(threads, budget_s, 50)
+    v1, sweeps1 = timed(1, budget_s / 3, 20)
     return {
-        "value": sub.num_tokens * sweeps / dt,
+        "value": v,
         "unit": "tokens/s",
         "cores": threads,
         "kind": "port",
+        "t1_value": v1,
         "sample": (f"cpu_mallet (Mallet 2.0.7 SparseLDA restatement, oracle/lda_oracle.c), "
                    f"{threads} threads (= setNumThreads(4), src/cmu_ron/TrainAndPredict.java:164), "
                    f"first {ndocs} docs ({sub.num_tokens} tokens) of this workload, "
-                   f"{sweeps} timed sweeps after 2 warm-up, host {platform.processor() or platform.machine()}"),
+                   f"{sweeps} timed sweeps after 2 warm-up; t1_value: 1 thread, {sweeps1} sweeps; "
+                   f"host {_cpu_model()}, {os.cpu_count()} logical CPUs visible"),
     }
 
 
