@@ -25,7 +25,9 @@ constexpr uint32_t STREAM_INFER = 2u;
 #define SAMPLE_P16 2
 #endif
 // sparse sampler: tokens in flight, 64-entry rounds prefetched per token
+#ifndef SPARSE_P
 #define SPARSE_P 4
+#endif
 #define SPARSE_R0 2
 
 struct SampleParams {

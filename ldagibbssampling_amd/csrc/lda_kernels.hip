@@ -800,8 +800,14 @@ __global__ __launch_bounds__(256) void k_sample_sparse(SampleParams p) {
 // 64 entries (the first SB_RB of the next P tokens prefetched, the rest in
 // batches); the selected lane's rounds are re-walked one per lane, followed
 // by a serial readlane chain that reproduces the sum pass's order.
-#define SB_RB 2
-#define SB_BATCH 4
+// prefetched rounds per upcoming token / loads per streamed batch (A/B on C5:
+// 8/8 vs 2/4 is +13% near init, +15% after 30 sweeps; 127 VGPRs, 4 waves/SIMD)
+#ifndef SB_RB
+#define SB_RB 8
+#endif
+#ifndef SB_BATCH
+#define SB_BATCH 8
+#endif
 template <int C>
 constexpr int sb_waves() { return 16; }
 
