@@ -38,6 +38,17 @@ CASES = {
                                           max_len=300, seed=3), 128, 0.1, 0.01, 13, (1, 10)),
     "k1000_wide": (lambda: synthetic_lda(40, 300, 1000, doc_len=None, mean_len=90, min_len=1,
                                          max_len=250, seed=4), 1000, 0.05, 0.01, 14, (1, 3)),
+    # the sparse draw (LDA_SAMPLER_SPARSE): C <= 16 fma-chain doc partials and
+    # C = 32 / 64 16-lane row-scan group partials (k_sample_sparse_big)
+    "k128_sparse": (lambda: synthetic_lda(100, 400, 128, doc_len=None, mean_len=70, min_len=0,
+                                          max_len=300, seed=7), 128, 0.1, 0.01, 17, (1, 10),
+                    "sparse"),
+    "k2048_sparse": (lambda: synthetic_lda(60, 500, 64, doc_len=None, mean_len=120, min_len=1,
+                                           max_len=400, seed=8), 2048, 0.02, 0.01, 18, (1, 5),
+                     "sparse"),
+    "k4096_sparse": (lambda: synthetic_lda(40, 300, 64, doc_len=None, mean_len=150, min_len=1,
+                                           max_len=500, seed=9), 4096, 0.01, 0.05, 19, (1, 4),
+                     "sparse"),
 }
 
 
@@ -46,12 +57,13 @@ def sha(a):
 
 
 def exact_case(name):
-    build, K, alpha, beta, seed, checkpoints = CASES[name]
+    build, K, alpha, beta, seed, checkpoints = CASES[name][:6]
+    kind = CASES[name][6] if len(CASES[name]) > 6 else "dense"
     c = build()
-    o = O.ExactSampler(K, c.num_types, c.doc_off, c.words, alpha, beta, seed)
+    o = O.ExactSampler(K, c.num_types, c.doc_off, c.words, alpha, beta, seed, kind=kind)
     o.apply()
     out = {"doc_off": c.doc_off, "words": c.words, "K": K, "V": c.num_types, "alpha": alpha,
-           "beta": beta, "seed": seed, "checkpoints": np.array(checkpoints)}
+           "beta": beta, "seed": seed, "checkpoints": np.array(checkpoints), "kind": kind}
     out["z_0"] = o.z().astype(np.int16 if K < 32768 else np.int32)
     done = 0
     meta = {}
@@ -84,6 +96,41 @@ def mallet_traces():
         json.dump(res, f, indent=1)
 
 
+def hyper():
+    """Dirichlet estimators on fixed histograms, and the Mallet restatement's
+    optimisation schedule (optimizeInterval 10, burn-in 20) on a small corpus."""
+    rng = np.random.default_rng(10)
+    hist = rng.integers(0, 40, size=(12, 61)).astype(np.int32)
+    hist[:, 0] = 0
+    hist[3] = 0                                     # a topic in no document
+    lens = rng.integers(0, 30, size=61).astype(np.int32)
+    lens[0] = 0
+    a0 = rng.uniform(0.05, 1.0, size=12)
+    a1, s1 = O.learn_parameters(a0, hist, lens, 1.001, 1.0, 1)
+    a5, s5 = O.learn_parameters(a0, hist, lens, 1.001, 1.0, 5)
+    counts = np.bincount(rng.integers(1, 200, size=5000), minlength=201).astype(np.int32)
+    sizes = np.zeros(3001, np.int32)
+    sizes[rng.integers(1, 3000, size=40)] += 1
+    sym = O.learn_symmetric_concentration(counts, sizes, 700, 7.0)
+    c = synthetic_changelists(300, 600, seed=5)
+    m = O.MalletModel(20, 10.0, 0.01, c.num_types, c.doc_off, c.words, seed=4, num_threads=2)
+    m.set_optimize(10, burnin=20)
+    m.estimate(60)
+    a_m, b_m = m.hyper()
+    res = {"learn_parameters": {"hist": hist.tolist(), "lens": lens.tolist(), "alpha0": a0.tolist(),
+                                "alpha_1": a1.tolist(), "sum_1": s1, "alpha_5": a5.tolist(),
+                                "sum_5": s5},
+           "learn_symmetric_concentration": {"counts": counts.tolist(), "sizes": sizes.tolist(),
+                                             "dims": 700, "value0": 7.0, "value": sym},
+           "mallet_optimised": {"corpus": "synthetic_changelists(300, 600, seed=5)", "K": 20,
+                                "alpha_sum": 10.0, "beta": 0.01, "seed": 4, "threads": 2,
+                                "optimize_interval": 10, "burnin": 20, "iterations": 60,
+                                "alpha": a_m.tolist(), "beta_out": b_m,
+                                "z_sha256": sha(m.z())}}
+    with open(os.path.join(HERE, "hyper.json"), "w") as f:
+        json.dump(res, f)
+
+
 def inverse_docs():
     c = synthetic_changelists(50, 300, seed=6)
     # mixed case on purpose: the pipeline lower-cases (InstanceImporter.java:35)
@@ -97,9 +144,16 @@ def inverse_docs():
 
 
 if __name__ == "__main__":
+    # python tests/golden/make_golden.py [case | mallet | hyper | inverse ...]  (default: all)
     O.build()
+    want = set(sys.argv[1:])
     for n in CASES:
-        exact_case(n)
-    mallet_traces()
-    inverse_docs()
+        if not want or n in want:
+            exact_case(n)
+    if not want or "mallet" in want:
+        mallet_traces()
+    if not want or "hyper" in want:
+        hyper()
+    if not want or "inverse" in want:
+        inverse_docs()
     print("golden fixtures written to", HERE)
