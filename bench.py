@@ -176,8 +176,10 @@ def main():
     docs = args.docs or cfg["docs"]
     alpha_sum, beta = 0.1 * K, 0.01
     t_gen = time.perf_counter()
-    corpus = synthetic_lda_torch(docs, V, K, doc_len=L, seed=20261015 + rank,
-                                 device=f"cuda:{device}")
+    # one corpus: the topics (phi) are shared by every shard, the documents are
+    # drawn per rank (rank 0 == the N=1 workload)
+    corpus = synthetic_lda_torch(docs, V, K, doc_len=L, seed=20261015,
+                                 doc_seed=20261015 + rank, device=f"cuda:{device}")
     t_gen = time.perf_counter() - t_gen
     n_local = corpus.num_tokens
     sampler = GibbsSampler(K, V, corpus.doc_off, corpus.words, np.full(K, alpha_sum / K), beta,

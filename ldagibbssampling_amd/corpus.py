@@ -180,9 +180,11 @@ def document_completion_split(corpus: Corpus):
 
 def synthetic_lda_torch(num_docs: int, num_types: int, num_topics: int, doc_len: int = 200,
                         seed: int = 20261015, device: str = "cuda", phi_conc: float = 0.01,
-                        theta_conc: float = 0.1) -> Corpus:
+                        theta_conc: float = 0.1, doc_seed: int | None = None) -> Corpus:
     """The same generative process as synthetic_lda, drawn on the GPU with
-    torch (plumbing for benchmark-sized corpora: 1e8+ tokens in seconds)."""
+    torch (plumbing for benchmark-sized corpora: 1e8+ tokens in seconds).
+    `seed` draws the topics (phi); `doc_seed` (default: seed) the documents,
+    so that the shards of one corpus share its topics."""
     import torch
 
     kt = min(num_topics, 100)
@@ -194,6 +196,8 @@ def synthetic_lda_torch(num_docs: int, num_types: int, num_topics: int, doc_len:
         phi = phi / phi.sum(1, keepdim=True)
         cdf = torch.cumsum(phi, 1)
         cdf = cdf / cdf[:, -1:]
+        if doc_seed is not None and doc_seed != seed:
+            torch.manual_seed(doc_seed)
         theta = torch._standard_gamma(torch.full((num_docs, kt), theta_conc, dtype=torch.float32,
                                                  device=dev))
         theta = theta / theta.sum(1, keepdim=True).clamp_min(1e-30)
