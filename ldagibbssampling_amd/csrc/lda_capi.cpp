@@ -102,7 +102,7 @@ struct lda_ctx {
   bool pending = true;
   int cus = 256;
   int sampler = LDA_SAMPLER_DENSE;
-  int sample_blocks = 0, sample_blocks_frozen = 0;
+  int sample_blocks = 0, sample_blocks_frozen = 0, waves_per_block = 4;
   // sparse rows of the snapshot (LDA_SAMPLER_SPARSE)
   uint32_t* ent = nullptr;
   int64_t* row_off = nullptr;
@@ -317,7 +317,8 @@ lda_status lda_create(lda_ctx** out, const lda_config* cfg, const int64_t* doc_o
     c->sample_blocks = lda::sample_blocks_per_cu(c->C, false) * c->cus;
     c->sample_blocks_frozen = lda::sample_blocks_per_cu(c->C, true) * c->cus;
   }
-  const int64_t waves = (int64_t)c->sample_blocks * 4;
+  c->waves_per_block = lda::sample_waves_per_block(c->C, c->sampler == LDA_SAMPLER_SPARSE);
+  const int64_t waves = (int64_t)c->sample_blocks * c->waves_per_block;
   int64_t tpr = cfg->tokens_per_range;
   if (tpr <= 0) tpr = std::max<int64_t>(256, std::min<int64_t>(65536, N / std::max<int64_t>(1, waves * 8)));
   c->tokens_per_range = tpr;
@@ -424,7 +425,8 @@ lda_status lda_sample(lda_ctx* c) {
   if (c->N > 0) {
     HIP_TRY(hipMemsetAsync(c->queue, 0, sizeof(int32_t), c->stream));
     const lda::SampleParams p = c->params(false);
-    const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>(c->sample_blocks, (c->R + 3) / 4));
+    const int64_t wpb = c->waves_per_block;
+    const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>(c->sample_blocks, (c->R + wpb - 1) / wpb));
     const int slot = (int)(c->launches % lda_ctx::LDA_TIME_RING);
     HIP_TRY(hipEventRecord(c->ev0[slot], c->stream));
     if (c->sampler == LDA_SAMPLER_SPARSE)
@@ -451,7 +453,8 @@ lda_status lda_debug_sample_trace(lda_ctx* c, float* host_trace) {
   hipError_t e = hipMemsetAsync(c->queue, 0, sizeof(int32_t), c->stream);
   lda::SampleParams p = c->params(false);
   p.trace = tr;
-  const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>(c->sample_blocks, (c->R + 3) / 4));
+  const int64_t wpb = c->waves_per_block;
+  const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>(c->sample_blocks, (c->R + wpb - 1) / wpb));
   if (e == hipSuccess && c->N > 0) e = lda::launch_sample_sparse(c->C, false, p, blocks, c->stream);
   if (e == hipSuccess) e = hipMemcpyAsync(host_trace, tr, sizeof(float) * 8 * c->N, hipMemcpyDeviceToHost, c->stream);
   if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
@@ -693,7 +696,7 @@ lda_status lda_infer(lda_ctx* c, int64_t Dh, const int64_t* doc_off, const int32
   HIP_TRY(hipSetDevice(c->device));
   int32_t *dw = nullptr, *dz = nullptr, *acc = nullptr, *q = nullptr;
   int64_t *doff = nullptr, *drange = nullptr;
-  std::vector<int64_t> ranges = make_ranges(off, std::max<int64_t>(256, std::min<int64_t>(c->tokens_per_range, N / std::max<int64_t>(1, (int64_t)c->sample_blocks_frozen * 32))));
+  std::vector<int64_t> ranges = make_ranges(off, std::max<int64_t>(256, std::min<int64_t>(c->tokens_per_range, N / std::max<int64_t>(1, (int64_t)c->sample_blocks_frozen * c->waves_per_block * 8))));
   const int64_t R = (int64_t)ranges.size() - 1;
   hipError_t e = hipSuccess;
   auto chk = [&](hipError_t x) {
@@ -724,7 +727,8 @@ lda_status lda_infer(lda_ctx* c, int64_t Dh, const int64_t* doc_off, const int32
   p.k0 = (uint32_t)seed;
   p.k1 = (uint32_t)(seed >> 32);
   p.c3 = lda::STREAM_INFER;
-  const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>(c->sample_blocks_frozen, (R + 3) / 4));
+  const int64_t wpb = c->waves_per_block;
+  const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>(c->sample_blocks_frozen, (R + wpb - 1) / wpb));
   for (int32_t it = 1; it <= n_iter && e == hipSuccess && N > 0; ++it) {
     p.c2 = (uint32_t)(it - 1);
     chk(hipMemsetAsync(q, 0, sizeof(int32_t), c->stream));

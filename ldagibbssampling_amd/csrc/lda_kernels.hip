@@ -1571,6 +1571,12 @@ int sample_sparse_blocks_per_cu(int C, bool frozen) {
   return frozen ? occupancy_sparse_c<true>(C) : occupancy_sparse_c<false>(C);
 }
 
+int sample_waves_per_block(int C, bool sparse) {
+  if (sparse && C == 32) return sb_waves<32>();
+  if (sparse && C == 64) return sb_waves<64>();
+  return 4;
+}
+
 hipError_t launch_row_caps(const int32_t* nw, int64_t V, int32_t Kp, int32_t* caps, hipStream_t st) {
   if (V <= 0) return hipSuccess;
   const int blocks = (int)std::min<int64_t>((V + 3) / 4, 8192);

@@ -1,5 +1,6 @@
 # A/B: bench for the in-tree library and each variants/*/ library (CFG, BURNIN env)
 set -o pipefail
+shopt -s nullglob
 cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out
 CFG=${CFG:-c4}
