@@ -142,6 +142,8 @@ def main():
     ap.add_argument("--burnin", type=int, default=0,
                     help="extra untimed sweeps before the warm-up (steady-state measurement)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--tokens-per-range", type=int, default=0,
+                    help="work-queue granule (0 = the library's default)")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="collective backend for N > 1 (nccl = RCCL over xGMI; gloo only to "
                          "rehearse several ranks on one GPU)")
@@ -184,7 +186,7 @@ def main():
     n_local = corpus.num_tokens
     sampler = GibbsSampler(K, V, corpus.doc_off, corpus.words, np.full(K, alpha_sum / K), beta,
                            seed=1, device=device, token_base=rank * n_local,
-                           sampler=args.sampler)
+                           tokens_per_range=args.tokens_per_range, sampler=args.sampler)
     # one non-default stream carries the sampler kernels and (as torch's
     # current stream) orders the all-reduce behind them: no host sync per sweep.
     # (handle 0 = the legacy default stream would mean "the context's own
