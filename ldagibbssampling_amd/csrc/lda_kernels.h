@@ -19,7 +19,7 @@ constexpr uint32_t STREAM_INFER = 2u;
 #define SAMPLE_P4 4
 #endif
 #ifndef SAMPLE_P8
-#define SAMPLE_P8 4
+#define SAMPLE_P8 2
 #endif
 #ifndef SAMPLE_P16
 #define SAMPLE_P16 2
