@@ -47,15 +47,22 @@ def bytes_per_token(K: int) -> int:
 
 def pmc_traffic(K: int, tokens_per_launch: int, kernel_prefix: str):
     """HBM bytes per sampler launch from the newest committed rocprofv3 PMC
-    summary (profiles/rNN/traffic_k{K}.json, written from separate
-    FETCH_SIZE / WRITE_SIZE passes over this same command by
-    tools/profile_round*.sh).  None when no summary matches this workload."""
+    summary (profiles/rNN/traffic_k{K}.json, written by tools/make_traffic.py
+    from separate FETCH_SIZE / WRITE_SIZE passes over this same command).
+    Used only when it was measured on exactly the library loaded now (sha256)
+    for this workload and kernel; None otherwise."""
     import glob
+    import hashlib
+    from ldagibbssampling_amd import capi
+    lib = os.environ.get("LDA_MI355X_LIB") or capi.LIB_PATH
+    with open(lib, "rb") as f:
+        lib_sha = hashlib.sha256(f.read()).hexdigest()
     paths = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", f"traffic_k{K}.json")))
     for path in reversed(paths):
         with open(path) as f:
             t = json.load(f)
-        if t.get("tokens_per_launch") == tokens_per_launch and t.get("kernel", "").startswith(kernel_prefix):
+        if (t.get("tokens_per_launch") == tokens_per_launch and t.get("lib_sha256") == lib_sha
+                and t.get("kernel", "").startswith(kernel_prefix)):
             return t["hbm_bytes_per_launch"] / 1e9, os.path.relpath(path, ROOT)
     return None, None
 

@@ -16,6 +16,12 @@ import os
 import sys
 
 
+def lib_sha256(path):
+    import hashlib
+    with open(path, "rb") as f:
+        return hashlib.sha256(f.read()).hexdigest()
+
+
 def main(d, kernel, tokens, workload, out):
     kt = json.load(open(os.path.join(d, "summary_kt.json")))
     fe = json.load(open(os.path.join(d, "summary_fetch.json")))["counters"][kernel]["FETCH_SIZE"]
@@ -41,6 +47,11 @@ def main(d, kernel, tokens, workload, out):
             h, m = c["TCC_HIT_sum"]["avg_per_dispatch"], c["TCC_MISS_sum"]["avg_per_dispatch"]
             t["l2_hit_rate"] = h / (h + m) if h + m else None
     t["bytes_per_token"] = t["hbm_bytes_per_launch"] / t["tokens_per_launch"]
+    # the library these counters belong to: bench.py uses the file only for it
+    lib = os.environ.get("LDA_MI355X_LIB") or os.path.join(
+        os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "ldagibbssampling_amd", "lib",
+        "liblda_mi355x.so")
+    t["lib_sha256"] = lib_sha256(lib)
     with open(out, "w") as f:
         json.dump(t, f, indent=1)
     print(json.dumps(t, indent=1))
