@@ -598,7 +598,7 @@ __global__ __launch_bounds__(256) void k_sample_sparse(SampleParams p) {
 #pragma unroll
     for (int s = 0; s < P; ++s) {
       const int64_t tp = t0 + s;
-      const int n = readlane_i(cmn, s);
+      const int n = readlane_i(cmn, s) & 0x7FFFFFFF;
       const int64_t o = ((int64_t)readlane_i((int)(cmo >> 32), s) << 32) |
                         (uint32_t)readlane_i((int)cmo, s);
 #pragma unroll
@@ -655,7 +655,9 @@ __global__ __launch_bounds__(256) void k_sample_sparse(SampleParams p) {
         const int w = readlane_i(cw, idx);
         const int zo = readlane_i(cz, idx);
         const float u = readlane_f(cu, idx);
-        const int n = readlane_i(cmn, idx);
+        const int n_raw = readlane_i(cmn, idx);
+        const bool row_sat = n_raw < 0;           // the row holds a saturated count
+        const int n = n_raw & 0x7FFFFFFF;
         const int64_t off = ((int64_t)readlane_i((int)(cmo >> 32), idx) << 32) |
                             (uint32_t)readlane_i((int)cmo, idx);
         const int lo = zo / C;
@@ -693,7 +695,7 @@ __global__ __launch_bounds__(256) void k_sample_sparse(SampleParams p) {
             const bool valid = q * 64 + lane < n;
             const int tq = (int)(e[q] & ENT_TOPIC_MASK);
             int cq = (int)(e[q] >> ENT_TOPIC_BITS);
-            if (valid && (uint32_t)cq == ENT_COUNT_SAT) cq = nw[(int64_t)w * KP + tq];
+            if (row_sat && valid && (uint32_t)cq == ENT_COUNT_SAT) cq = nw[(int64_t)w * KP + tq];
             if (!FROZEN) cq -= (tq == zo) ? 1 : 0;
             const float b = valid ? coef[tq] * (float)cq : 0.0f;
             accB = accB + b;
@@ -784,10 +786,10 @@ __global__ __launch_bounds__(256) void k_sample_sparse(SampleParams p) {
           int np;
           int64_t op;
           if (pidx < 64) {
-            np = readlane_i(cmn, pidx);
+            np = readlane_i(cmn, pidx) & 0x7FFFFFFF;
             op = ((int64_t)readlane_i((int)(cmo >> 32), pidx) << 32) | (uint32_t)readlane_i((int)cmo, pidx);
           } else {
-            np = readlane_i(m1n, pidx - 64);
+            np = readlane_i(m1n, pidx - 64) & 0x7FFFFFFF;
             op = ((int64_t)readlane_i((int)(m1o >> 32), pidx - 64) << 32) |
                  (uint32_t)readlane_i((int)m1o, pidx - 64);
           }
@@ -968,7 +970,7 @@ __global__ __launch_bounds__(64 * sb_waves<C>()) void k_sample_sparse_big(Sample
 #pragma unroll
     for (int s = 0; s < P; ++s) {
       const int64_t tp = t0 + s;
-      const int n = readlane_i(cmn, s);
+      const int n = readlane_i(cmn, s) & 0x7FFFFFFF;
       const int64_t o = ((int64_t)readlane_i((int)(cmo >> 32), s) << 32) | (uint32_t)readlane_i((int)cmo, s);
 #pragma unroll
       for (int q = 0; q < SB_RB; ++q)
@@ -1012,7 +1014,9 @@ __global__ __launch_bounds__(64 * sb_waves<C>()) void k_sample_sparse_big(Sample
         const int w = readlane_i(cw, idx);
         const int zo = readlane_i(cz, idx);
         const float u = readlane_f(cu, idx);
-        const int n = readlane_i(cmn, idx);
+        const int n_raw = readlane_i(cmn, idx);
+        const bool row_sat = n_raw < 0;           // the row holds a saturated count
+        const int n = n_raw & 0x7FFFFFFF;
         const int64_t off = ((int64_t)readlane_i((int)(cmo >> 32), idx) << 32) | (uint32_t)readlane_i((int)cmo, idx);
         const int lo = zo / C;
         const int go = (zo % C) / 16;
@@ -1031,7 +1035,7 @@ __global__ __launch_bounds__(64 * sb_waves<C>()) void k_sample_sparse_big(Sample
         auto entry_b = [&](uint32_t e, bool valid, int& tq) -> float {
           tq = (int)(e & ENT_TOPIC_MASK);
           int cq = (int)(e >> ENT_TOPIC_BITS);
-          if (valid && (uint32_t)cq == ENT_COUNT_SAT) cq = nw[(int64_t)w * KP + tq];
+          if (row_sat && valid && (uint32_t)cq == ENT_COUNT_SAT) cq = nw[(int64_t)w * KP + tq];
           if (!FROZEN) cq -= (tq == zo) ? 1 : 0;
           return valid ? coef_at(tq, zc, invc) * (float)cq : 0.0f;
         };
@@ -1142,11 +1146,11 @@ __global__ __launch_bounds__(64 * sb_waves<C>()) void k_sample_sparse_big(Sample
           int np, zp;
           int64_t op;
           if (pidx < 64) {
-            np = readlane_i(cmn, pidx);
+            np = readlane_i(cmn, pidx) & 0x7FFFFFFF;
             op = ((int64_t)readlane_i((int)(cmo >> 32), pidx) << 32) | (uint32_t)readlane_i((int)cmo, pidx);
             zp = readlane_i(cz, pidx);
           } else {
-            np = readlane_i(m1n, pidx - 64);
+            np = readlane_i(m1n, pidx - 64) & 0x7FFFFFFF;
             op = ((int64_t)readlane_i((int)(m1o >> 32), pidx - 64) << 32) |
                  (uint32_t)readlane_i((int)m1o, pidx - 64);
             zp = readlane_i(z1, pidx - 64);
@@ -1198,8 +1202,13 @@ __global__ __launch_bounds__(256) void k_build_sparse(const int32_t* __restrict_
     int32_t c[C];
     load_row<C>(c, nw + w * KP + lane * C);
     int cnt = 0;
+    bool sat = false;
 #pragma unroll
-    for (int j = 0; j < C; ++j) cnt += c[j] > 0 ? 1 : 0;
+    for (int j = 0; j < C; ++j) {
+      cnt += c[j] > 0 ? 1 : 0;
+      sat |= (uint32_t)c[j] >= ENT_COUNT_SAT;
+    }
+    const bool row_sat = __ballot(sat) != 0;
     const int incl = wave_incl_scan_i(cnt);
     int pos = incl - cnt;
     const int64_t o = row_off[w];
@@ -1211,7 +1220,9 @@ __global__ __launch_bounds__(256) void k_build_sparse(const int32_t* __restrict_
         ++pos;
       }
     }
-    if (lane == 63) row_nnz[w] = incl;
+    // sign bit: the row holds a saturated count (the sampler then checks
+    // entries for the escape; otherwise it skips that per-entry branch)
+    if (lane == 63) row_nnz[w] = row_sat ? (int32_t)((uint32_t)incl | 0x80000000u) : incl;
   }
 }
 
