@@ -28,7 +28,9 @@ constexpr uint32_t STREAM_INFER = 2u;
 #ifndef SPARSE_P
 #define SPARSE_P 4
 #endif
+#ifndef SPARSE_R0
 #define SPARSE_R0 2
+#endif
 
 struct SampleParams {
   const int32_t* words;     // [N] token stream (doc-contiguous)
