@@ -211,6 +211,7 @@ def main():
     for _ in range(args.burnin + args.warmup):
         step()
     torch.cuda.synchronize()
+    nnz0 = sampler.row_stats() if args.sampler == "sparse" and rank == 0 else None
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -226,6 +227,7 @@ def main():
     # events recorded around every launch on the sampler's stream, read back
     # after the closing synchronize (no host sync inside the timed loop)
     ks = sampler.sample_times(args.steps)
+    nnz1 = sampler.row_stats() if nnz0 is not None else None
     assert len(ks) == min(args.steps, 256)
     kern_ms = float(np.mean(ks))
     copy_gbs = stream_copy_gbs(device) if rank == 0 else None
@@ -290,6 +292,16 @@ def main():
             "ll_per_token": ll / (n_local * world),
             "corpus_gen_s": t_gen,
         }
+        if nnz0 is not None:
+            # the sparse variant also against its own bytes per
+            # token: 4 B per nonzero entry of the token's word row (token-
+            # weighted mean over the timed region's snapshots) + 16 B stream
+            mean_nnz = 0.5 * (nnz0 + nnz1)
+            b_sparse = 4.0 * mean_nnz + 16.0
+            ach = n_local * b_sparse / (kern_ms * 1e-3) / 1e9
+            result["roofline_sparse"] = {
+                "bound": "hbm", "bytes_per_token": b_sparse, "mean_row_nnz": [nnz0, nnz1],
+                "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": ach / HBM_PEAK_GBS}
         if world == 1 and not args.no_cpu_baseline:
             result["cpu_baseline"] = cpu_baseline(corpus, K, alpha_sum, beta, args.cpu_budget)
         print(json.dumps(result), flush=True)

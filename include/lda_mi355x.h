@@ -192,6 +192,11 @@ lda_status lda_learn_symmetric_concentration(const int32_t* count_hist, int64_t 
 /* Dirichlet.digamma (the series the estimators use).  Host-only. */
 double lda_digamma(double z);
 
+/* Token-weighted mean number of nonzero topics in a token's word row of the
+ * current (global) snapshot: sum_w n_w * nnz(nw[w]) / sum_w n_w.  The sparse
+ * samplers read 4 bytes per such entry (SURVEY.md §8d's B_sparse). */
+lda_status lda_row_stats(lda_ctx* ctx, double* mean_row_nnz);
+
 /* Kernel-level timing of the last lda_sample (ms, HIP events on the
  * context's stream). */
 lda_status lda_last_sample_ms(lda_ctx* ctx, float* ms);

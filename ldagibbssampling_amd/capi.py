@@ -90,6 +90,7 @@ SIGNATURES = {
                                                       C.POINTER(C.c_double)]),
     "lda_digamma": (C.c_double, [C.c_double]),
     "lda_last_sample_ms": (C.c_int32, [_vp, C.POINTER(C.c_float)]),
+    "lda_row_stats": (C.c_int32, [_vp, C.POINTER(C.c_double)]),
     "lda_sample_times": (C.c_int32, [_vp, C.c_int32, _vp, C.POINTER(C.c_int32)]),
     "lda_last_error": (C.c_char_p, []),
     "lda_version": (C.c_char_p, []),

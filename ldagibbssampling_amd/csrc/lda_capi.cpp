@@ -677,6 +677,23 @@ lda_status lda_count_histogram(lda_ctx* c, int64_t max_count, int32_t* count_his
   return LDA_OK;
 }
 
+lda_status lda_row_stats(lda_ctx* c, double* mean_row_nnz) {
+  if (!c || !mean_row_nnz) return fail(LDA_ERR_INVALID_ARG, "null argument");
+  if (c->pending) return fail(LDA_ERR_STATE, "row statistics with a pending delta: call lda_apply first");
+  HIP_TRY(hipSetDevice(c->device));
+  unsigned long long* buf = nullptr;
+  HIP_TRY(dalloc(&buf, 2));
+  unsigned long long h[2] = {0, 0};
+  hipError_t e = hipMemsetAsync(buf, 0, 2 * sizeof(unsigned long long), c->stream);
+  if (e == hipSuccess) e = lda::launch_row_stats(c->nw, c->V, c->K, c->Kp, buf, c->stream);
+  if (e == hipSuccess) e = hipMemcpyAsync(h, buf, sizeof(h), hipMemcpyDeviceToHost, c->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+  (void)hipFree(buf);
+  HIP_TRY(e);
+  *mean_row_nnz = h[1] ? (double)h[0] / (double)h[1] : 0.0;
+  return LDA_OK;
+}
+
 lda_status lda_infer(lda_ctx* c, int64_t Dh, const int64_t* doc_off, const int32_t* words,
                      int32_t n_iter, int32_t burn_in, int32_t thin, uint64_t seed, double* theta) {
   if (!c || !doc_off || !theta) return fail(LDA_ERR_INVALID_ARG, "null argument");

@@ -96,6 +96,8 @@ hipError_t launch_ll_words(const int32_t* nw, int64_t V, int32_t K, int32_t Kp, 
 // wavefronts per block of the sampler kernel used for (C, sampler): 4, or
 // 16 for the large-K sparse kernel (C >= 32)
 int sample_waves_per_block(int C, bool sparse);
+hipError_t launch_row_stats(const int32_t* nw, int64_t V, int32_t K, int32_t Kp,
+                            unsigned long long* out, hipStream_t st);
 hipError_t launch_doc_hist(const int32_t* z, const int64_t* doc_off, int64_t D, int32_t K, int32_t Kp,
                            int32_t L, int32_t* len_hist, int32_t* topic_hist, hipStream_t st);
 hipError_t launch_count_hist(const int32_t* nw, int64_t V, int32_t K, int32_t Kp, int64_t max_count,

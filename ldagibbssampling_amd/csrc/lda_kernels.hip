@@ -1458,6 +1458,40 @@ __global__ __launch_bounds__(256) void k_count_hist(const int32_t* __restrict__ 
     if (sh[i]) atomicAdd(&hist[i], sh[i]);
 }
 
+// Token-weighted row sparsity of the snapshot: sum_w total_w * nnz_w and
+// sum_w total_w (one wave per row, one pair of atomics per block).
+__global__ __launch_bounds__(256) void k_row_stats(const int32_t* __restrict__ nw, int64_t V,
+                                                   int32_t K, int32_t Kp,
+                                                   unsigned long long* __restrict__ out) {
+  __shared__ unsigned long long part[2][4];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  unsigned long long wsum = 0, wtot = 0;
+  for (int64_t w = (int64_t)blockIdx.x * 4 + wid; w < V; w += (int64_t)gridDim.x * 4) {
+    unsigned long long tot = 0, nnz = 0;
+    for (int k = lane; k < K; k += 64) {
+      const int32_t c = nw[w * Kp + k];
+      tot += (unsigned long long)c;
+      nnz += c > 0 ? 1 : 0;
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      tot += __shfl_xor(tot, o);
+      nnz += __shfl_xor(nnz, o);
+    }
+    wsum += tot * nnz;
+    wtot += tot;
+  }
+  if (lane == 0) {
+    part[0][wid] = wsum;
+    part[1][wid] = wtot;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    atomicAdd(&out[0], part[0][0] + part[0][1] + part[0][2] + part[0][3]);
+    atomicAdd(&out[1], part[1][0] + part[1][1] + part[1][2] + part[1][3]);
+  }
+}
+
 __global__ __launch_bounds__(256) void k_infer_init(const int32_t* __restrict__ words,
                                                     int32_t* __restrict__ z, int64_t n,
                                                     const int32_t* __restrict__ nw, int32_t K,
@@ -1725,6 +1759,14 @@ hipError_t launch_count_hist(const int32_t* nw, int64_t V, int32_t K, int32_t Kp
   const int blocks = (int)std::min<int64_t>((V * Kp + 255) / 256, 4096);
   hipLaunchKernelGGL(k_count_hist, dim3(blocks), dim3(256), 0, st, nw, V, K, Kp, max_count, hist,
                      overflow);
+  return hipGetLastError();
+}
+
+hipError_t launch_row_stats(const int32_t* nw, int64_t V, int32_t K, int32_t Kp,
+                            unsigned long long* out, hipStream_t st) {
+  if (V <= 0) return hipSuccess;
+  const int blocks = (int)std::min<int64_t>((V + 3) / 4, 2048);
+  hipLaunchKernelGGL(k_row_stats, dim3(blocks), dim3(256), 0, st, nw, V, K, Kp, out);
   return hipGetLastError();
 }
 

@@ -226,6 +226,12 @@ class GibbsSampler:
         capi.check(self._L.lda_count_histogram(self._h, int(max_count), out), "lda_count_histogram")
         return out
 
+    def row_stats(self) -> float:
+        """Token-weighted mean nonzeros per word row of the snapshot."""
+        v = C.c_double()
+        capi.check(self._L.lda_row_stats(self._h, C.byref(v)), "lda_row_stats")
+        return v.value
+
     def mallet_packed(self):
         """typeTopicCounts in Mallet's packed layout: (rows, row_off, topic_bits)."""
         row_off = np.zeros(self.V + 1, dtype=np.int64)
