@@ -77,13 +77,25 @@ __device__ __forceinline__ float dpp_mov(float v) {
 // Inclusive wavefront scan: row_shr:1,2,4,8 inside 16-lane rows (sources
 // outside the row read 0), row_bcast:15 into rows 1 and 3, row_bcast:31 into
 // rows 2 and 3.  Restated lane by lane in oracle/lda_oracle.c:wave_scan_emulate.
+#ifndef LDA_ASM_SCAN
+#define LDA_ASM_SCAN 1
+#endif
 __device__ __forceinline__ float wave_incl_scan(float x) {
   x = dpp_mov<0x111, 0xf, true>(x) + x;
   x = dpp_mov<0x112, 0xf, true>(x) + x;
   x = dpp_mov<0x114, 0xf, true>(x) + x;
   x = dpp_mov<0x118, 0xf, true>(x) + x;
+#if LDA_ASM_SCAN
+  // The two broadcast steps as one masked DPP add each: rows outside the row
+  // mask are not written and keep x (= x + 0 of the two-instruction form).
+  // s_nop 1: a VALU-written VGPR needs two wait states before a DPP read.
+  asm("s_nop 1\n\tv_add_f32_dpp %0, %0, %0 row_bcast:15 row_mask:0xa bank_mask:0xf\n\t"
+      "s_nop 1\n\tv_add_f32_dpp %0, %0, %0 row_bcast:31 row_mask:0xc bank_mask:0xf"
+      : "+v"(x));
+#else
   x = x + dpp_mov<0x142, 0xa, false>(x);
   x = x + dpp_mov<0x143, 0xc, false>(x);
+#endif
   return x;
 }
 
