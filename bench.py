@@ -11,7 +11,7 @@ Synthetic corpus: LDA generative process, drawn on the GPU.
 Prints ONE JSON line (rank 0).  value = tokens sampled by all ranks per
 second of the max-over-ranks wall time of the K timed sweeps.
 
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--config c4|c2|c3]
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--config c4|c1|c2|c3|c5]
 """
 from __future__ import annotations
 
@@ -29,6 +29,10 @@ sys.path.insert(0, ROOT)
 
 CONFIGS = {
     # name: docs per GPU, doc length, V, K, description
+    # c1: BASELINE configs[0], the reference's own scale (changelist-shaped
+    # inverse_docs corpus; K=20, alphaSum 10 as src/cmu, 100 sweeps)
+    "c1": dict(docs=2_000, doc_len=None, V=5_000, K=20, alpha_sum=10.0, steps=100,
+               desc="C1: changelist-shaped corpus, 2000 docs x Poisson(8) tok, Zipf(1.1) over 5000 paths, K=20"),
     "c4": dict(docs=1_250_000, doc_len=200, V=100_000, K=512,
                desc="C4 shard: 1.25M docs x 200 tok per GPU, V=100k, K=512 (N=8 == C4: 10M docs)"),
     "c2": dict(docs=100_000, doc_len=200, V=50_000, K=128, desc="C2: 100k docs x 200 tok, V=50k, K=128"),
@@ -140,7 +144,7 @@ def cpu_baseline(corpus, K, alpha_sum, beta, budget_s=15.0, threads=4):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--steps", type=int, default=None, help="timed sweeps (default 10; 100 for c1)")
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="c4", choices=sorted(CONFIGS))
     ap.add_argument("--docs", type=int, default=0, help="override docs per GPU")
@@ -181,18 +185,27 @@ def main():
     cfg = CONFIGS[args.config]
     if args.sampler is None:
         args.sampler = cfg.get("sampler", "dense")
+    if args.steps is None:
+        args.steps = cfg.get("steps", 10)
     K, V, L = cfg["K"], cfg["V"], cfg["doc_len"]
     docs = args.docs or cfg["docs"]
-    alpha_sum, beta = 0.1 * K, 0.01
+    alpha_sum, beta = cfg.get("alpha_sum", 0.1 * K), 0.01
     t_gen = time.perf_counter()
-    # one corpus: the topics (phi) are shared by every shard, the documents are
-    # drawn per rank (rank 0 == the N=1 workload)
-    corpus = synthetic_lda_torch(docs, V, K, doc_len=L, seed=20261015,
-                                 doc_seed=20261015 + rank, device=f"cuda:{device}")
+    if args.config == "c1":
+        from ldagibbssampling_amd.corpus import synthetic_changelists
+        corpus = synthetic_changelists(num_docs=docs, num_types=V, seed=20261015 + rank)
+        V = corpus.num_types          # the alphabet: paths seen in this shard
+    else:
+        # one corpus: the topics (phi) are shared by every shard, the documents
+        # are drawn per rank (rank 0 == the N=1 workload)
+        corpus = synthetic_lda_torch(docs, V, K, doc_len=L, seed=20261015,
+                                     doc_seed=20261015 + rank, device=f"cuda:{device}")
     t_gen = time.perf_counter() - t_gen
     n_local = corpus.num_tokens
     sampler = GibbsSampler(K, V, corpus.doc_off, corpus.words, np.full(K, alpha_sum / K), beta,
-                           seed=1, device=device, token_base=rank * n_local,
+                           seed=1, device=device,
+                           # unique Philox counters per rank (c1 shards differ in size)
+                           token_base=(rank << 32) if args.config == "c1" else rank * n_local,
                            tokens_per_range=args.tokens_per_range, sampler=args.sampler)
     # one non-default stream carries the sampler kernels and (as torch's
     # current stream) orders the all-reduce behind them: no host sync per sweep.
@@ -258,7 +271,9 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "fp32 weights / int32 counts",
-            "data": "synthetic (LDA generative process, SURVEY.md §8d; phi~Dir(0.01), theta~Dir(0.1))",
+            "data": ("synthetic (changelist-shaped inverse_docs corpus, SURVEY.md §8d; corpus.synthetic_changelists)"
+                     if args.config == "c1" else
+                     "synthetic (LDA generative process, SURVEY.md §8d; phi~Dir(0.01), theta~Dir(0.1))"),
             "config": {
                 "workload": cfg["desc"],
                 "docs_per_gpu": docs,

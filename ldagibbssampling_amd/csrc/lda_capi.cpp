@@ -204,6 +204,14 @@ static lda_status build_row_capacity(lda_ctx* c) {
 
 static lda_status apply_impl(lda_ctx* c) {
   HIP_TRY(hipSetDevice(c->device));
+  if (c->sampler == LDA_SAMPLER_DENSE) {
+    // one launch: apply, 16-bit rows, topic tables, queue reset (k_apply_packed)
+    lda::TopicTables t{c->nwsum, c->alpha_d, c->alpha_f, c->inv, c->inv_m1,
+                       (float)((double)c->V * c->beta), c->K, c->queue};
+    HIP_TRY(lda::launch_apply_packed(c->nw, c->delta, c->V, c->Kp, c->nw16, c->wide, t, c->stream));
+    c->pending = false;
+    return LDA_OK;
+  }
   HIP_TRY(lda::launch_apply(c->nw, c->delta, (int64_t)c->V * c->Kp, c->stream));
   HIP_TRY(lda::launch_prepare_topics(c->nwsum, c->delta + (int64_t)c->V * c->Kp, c->alpha_d,
                                      c->beta, (double)c->V * c->beta, c->K, c->Kp, c->alpha_f,
@@ -321,8 +329,10 @@ lda_status lda_create(lda_ctx** out, const lda_config* cfg, const int64_t* doc_o
   const int64_t waves = (int64_t)c->sample_blocks * c->waves_per_block;
   int64_t tpr = cfg->tokens_per_range;
   // ~32 ranges per wave: fine enough that the launch tail stays short (C4: +5%
-  // over 8 per wave), coarse enough to amortise a range start
-  if (tpr <= 0) tpr = std::max<int64_t>(256, std::min<int64_t>(65536, N / std::max<int64_t>(1, waves * 32)));
+  // over 8 per wave), coarse enough to amortise a range start; at least 16
+  // tokens, so a small corpus spreads over many waves (C1, 16k tokens: 168 ->
+  // 56 us per sweep against a 256-token floor)
+  if (tpr <= 0) tpr = std::max<int64_t>(16, std::min<int64_t>(65536, N / std::max<int64_t>(1, waves * 32)));
   c->tokens_per_range = tpr;
   std::vector<int64_t> ranges = make_ranges(off, tpr);
   c->R = (int64_t)ranges.size() - 1;
@@ -425,7 +435,8 @@ lda_status lda_sample(lda_ctx* c) {
   if (c->pending) return fail(LDA_ERR_STATE, "lda_sample with a pending delta: call lda_apply first");
   HIP_TRY(hipSetDevice(c->device));
   if (c->N > 0) {
-    HIP_TRY(hipMemsetAsync(c->queue, 0, sizeof(int32_t), c->stream));
+    // the dense sampler's apply (which every sample follows) zeroed the queue
+    if (c->sampler != LDA_SAMPLER_DENSE) HIP_TRY(hipMemsetAsync(c->queue, 0, sizeof(int32_t), c->stream));
     const lda::SampleParams p = c->params(false);
     const int64_t wpb = c->waves_per_block;
     const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>(c->sample_blocks, (c->R + wpb - 1) / wpb));
@@ -715,7 +726,7 @@ lda_status lda_infer(lda_ctx* c, int64_t Dh, const int64_t* doc_off, const int32
   HIP_TRY(hipSetDevice(c->device));
   int32_t *dw = nullptr, *dz = nullptr, *acc = nullptr, *q = nullptr;
   int64_t *doff = nullptr, *drange = nullptr;
-  std::vector<int64_t> ranges = make_ranges(off, std::max<int64_t>(256, std::min<int64_t>(c->tokens_per_range, N / std::max<int64_t>(1, (int64_t)c->sample_blocks_frozen * c->waves_per_block * 8))));
+  std::vector<int64_t> ranges = make_ranges(off, std::max<int64_t>(16, std::min<int64_t>(c->tokens_per_range, N / std::max<int64_t>(1, (int64_t)c->sample_blocks_frozen * c->waves_per_block * 8))));
   const int64_t R = (int64_t)ranges.size() - 1;
   hipError_t e = hipSuccess;
   auto chk = [&](hipError_t x) {

@@ -77,6 +77,21 @@ hipError_t launch_build_sparse(const int32_t* nw, int64_t V, int32_t Kp, const i
                                uint32_t* ent, int32_t* row_nnz, hipStream_t st);
 hipError_t launch_build_packed(const int32_t* nw, int64_t V, int32_t Kp, uint16_t* nw16,
                                uint8_t* wide, hipStream_t st);
+// per-topic state refreshed by an apply (k_prepare_topics' arguments)
+struct TopicTables {
+  int32_t* nwsum;           // [Kp]
+  const double* alpha;      // [K]
+  float* alpha_f;           // [Kp]
+  float* inv;               // [Kp]
+  float* inv_m1;            // [Kp]
+  float vbeta;              // (float)(V * beta)
+  int32_t K;
+  int32_t* queue;           // work-queue counter zeroed for the next sample (nullable)
+};
+// dense sampler's apply: nw += delta, delta = 0, 16-bit rows + wide flags,
+// nwsum/tables (k_apply + k_build_packed + k_prepare_topics in one launch)
+hipError_t launch_apply_packed(int32_t* nw, int32_t* delta, int64_t V, int32_t Kp, uint16_t* nw16,
+                               uint8_t* wide, const TopicTables& t, hipStream_t st);
 hipError_t launch_init_z(int32_t* z, int64_t n, int32_t K, int64_t token_base, uint32_t k0,
                          uint32_t k1, hipStream_t st);
 hipError_t launch_count(const int32_t* words, const int32_t* z, int64_t n, int32_t Kp,

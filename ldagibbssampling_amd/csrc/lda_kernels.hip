@@ -80,6 +80,9 @@ __device__ __forceinline__ float dpp_mov(float v) {
 #ifndef LDA_ASM_SCAN
 #define LDA_ASM_SCAN 1
 #endif
+#ifndef LDA_INV_LDS
+#define LDA_INV_LDS 0
+#endif
 __device__ __forceinline__ float wave_incl_scan(float x) {
   x = dpp_mov<0x111, 0xf, true>(x) + x;
   x = dpp_mov<0x112, 0xf, true>(x) + x;
@@ -227,26 +230,35 @@ void k_sample(SampleParams p) {
   // inv_m1 as a per-block LDS table for C <= 8; for C = 16 the extra table
   // would cost a block per CU, so inv_m1[z_old] is prefetched from memory
   constexpr bool kInvLds = C <= 8;
+  // LDA_INV_LDS: the lane's inv factors come from a per-block LDS table (in
+  // place of the inv_m1 table, whose one value per token is prefetched
+  // instead), freeing C VGPRs for rows in flight
+  constexpr bool kInvTab = LDA_INV_LDS && kInvLds;
+  constexpr bool kInvM1Lds = kInvLds && !kInvTab;
   constexpr int TB = kInvLds ? 3 : 2;                // per-block tables before the per-wave area
   const int lane = threadIdx.x & 63;
   const int wid = threadIdx.x >> 6;
   float* t_alpha = reinterpret_cast<float*>(smem);   // [KP] per block
   int32_t* bsum = smem + KP;                         // [KP] per-block nwsum delta
-  float* t_invm1 = reinterpret_cast<float*>(smem + 2 * KP);  // [KP] per block (kInvLds)
+  float* t_invm1 = reinterpret_cast<float*>(smem + 2 * KP);  // [KP] per block (kInvM1Lds)
+  float* t_inv = t_invm1;                                    // [KP] per block (kInvTab)
   int32_t* nd = smem + TB * KP + wid * 2 * KP;       // [KP] per-wave live doc counts
   float* av = reinterpret_cast<float*>(nd + KP);     // [KP] per-wave a_k = float(nd_k) + alpha_k
 
   for (int i = threadIdx.x; i < KP; i += 256) {
     t_alpha[i] = p.alpha[i];
     bsum[i] = 0;
-    if (kInvLds) t_invm1[i] = FROZEN ? 0.0f : p.inv_m1[i];
+    if (kInvM1Lds) t_invm1[i] = FROZEN ? 0.0f : p.inv_m1[i];
+    if (kInvTab) t_inv[i] = p.inv[i];
   }
   for (int i = threadIdx.x; i < 8 * KP; i += 256) smem[TB * KP + i] = 0;
   __syncthreads();
 
-  float inv_r[C];
+  float inv_r[kInvTab ? 1 : C];
+  if constexpr (!kInvTab) {
 #pragma unroll
-  for (int j = 0; j < C; ++j) inv_r[j] = p.inv[lane * C + j];
+    for (int j = 0; j < C; ++j) inv_r[j] = p.inv[lane * C + j];
+  }
   const float beta = p.beta;
   const int last_lane = (p.K - 1) / C;
   const int last_j_tail = (p.K - 1) % C;
@@ -308,7 +320,7 @@ void k_sample(SampleParams p) {
     for (int s = 0; s < P; ++s) {
       const int wp = (s < nt) ? readlane_i(cw, s) : 0;
       load_row16<C>(rows[s], nw16 + (int64_t)wp * KP, lane);
-      if (!FROZEN && !kInvLds) cinv_r[s] = inv_m1[(s < nt) ? readlane_i(cz, s) : 0];
+      if (!FROZEN && !kInvM1Lds) cinv_r[s] = inv_m1[(s < nt) ? readlane_i(cz, s) : 0];
     }
 
     for (int tb = 0; tb < nt; tb += P) {
@@ -367,7 +379,7 @@ void k_sample(SampleParams p) {
         }
         float a[C];
         load_lds_f<C>(a, av + lane * C);
-        const float cinv = FROZEN ? 0.0f : (kInvLds ? t_invm1[zo] : cinv_r[s]);
+        const float cinv = FROZEN ? 0.0f : (kInvM1Lds ? t_invm1[zo] : cinv_r[s]);
         const bool own_old = (lane == lo);
 
         // word factors b = (float(c) + beta) * inv (packed fp32 pairs, each
@@ -388,17 +400,24 @@ void k_sample(SampleParams p) {
 #pragma unroll
         for (int j = 1; j < C; ++j) c_old = (j == jo) ? cfull[j] : c_old;
         const float bc = FROZEN ? 0.0f : ((float)(c_old - 1) + beta) * cinv;
+        float invf[C];
+        if constexpr (kInvTab) {
+          load_lds_f<C>(invf, t_inv + lane * C);
+        } else {
+#pragma unroll
+          for (int j = 0; j < C; ++j) invf[j] = inv_r[j];
+        }
         float bw[C];
         if constexpr (C >= 2) {
 #pragma unroll
           for (int j = 0; j < C; j += 2) {
             pkf32 c2v = {(float)cfull[j], (float)cfull[j + 1]};
-            const pkf32 b2 = (c2v + beta) * (pkf32){inv_r[j], inv_r[j + 1]};
+            const pkf32 b2 = (c2v + beta) * (pkf32){invf[j], invf[j + 1]};
             bw[j] = b2.x;
             bw[j + 1] = b2.y;
           }
         } else {
-          bw[0] = ((float)cfull[0] + beta) * inv_r[0];
+          bw[0] = ((float)cfull[0] + beta) * invf[0];
         }
 
         // lane-serial fma prefix (the z_old element of lane lo uses bc)
@@ -452,7 +471,7 @@ void k_sample(SampleParams p) {
           const int pidx = tp - cbase;
           const int wp = pidx < 64 ? readlane_i(cw, pidx) : readlane_i(w1, pidx - 64);
           load_row16<C>(rows[s], nw16 + (int64_t)wp * KP, lane);
-          if (!FROZEN && !kInvLds)
+          if (!FROZEN && !kInvM1Lds)
             cinv_r[s] = inv_m1[pidx < 64 ? readlane_i(cz, pidx) : readlane_i(z1, pidx - 64)];
         }
       }
@@ -1283,6 +1302,62 @@ __global__ __launch_bounds__(256) void k_apply(int4* __restrict__ nw, int4* __re
   }
 }
 
+// One pass per sweep for the dense sampler: nw += delta (rows with an
+// all-zero delta are not rewritten), delta = 0, the 16-bit copy and wide
+// flag of every row, and — in the first block — nwsum += dsum and the
+// per-topic fp32 tables, plus the work-queue reset of the next lda_sample.
+// Replaces k_apply + k_build_packed + k_prepare_topics (+ a memset): one
+// read of nw instead of two and one launch instead of four.
+template <int C>
+__global__ __launch_bounds__(256) void k_apply_packed(int32_t* __restrict__ nw, int32_t* __restrict__ delta,
+                                                      int64_t V, uint16_t* __restrict__ nw16,
+                                                      uint8_t* __restrict__ wide, TopicTables t) {
+  constexpr int KP = C * 64;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  if (blockIdx.x == 0) {
+    int32_t* dsum = delta + V * KP;
+    for (int k = threadIdx.x; k < KP; k += 256) {
+      const int32_t s = t.nwsum[k] + dsum[k];
+      t.nwsum[k] = s;
+      dsum[k] = 0;
+      if (k < t.K) {
+        t.alpha_f[k] = (float)t.alpha[k];
+        t.inv[k] = 1.0f / ((float)s + t.vbeta);
+        t.inv_m1[k] = 1.0f / ((float)(s - 1) + t.vbeta);
+      } else {
+        t.alpha_f[k] = 0.0f;
+        t.inv[k] = 0.0f;
+        t.inv_m1[k] = 0.0f;
+      }
+    }
+    if (threadIdx.x == 0 && t.queue) *t.queue = 0;
+  }
+  for (int64_t w = (int64_t)blockIdx.x * 4 + wid; w < V; w += (int64_t)gridDim.x * 4) {
+    int32_t c[C], d[C];
+    load_row<C>(c, nw + w * KP + lane * C);
+    load_row<C>(d, delta + w * KP + lane * C);
+    bool changed = false;
+#pragma unroll
+    for (int j = 0; j < C; ++j) changed |= d[j] != 0;
+    if (changed) {
+#pragma unroll
+      for (int j = 0; j < C; ++j) {
+        c[j] += d[j];
+        nw[w * KP + lane * C + j] = c[j];
+        delta[w * KP + lane * C + j] = 0;
+      }
+    }
+    bool big = false;
+#pragma unroll
+    for (int j = 0; j < C; ++j) big |= (uint32_t)c[j] > 0xFFFFu;
+#pragma unroll
+    for (int j = 0; j < C; ++j)
+      nw16[w * KP + lane * C + j] = (uint16_t)((uint32_t)c[j] > 0xFFFFu ? 0xFFFFu : (uint32_t)c[j]);
+    const uint64_t any = __ballot(big);
+    if (lane == 0) wide[w] = any ? 1 : 0;
+  }
+}
+
 // nwsum += dsum; dsum = 0; per-topic fp32 tables (one block, Kp <= 1024).
 __global__ void k_prepare_topics(int32_t* __restrict__ nwsum, int32_t* __restrict__ dsum,
                                  const double* __restrict__ alpha, double beta, double vbeta,
@@ -1692,6 +1767,20 @@ hipError_t launch_build_packed(const int32_t* nw, int64_t V, int32_t Kp, uint16_
     case 4: hipLaunchKernelGGL(k_build_packed<4>, dim3(blocks), dim3(256), 0, st, nw, V, nw16, wide); break;
     case 8: hipLaunchKernelGGL(k_build_packed<8>, dim3(blocks), dim3(256), 0, st, nw, V, nw16, wide); break;
     case 16: hipLaunchKernelGGL(k_build_packed<16>, dim3(blocks), dim3(256), 0, st, nw, V, nw16, wide); break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+hipError_t launch_apply_packed(int32_t* nw, int32_t* delta, int64_t V, int32_t Kp, uint16_t* nw16,
+                               uint8_t* wide, const TopicTables& t, hipStream_t st) {
+  const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>((V + 3) / 4, 16384));
+  switch (Kp / 64) {
+    case 1: hipLaunchKernelGGL(k_apply_packed<1>, dim3(blocks), dim3(256), 0, st, nw, delta, V, nw16, wide, t); break;
+    case 2: hipLaunchKernelGGL(k_apply_packed<2>, dim3(blocks), dim3(256), 0, st, nw, delta, V, nw16, wide, t); break;
+    case 4: hipLaunchKernelGGL(k_apply_packed<4>, dim3(blocks), dim3(256), 0, st, nw, delta, V, nw16, wide, t); break;
+    case 8: hipLaunchKernelGGL(k_apply_packed<8>, dim3(blocks), dim3(256), 0, st, nw, delta, V, nw16, wide, t); break;
+    case 16: hipLaunchKernelGGL(k_apply_packed<16>, dim3(blocks), dim3(256), 0, st, nw, delta, V, nw16, wide, t); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();
