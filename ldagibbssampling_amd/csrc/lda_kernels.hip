@@ -80,9 +80,19 @@ __device__ __forceinline__ float dpp_mov(float v) {
 #ifndef LDA_ASM_SCAN
 #define LDA_ASM_SCAN 1
 #endif
-#ifndef LDA_INV_LDS
-#define LDA_INV_LDS 0
+#ifndef LDA_GPRIDX
+#define LDA_GPRIDX 1
 #endif
+#ifndef LDA_SALU_TRIM
+#define LDA_SALU_TRIM 1
+#endif
+// (jo == j) ? m : 0 as s_cmp + s_cselect_b64 (the compiler splits the 64-bit
+// select in two and adds an s_and)
+__device__ __forceinline__ uint64_t select_mask(int jo, int j, uint64_t m) {
+  uint64_t r;
+  asm("s_cmp_eq_u32 %1, %2\n\ts_cselect_b64 %0, %3, 0" : "=s"(r) : "s"(jo), "s"(j), "s"(m) : "scc");
+  return r;
+}
 __device__ __forceinline__ float wave_incl_scan(float x) {
   x = dpp_mov<0x111, 0xf, true>(x) + x;
   x = dpp_mov<0x112, 0xf, true>(x) + x;
@@ -230,18 +240,13 @@ void k_sample(SampleParams p) {
   // inv_m1 as a per-block LDS table for C <= 8; for C = 16 the extra table
   // would cost a block per CU, so inv_m1[z_old] is prefetched from memory
   constexpr bool kInvLds = C <= 8;
-  // LDA_INV_LDS: the lane's inv factors come from a per-block LDS table (in
-  // place of the inv_m1 table, whose one value per token is prefetched
-  // instead), freeing C VGPRs for rows in flight
-  constexpr bool kInvTab = LDA_INV_LDS && kInvLds;
-  constexpr bool kInvM1Lds = kInvLds && !kInvTab;
+  constexpr bool kInvM1Lds = kInvLds;
   constexpr int TB = kInvLds ? 3 : 2;                // per-block tables before the per-wave area
   const int lane = threadIdx.x & 63;
   const int wid = threadIdx.x >> 6;
   float* t_alpha = reinterpret_cast<float*>(smem);   // [KP] per block
   int32_t* bsum = smem + KP;                         // [KP] per-block nwsum delta
-  float* t_invm1 = reinterpret_cast<float*>(smem + 2 * KP);  // [KP] per block (kInvM1Lds)
-  float* t_inv = t_invm1;                                    // [KP] per block (kInvTab)
+  float* t_invm1 = reinterpret_cast<float*>(smem + 2 * KP);  // [KP] per block (kInvLds)
   int32_t* nd = smem + TB * KP + wid * 2 * KP;       // [KP] per-wave live doc counts
   float* av = reinterpret_cast<float*>(nd + KP);     // [KP] per-wave a_k = float(nd_k) + alpha_k
 
@@ -249,16 +254,13 @@ void k_sample(SampleParams p) {
     t_alpha[i] = p.alpha[i];
     bsum[i] = 0;
     if (kInvM1Lds) t_invm1[i] = FROZEN ? 0.0f : p.inv_m1[i];
-    if (kInvTab) t_inv[i] = p.inv[i];
   }
   for (int i = threadIdx.x; i < 8 * KP; i += 256) smem[TB * KP + i] = 0;
   __syncthreads();
 
-  float inv_r[kInvTab ? 1 : C];
-  if constexpr (!kInvTab) {
+  float inv_r[C];
 #pragma unroll
-    for (int j = 0; j < C; ++j) inv_r[j] = p.inv[lane * C + j];
-  }
+  for (int j = 0; j < C; ++j) inv_r[j] = p.inv[lane * C + j];
   const float beta = p.beta;
   const int last_lane = (p.K - 1) / C;
   const int last_j_tail = (p.K - 1) % C;
@@ -365,7 +367,11 @@ void k_sample(SampleParams p) {
         const int zo = readlane_i(cz, idx);
         const float u = readlane_f(cu, idx);
         const bool wide = readlane_i(cf, idx) != 0;
+#if LDA_SALU_TRIM
+        const int lo = (int)((uint32_t)zo / C), jo = (int)((uint32_t)zo % C);
+#else
         const int lo = zo / C, jo = zo % C;
+#endif
 
         // remove the token from its document (uniform address: lane 0 writes)
         {
@@ -385,7 +391,15 @@ void k_sample(SampleParams p) {
         // word factors b = (float(c) + beta) * inv (packed fp32 pairs, each
         // half an ordinary IEEE add / mul); rows with a count > 65535 come
         // from the int32 row instead (rare: uniform branch, not prefetched)
-        int32_t cfull[C];
+        // The own-token correction touches one element, j_old of lane l_old
+        // (uniform j_old): for C = 16 the row is a 16-wide vector, which
+        // hipcc indexes with s_set_gpr_idx (one move each for reading
+        // c_old and patching b) instead of a select per element (at C = 8 the
+        // 16-register tuple this needs costs 24 more spilled VGPRs).
+        constexpr bool kGprIdx = LDA_GPRIDX && C == 16;
+        typedef int32_t civ __attribute__((ext_vector_type(kGprIdx ? 16 : C)));
+        typedef float cfv __attribute__((ext_vector_type(kGprIdx ? 16 : C)));
+        civ cfull;
         if (wide) {
           const int32_t* wr = nw + (int64_t)w * KP + lane * C;
 #pragma unroll
@@ -396,28 +410,43 @@ void k_sample(SampleParams p) {
         }
         // the own-token-corrected factor of z_old, from lane lo's own row
         // element (exact: a 16-bit row holds every count below 65536)
-        int32_t c_old = cfull[0];
-#pragma unroll
-        for (int j = 1; j < C; ++j) c_old = (j == jo) ? cfull[j] : c_old;
-        const float bc = FROZEN ? 0.0f : ((float)(c_old - 1) + beta) * cinv;
-        float invf[C];
-        if constexpr (kInvTab) {
-          load_lds_f<C>(invf, t_inv + lane * C);
+        int32_t c_old;
+#if LDA_SALU_TRIM
+        // one 64-bit lane mask per element: lane lo where j == jo, else none
+        // (two SALU ops each; selecting under it is exact on lane lo, the
+        // only lane whose value is used)
+        const uint64_t own_mask = __ballot(own_old);
+        uint64_t jmask[kGprIdx ? 1 : C];
+        if constexpr (kGprIdx) {
+          c_old = cfull[jo];
         } else {
 #pragma unroll
-          for (int j = 0; j < C; ++j) invf[j] = inv_r[j];
+          for (int j = 0; j < C; ++j) jmask[j] = select_mask(jo, j, own_mask);
+          c_old = cfull[0];
+#pragma unroll
+          for (int j = 1; j < C; ++j) c_old = __builtin_amdgcn_inverse_ballot_w64(jmask[j]) ? cfull[j] : c_old;
         }
-        float bw[C];
+#else
+        c_old = cfull[0];
+#pragma unroll
+        for (int j = 1; j < C; ++j) c_old = (j == jo) ? cfull[j] : c_old;
+#endif
+        const float bc = FROZEN ? 0.0f : ((float)(c_old - 1) + beta) * cinv;
+        cfv bw;
         if constexpr (C >= 2) {
 #pragma unroll
           for (int j = 0; j < C; j += 2) {
             pkf32 c2v = {(float)cfull[j], (float)cfull[j + 1]};
-            const pkf32 b2 = (c2v + beta) * (pkf32){invf[j], invf[j + 1]};
+            const pkf32 b2 = (c2v + beta) * (pkf32){inv_r[j], inv_r[j + 1]};
             bw[j] = b2.x;
             bw[j + 1] = b2.y;
           }
         } else {
-          bw[0] = ((float)cfull[0] + beta) * invf[0];
+          bw[0] = ((float)cfull[0] + beta) * inv_r[0];
+        }
+        if constexpr (kGprIdx && !FROZEN) {
+          const float bo = bw[jo];
+          bw[jo] = own_old ? bc : bo;
         }
 
         // lane-serial fma prefix (the z_old element of lane lo uses bc)
@@ -425,7 +454,11 @@ void k_sample(SampleParams p) {
         float acc = 0.0f;
 #pragma unroll
         for (int j = 0; j < C; ++j) {
+#if LDA_SALU_TRIM
+          const float b = (kGprIdx || FROZEN) ? bw[j] : (__builtin_amdgcn_inverse_ballot_w64(jmask[j]) ? bc : bw[j]);
+#else
           const float b = (!FROZEN && j == jo && own_old) ? bc : bw[j];
+#endif
           acc = __builtin_fmaf(a[j], b, acc);
           S[j] = acc;
         }
