@@ -231,6 +231,15 @@ constexpr int sample_waves_per_eu() {
   return C == 8 ? 7 : 1;
 }
 
+// Lane i gets a[i + S] for i + S < 64, else b[i + S - 64] (a wave-wide
+// shift across two chunk registers; two ds_bpermutes).
+template <int S>
+__device__ __forceinline__ int shift_in(int a, int b, int lane) {
+  const int src = (lane + S) & 63;
+  const int va = __shfl(a, src), vb = __shfl(b, src);
+  return lane + S < 64 ? va : vb;
+}
+
 template <int C, int P, bool FROZEN>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(sample_waves_per_eu<C>())))
 void k_sample(SampleParams p) {
@@ -302,6 +311,11 @@ void k_sample(SampleParams p) {
     int cf = (int)wide_of[cw], f1 = (int)wide_of[w1];
     int cn = cz;
     float cu = u01(draw_u32(gbase + (uint64_t)lane, p.c2, p.c3, p.k0, p.k1));
+    // word (and, for the inv_m1 prefetch, topic) of token cbase + lane + P:
+    // the row prefetch reads it with one readlane instead of branching
+    // between chunks
+    int pw = shift_in<P>(cw, w1, lane);
+    int pz = kInvM1Lds ? 0 : shift_in<P>(cz, z1, lane);
 
     // --- first document of the range (nd is all zero here)
     int64_t doc = d0;
@@ -348,6 +362,8 @@ void k_sample(SampleParams p) {
             w2 = wrd[cbase + 128 + lane];
             z2 = zr[cbase + 128 + lane];
           }
+          pw = shift_in<P>(cw, w1, lane);
+          if constexpr (!kInvM1Lds) pz = shift_in<P>(cz, z1, lane);
         }
         if (t == doc_end) {
 #pragma unroll
@@ -469,7 +485,8 @@ void k_sample(SampleParams p) {
         const float thr = u * total;
         const uint64_t m = __ballot((T > thr) && (lane <= last_lane));
         const int lstar = m ? (int)__builtin_ctzll(m) : last_lane;
-        const float E = lstar > 0 ? readlane_f(T, lstar - 1) : 0.0f;
+        const float Er = readlane_f(T, lstar > 0 ? lstar - 1 : 0);
+        const float E = lstar > 0 ? Er : 0.0f;
         // every lane counts its own prefix against lane lstar's E; lstar's count is the one used
         int cl = 0;
 #pragma unroll
@@ -501,11 +518,9 @@ void k_sample(SampleParams p) {
         // keep the pipeline full: token t+P
         const int tp = t + P;
         if (tp < nt) {
-          const int pidx = tp - cbase;
-          const int wp = pidx < 64 ? readlane_i(cw, pidx) : readlane_i(w1, pidx - 64);
+          const int wp = readlane_i(pw, idx);
           load_row16<C>(rows[s], nw16 + (int64_t)wp * KP, lane);
-          if (!FROZEN && !kInvM1Lds)
-            cinv_r[s] = inv_m1[pidx < 64 ? readlane_i(cz, pidx) : readlane_i(z1, pidx - 64)];
+          if (!FROZEN && !kInvM1Lds) cinv_r[s] = inv_m1[readlane_i(pz, idx)];
         }
       }
     }
