@@ -59,6 +59,7 @@ typedef int32_t lda_status;
  *  SPARSE  reads only the row's nonzero (count, topic) entries (4 bytes each),
  *          SparseLDA-style split into a word part and a dense doc part
  *          (a different fp32 summation with its own oracle restatement). */
+/* The dense sampler needs num_types * Kp < 2^32 (V < 4.19M words at K = 1024). */
 #define LDA_SAMPLER_DENSE 0
 #define LDA_SAMPLER_SPARSE 1
 

@@ -257,6 +257,10 @@ lda_status lda_create(lda_ctx** out, const lda_config* cfg, const int64_t* doc_o
     return fail(LDA_ERR_UNSUPPORTED,
                 "num_topics above LDA_MAX_TOPICS_DENSE (1024): use LDA_SAMPLER_SPARSE");
   if (cfg->num_types < 1) return fail(LDA_ERR_INVALID_ARG, "num_types must be >= 1");
+  // the dense sampler indexes nw cells with 32 bits
+  if (cfg->sampler == LDA_SAMPLER_DENSE &&
+      (int64_t)cfg->num_types * pad_topics(cfg->num_topics) >= (int64_t(1) << 32))
+    return fail(LDA_ERR_UNSUPPORTED, "num_types * padded topics >= 2^32 with the dense sampler: use LDA_SAMPLER_SPARSE");
   if (cfg->num_docs < 0) return fail(LDA_ERR_INVALID_ARG, "num_docs must be >= 0");
   if (!cfg->alpha) return fail(LDA_ERR_INVALID_ARG, "alpha is null");
   if (!(cfg->beta > 0.0)) return fail(LDA_ERR_INVALID_ARG, "beta must be > 0");

@@ -83,9 +83,18 @@ __device__ __forceinline__ float dpp_mov(float v) {
 #ifndef LDA_GPRIDX
 #define LDA_GPRIDX 1
 #endif
+#ifndef LDA_UPD_MASK
+#define LDA_UPD_MASK 1
+#endif
 #ifndef LDA_SALU_TRIM
 #define LDA_SALU_TRIM 1
 #endif
+// (a != b) ? m : 0 as s_cmp + s_cselect_b64
+__device__ __forceinline__ uint64_t select_mask_ne(int a, int b, uint64_t m) {
+  uint64_t r;
+  asm("s_cmp_lg_u32 %1, %2\n\ts_cselect_b64 %0, %3, 0" : "=s"(r) : "s"(a), "s"(b), "s"(m) : "scc");
+  return r;
+}
 // (jo == j) ? m : 0 as s_cmp + s_cselect_b64 (the compiler splits the 64-bit
 // select in two and adds an s_and)
 __device__ __forceinline__ uint64_t select_mask(int jo, int j, uint64_t m) {
@@ -271,6 +280,7 @@ void k_sample(SampleParams p) {
 #pragma unroll
   for (int j = 0; j < C; ++j) inv_r[j] = p.inv[lane * C + j];
   const float beta = p.beta;
+  const uint64_t lt2_mask = __ballot(lane < 2);
   const int last_lane = (p.K - 1) / C;
   const int last_j_tail = (p.K - 1) % C;
   const uint16_t* __restrict__ nw16 = p.nw16;
@@ -506,13 +516,24 @@ void k_sample(SampleParams p) {
           wave_lds_fence();
         }
         cn = (lane == idx) ? kn : cn;
-        if (!FROZEN && kn != zo) {
-          if (lane < 2) {
+        if constexpr (!FROZEN) {
+#if LDA_UPD_MASK
+          // lanes 0 and 1 when the topic changed: one s_cmp + s_cselect; the
+          // 32-bit cell index is valid because lda_create keeps V*Kp < 2^32
+          if (__builtin_amdgcn_inverse_ballot_w64(select_mask_ne(kn, zo, lt2_mask))) {
+            const int k = lane == 0 ? zo : kn;
+            const int v = lane == 0 ? -1 : 1;
+            atomicAdd(p.delta + ((uint32_t)w * (uint32_t)KP + (uint32_t)k), v);
+            atomicAdd(&bsum[k], v);
+          }
+#else
+          if (kn != zo && lane < 2) {
             const int k = lane == 0 ? zo : kn;
             const int v = lane == 0 ? -1 : 1;
             atomicAdd(&p.delta[(int64_t)w * KP + k], v);
             atomicAdd(&bsum[k], v);
           }
+#endif
         }
 
         // keep the pipeline full: token t+P

@@ -80,6 +80,15 @@ def test_invalid_arguments_fail_loudly(lib):
         capi.check(st, "lda_create")
     assert lib.lda_sweep(None, 1) == -1
     assert lib.lda_sample(None) == -1
+    # the dense sampler indexes nw cells with 32 bits: V * Kp >= 2^32 is refused
+    alpha = np.full(1024, 0.1)
+    cfg.num_topics = 1024
+    cfg.num_types = 1 << 22
+    cfg.alpha = alpha.ctypes.data_as(C.POINTER(C.c_double))
+    cfg.beta = 0.01
+    cfg.sampler = capi.SAMPLERS["dense"]
+    st = lib.lda_create(C.byref(h), C.byref(cfg), off, w.ctypes.data, None)
+    assert st == -5 and b"2^32" in lib.lda_last_error()
 
 
 def test_no_cpu_fallback_without_library(tmp_path):
