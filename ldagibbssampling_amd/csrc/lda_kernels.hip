@@ -92,6 +92,10 @@ __device__ __forceinline__ float dpp_mov(float v) {
 // (a != b) ? m : 0 as s_cmp + s_cselect_b64
 __device__ __forceinline__ uint64_t select_mask_ne(int a, int b, uint64_t m) {
   uint64_t r;
+  // the operands are wave-uniform; readfirstlane keeps them in SGPRs even
+  // where the compiler's divergence analysis cannot tell
+  a = __builtin_amdgcn_readfirstlane(a);
+  b = __builtin_amdgcn_readfirstlane(b);
   asm("s_cmp_lg_u32 %1, %2\n\ts_cselect_b64 %0, %3, 0" : "=s"(r) : "s"(a), "s"(b), "s"(m) : "scc");
   return r;
 }
@@ -99,6 +103,7 @@ __device__ __forceinline__ uint64_t select_mask_ne(int a, int b, uint64_t m) {
 // select in two and adds an s_and)
 __device__ __forceinline__ uint64_t select_mask(int jo, int j, uint64_t m) {
   uint64_t r;
+  jo = __builtin_amdgcn_readfirstlane(jo);
   asm("s_cmp_eq_u32 %1, %2\n\ts_cselect_b64 %0, %3, 0" : "=s"(r) : "s"(jo), "s"(j), "s"(m) : "scc");
   return r;
 }
