@@ -99,6 +99,28 @@ __device__ __forceinline__ uint64_t select_mask_ne(int a, int b, uint64_t m) {
   asm("s_cmp_lg_u32 %1, %2\n\ts_cselect_b64 %0, %3, 0" : "=s"(r) : "s"(a), "s"(b), "s"(m) : "scc");
   return r;
 }
+// (jo == J) ? m : 0 for J = 0..C-1 (immediate J: no constant in an SGPR)
+template <int J>
+__device__ __forceinline__ uint64_t select_mask_c(int jo, uint64_t m) {
+  uint64_t r;
+  jo = __builtin_amdgcn_readfirstlane(jo);
+  asm("s_cmp_eq_u32 %1, %2\n\ts_cselect_b64 %0, %3, 0" : "=s"(r) : "s"(jo), "n"(J), "s"(m) : "scc");
+  return r;
+}
+template <int C, int J = 0>
+__device__ __forceinline__ void fill_masks(uint64_t (&jm)[C], int jo, uint64_t m) {
+  if constexpr (J < C) {
+    jm[J] = select_mask_c<J>(jo, m);
+    fill_masks<C, J + 1>(jm, jo, m);
+  }
+}
+// the lowest set lane of m, or `none` when m is empty (s_ff1 gives -1 for 0)
+__device__ __forceinline__ int first_lane_or(uint64_t m, int none) {
+  int r;
+  none = __builtin_amdgcn_readfirstlane(none);
+  asm("s_ff1_i32_b64 %0, %1\n\ts_min_u32 %0, %0, %2" : "=&s"(r) : "s"(m), "s"(none) : "scc");
+  return r;
+}
 // (jo == j) ? m : 0 as s_cmp + s_cselect_b64 (the compiler splits the 64-bit
 // select in two and adds an s_and)
 __device__ __forceinline__ uint64_t select_mask(int jo, int j, uint64_t m) {
@@ -287,6 +309,7 @@ void k_sample(SampleParams p) {
   const float beta = p.beta;
   const uint64_t lt2_mask = __ballot(lane < 2);
   const int last_lane = (p.K - 1) / C;
+  const uint64_t last_mask = __ballot(lane <= last_lane);
   const int last_j_tail = (p.K - 1) % C;
   const uint16_t* __restrict__ nw16 = p.nw16;
   const uint8_t* __restrict__ wide_of = p.wide;
@@ -451,8 +474,7 @@ void k_sample(SampleParams p) {
         if constexpr (kGprIdx) {
           c_old = cfull[jo];
         } else {
-#pragma unroll
-          for (int j = 0; j < C; ++j) jmask[j] = select_mask(jo, j, own_mask);
+          fill_masks<C>(jmask, jo, own_mask);
           c_old = cfull[0];
 #pragma unroll
           for (int j = 1; j < C; ++j) c_old = __builtin_amdgcn_inverse_ballot_w64(jmask[j]) ? cfull[j] : c_old;
@@ -498,16 +520,18 @@ void k_sample(SampleParams p) {
         const float T = wave_incl_scan(acc);
         const float total = readlane_f(T, 63);
         const float thr = u * total;
-        const uint64_t m = __ballot((T > thr) && (lane <= last_lane));
-        const int lstar = m ? (int)__builtin_ctzll(m) : last_lane;
-        const float Er = readlane_f(T, lstar > 0 ? lstar - 1 : 0);
-        const float E = lstar > 0 ? Er : 0.0f;
+        const uint64_t m = __ballot(T > thr) & last_mask;
+        const int lstar = first_lane_or(m, last_lane);
+        // T of lane lstar - 1 (0 for lane 0): the scan shifted one lane up
+        const float E = readlane_f(dpp_mov<0x138, 0xf, true>(T), lstar);
         // every lane counts its own prefix against lane lstar's E; lstar's count is the one used
         int cl = 0;
 #pragma unroll
         for (int j = 0; j < C; ++j) cl += (E + S[j] <= thr) ? 1 : 0;
         const int cnt = readlane_i(cl, lstar);
-        const int jsel = cnt < C ? cnt : (lstar < last_lane ? C - 1 : last_j_tail);
+        // cnt in [0, last valid topic of lstar] or C (padded topics add 0)
+        const int lim = lstar < last_lane ? C - 1 : last_j_tail;
+        const int jsel = cnt < lim ? cnt : lim;
         const int kn = lstar * C + jsel;
 
         // add the token back under its new topic
