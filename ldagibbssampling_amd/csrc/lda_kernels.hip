@@ -367,6 +367,8 @@ void k_sample(SampleParams p) {
       wave_lds_fence();
     }
 
+    int kp = 0, inc = 0;              // deferred add-back of the last drawn token
+
     // --- prime the pipeline: 16-bit rows of the next P tokens
     uint32_t rows[P][H];
     float cinv_r[P];
@@ -404,6 +406,7 @@ void k_sample(SampleParams p) {
           if constexpr (!kInvM1Lds) pz = shift_in<P>(cz, z1, lane);
         }
         if (t == doc_end) {
+          inc = 0;                    // the pending add belonged to the last document
 #pragma unroll
           for (int j = 0; j < C; ++j) nd[lane * C + j] = 0;
           wave_lds_fence();
@@ -427,16 +430,18 @@ void k_sample(SampleParams p) {
         const int lo = zo / C, jo = zo % C;
 #endif
 
-        // remove the token from its document (uniform address: lane 0 writes)
-        {
+        // lane 0: add the previous token back under its new topic kp (deferred
+        // from its draw; inc = 0 at a document's first token), then remove
+        // this token from its document
+        if (lane == 0) {
+          const int ndk = nd[kp] + inc;
+          nd[kp] = ndk;
+          av[kp] = (float)ndk + t_alpha[kp];
           const int ndz = nd[zo] - 1;
-          const float az = (float)ndz + t_alpha[zo];
-          if (lane == 0) {
-            nd[zo] = ndz;
-            av[zo] = az;
-          }
-          wave_lds_fence();
+          nd[zo] = ndz;
+          av[zo] = (float)ndz + t_alpha[zo];
         }
+        wave_lds_fence();
         float a[C];
         load_lds_f<C>(a, av + lane * C);
         const float cinv = FROZEN ? 0.0f : (kInvM1Lds ? t_invm1[zo] : cinv_r[s]);
@@ -534,16 +539,9 @@ void k_sample(SampleParams p) {
         const int jsel = cnt < lim ? cnt : lim;
         const int kn = lstar * C + jsel;
 
-        // add the token back under its new topic
-        {
-          const int ndk = nd[kn] + 1;
-          const float ak = (float)ndk + t_alpha[kn];
-          if (lane == 0) {
-            nd[kn] = ndk;
-            av[kn] = ak;
-          }
-          wave_lds_fence();
-        }
+        // the token goes back under kn with the next token's update
+        kp = kn;
+        inc = 1;
         cn = (lane == idx) ? kn : cn;
         if constexpr (!FROZEN) {
 #if LDA_UPD_MASK
