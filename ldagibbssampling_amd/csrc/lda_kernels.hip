@@ -358,7 +358,7 @@ void k_sample(SampleParams p) {
     // --- first document of the range (nd is all zero here)
     int64_t doc = d0;
     while (p.doc_off[doc + 1] <= t0) ++doc;
-    int doc_end = (int)(p.doc_off[doc + 1] - t0);
+    int doc_end = uniform_i((int)(p.doc_off[doc + 1] - t0));
     {
       for (int i = lane; i < doc_end; i += 64) atomicAdd(&nd[zr[i]], 1);
       wave_lds_fence();
@@ -368,6 +368,7 @@ void k_sample(SampleParams p) {
     }
 
     int kp = 0, inc = 0;              // deferred add-back of the last drawn token
+    int ev = min(64, doc_end);        // token index of the next chunk or document start
 
     // --- prime the pipeline: 16-bit rows of the next P tokens
     uint32_t rows[P][H];
@@ -384,41 +385,45 @@ void k_sample(SampleParams p) {
       for (int s = 0; s < P; ++s) {
         const int t = tb + s;
         if (t >= nt) break;
-        int idx = t - cbase;
-        if (idx == 64) {
-          // chunk switch: publish the finished chunk's new z, shift
-          zr[cbase + lane] = cn;
-          cbase += 64;
-          idx = 0;
-          cw = w1;
-          cz = z1;
-          cf = f1;
-          w1 = w2;
-          z1 = z2;
-          f1 = (int)wide_of[w1];
-          cn = cz;
-          cu = u01(draw_u32(gbase + (uint64_t)(cbase + lane), p.c2, p.c3, p.k0, p.k1));
-          if (cbase + 128 + lane < nt) {
-            w2 = wrd[cbase + 128 + lane];
-            z2 = zr[cbase + 128 + lane];
+        if (t == ev) {
+          // the next chunk and/or the next document start here (one compare
+          // per token for both)
+          if (t - cbase == 64) {
+            // chunk switch: publish the finished chunk's new z, shift
+            zr[cbase + lane] = cn;
+            cbase += 64;
+            cw = w1;
+            cz = z1;
+            cf = f1;
+            w1 = w2;
+            z1 = z2;
+            f1 = (int)wide_of[w1];
+            cn = cz;
+            cu = u01(draw_u32(gbase + (uint64_t)(cbase + lane), p.c2, p.c3, p.k0, p.k1));
+            if (cbase + 128 + lane < nt) {
+              w2 = wrd[cbase + 128 + lane];
+              z2 = zr[cbase + 128 + lane];
+            }
+            pw = shift_in<P>(cw, w1, lane);
+            if constexpr (!kInvM1Lds) pz = shift_in<P>(cz, z1, lane);
           }
-          pw = shift_in<P>(cw, w1, lane);
-          if constexpr (!kInvM1Lds) pz = shift_in<P>(cz, z1, lane);
-        }
-        if (t == doc_end) {
-          inc = 0;                    // the pending add belonged to the last document
+          if (t == doc_end) {
+            inc = 0;                  // the pending add belonged to the last document
 #pragma unroll
-          for (int j = 0; j < C; ++j) nd[lane * C + j] = 0;
-          wave_lds_fence();
-          ++doc;
-          while (p.doc_off[doc + 1] - t0 <= t) ++doc;
-          doc_end = (int)(p.doc_off[doc + 1] - t0);
-          for (int i = t + lane; i < doc_end; i += 64) atomicAdd(&nd[zr[i]], 1);
-          wave_lds_fence();
+            for (int j = 0; j < C; ++j) nd[lane * C + j] = 0;
+            wave_lds_fence();
+            ++doc;
+            while (p.doc_off[doc + 1] - t0 <= t) ++doc;
+            doc_end = uniform_i((int)(p.doc_off[doc + 1] - t0));
+            for (int i = t + lane; i < doc_end; i += 64) atomicAdd(&nd[zr[i]], 1);
+            wave_lds_fence();
 #pragma unroll
-          for (int j = 0; j < C; ++j) av[lane * C + j] = (float)nd[lane * C + j] + t_alpha[lane * C + j];
-          wave_lds_fence();
+            for (int j = 0; j < C; ++j) av[lane * C + j] = (float)nd[lane * C + j] + t_alpha[lane * C + j];
+            wave_lds_fence();
+          }
+          ev = min(cbase + 64, doc_end);
         }
+        const int idx = t - cbase;
 
         const int w = readlane_i(cw, idx);
         const int zo = readlane_i(cz, idx);
