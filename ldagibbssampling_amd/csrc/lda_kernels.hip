@@ -456,13 +456,17 @@ void k_sample(SampleParams p) {
         // half an ordinary IEEE add / mul); rows with a count > 65535 come
         // from the int32 row instead (rare: uniform branch, not prefetched)
         // The own-token correction touches one element, j_old of lane l_old
-        // (uniform j_old): for C = 16 the row is a 16-wide vector, which
-        // hipcc indexes with s_set_gpr_idx (one move each for reading
-        // c_old and patching b) instead of a select per element (at C = 8 the
-        // 16-register tuple this needs costs 24 more spilled VGPRs).
-        constexpr bool kGprIdx = LDA_GPRIDX && C == 16;
-        typedef int32_t civ __attribute__((ext_vector_type(kGprIdx ? 16 : C)));
-        typedef float cfv __attribute__((ext_vector_type(kGprIdx ? 16 : C)));
+        // (uniform j_old): for C >= 8 the row is a vector that hipcc indexes
+        // with s_set_gpr_idx (one move each for reading c_old and patching b)
+        // instead of a select per element and a lane mask per element (C4:
+        // 5.93 -> 6.26 G tok/s, although the tuples spill 9 more VGPRs).
+        constexpr bool kGprIdx = LDA_GPRIDX && C >= 8;
+        // C = 8 rows as 9-wide vectors: hipcc expands a dynamic index into
+        // selects for up to 8 elements, and indexes 9 or more with
+        // s_set_gpr_idx (the 9th register is never addressed: jo < C)
+        constexpr int CV = (kGprIdx && C == 8) ? 9 : C;
+        typedef int32_t civ __attribute__((ext_vector_type(CV)));
+        typedef float cfv __attribute__((ext_vector_type(CV)));
         civ cfull;
         if (wide) {
           const int32_t* wr = nw + (int64_t)w * KP + lane * C;
