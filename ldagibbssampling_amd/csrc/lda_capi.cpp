@@ -63,14 +63,20 @@ double log_gamma_stirling(double z) {  // Dirichlet.logGammaStirling [M]
   return result;
 }
 
-// Group whole documents into work ranges of about `target` tokens.
+// Group whole documents into work ranges of about `target` tokens.  The
+// queue hands ranges out in order, so the last ~1/8 of the tokens go in
+// ranges of target/4: the waves that take them finish closer together
+// (a shorter launch tail).
 std::vector<int64_t> make_ranges(const std::vector<int64_t>& off, int64_t target) {
   std::vector<int64_t> r;
   const int64_t D = (int64_t)off.size() - 1;
   r.push_back(0);
   int64_t start_tok = off[0];
+  const int64_t tail_from = off[0] + (off[D] - off[0]) / 8 * 7;
+  const int64_t tail_target = std::max<int64_t>(16, target / 4);
   for (int64_t d = 0; d < D; ++d) {
-    if (off[d + 1] - start_tok >= target) {
+    const int64_t tgt = start_tok >= tail_from ? tail_target : target;
+    if (off[d + 1] - start_tok >= tgt) {
       r.push_back(d + 1);
       start_tok = off[d + 1];
     }
