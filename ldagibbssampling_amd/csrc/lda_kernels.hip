@@ -540,8 +540,17 @@ void k_sample(SampleParams p) {
         const float E = readlane_f(dpp_mov<0x138, 0xf, true>(T), lstar);
         // every lane counts its own prefix against lane lstar's E; lstar's count is the one used
         int cl = 0;
+        if constexpr (C >= 2) {
+          // E + S_j in packed pairs (each half an IEEE add)
 #pragma unroll
-        for (int j = 0; j < C; ++j) cl += (E + S[j] <= thr) ? 1 : 0;
+          for (int j = 0; j < C; j += 2) {
+            const pkf32 es = (pkf32){E, E} + (pkf32){S[j], S[j + 1]};
+            cl += (es.x <= thr) ? 1 : 0;
+            cl += (es.y <= thr) ? 1 : 0;
+          }
+        } else {
+          cl = (E + S[0] <= thr) ? 1 : 0;
+        }
         const int cnt = readlane_i(cl, lstar);
         // cnt in [0, last valid topic of lstar] or C (padded topics add 0)
         const int lim = lstar < last_lane ? C - 1 : last_j_tail;
