@@ -89,6 +89,21 @@ __device__ __forceinline__ float dpp_mov(float v) {
 #ifndef LDA_SALU_TRIM
 #define LDA_SALU_TRIM 1
 #endif
+// Keep the row prefetch a real pipeline: vmcnt counts vector memory
+// operations in issue order, and the compiler waits for row t while row t+1
+// stays in flight (vmcnt(P-1)) only when every token issues the same number
+// of them.  So the delta atomics are issued per 64-token chunk instead of per
+// token (LDA_CHUNK_DELTA), the prefetch load is unconditional, and the rare
+// int32-row load drains itself (LDA_WIDE_DRAIN).  Without them every token
+// waited vmcnt(0), i.e. for the row prefetched one token earlier.
+#ifndef LDA_WIDE_DRAIN
+#define LDA_WIDE_DRAIN 1
+#endif
+#ifndef LDA_CHUNK_DELTA
+#define LDA_CHUNK_DELTA 1
+#endif
+// s_waitcnt vmcnt(0) (gfx9 encoding: expcnt and lgkmcnt left at their maxima)
+constexpr int kVmcnt0 = 0x0F70;
 // (a != b) ? m : 0 as s_cmp + s_cselect_b64
 __device__ __forceinline__ uint64_t select_mask_ne(int a, int b, uint64_t m) {
   uint64_t r;
@@ -329,6 +344,18 @@ void k_sample(SampleParams p) {
     const int32_t* __restrict__ wrd = p.words + t0;
     int32_t* __restrict__ zr = p.z + t0;
     const uint64_t gbase = (uint64_t)(p.token_base + t0);
+    // a finished chunk's count changes, lane i = token cbase + i (word w_,
+    // topic zo_ -> zn_): two wave-wide atomics per 64 tokens; the 32-bit cell
+    // index is valid because lda_create keeps V*Kp < 2^32
+    auto flush_delta = [&](int w_, int zo_, int zn_) {
+      if (!FROZEN && LDA_CHUNK_DELTA && zn_ != zo_) {
+        const uint32_t row = (uint32_t)w_ * (uint32_t)KP;
+        atomicAdd(p.delta + (row + (uint32_t)zo_), -1);
+        atomicAdd(p.delta + (row + (uint32_t)zn_), 1);
+        atomicAdd(&bsum[zo_], -1);
+        atomicAdd(&bsum[zn_], 1);
+      }
+    };
 
     // --- chunk registers: chunk c (cw, cz, cu, cn, cf), c+1 (w1, z1, f1), c+2 (w2, z2);
     // f = 1 when the word's row holds a count > 65535 (read the int32 row)
@@ -380,17 +407,16 @@ void k_sample(SampleParams p) {
       if (!FROZEN && !kInvM1Lds) cinv_r[s] = inv_m1[(s < nt) ? readlane_i(cz, s) : 0];
     }
 
-    for (int tb = 0; tb < nt; tb += P) {
-#pragma unroll
-      for (int s = 0; s < P; ++s) {
-        const int t = tb + s;
-        if (t >= nt) break;
+    // one token (slot s of its group of P: rows[s] holds its row)
+    auto token = [&](const int t, const int s) __attribute__((always_inline)) {
         if (t == ev) {
           // the next chunk and/or the next document start here (one compare
           // per token for both)
           if (t - cbase == 64) {
-            // chunk switch: publish the finished chunk's new z, shift
+            // chunk switch: publish the finished chunk's new z and count
+            // changes, shift
             zr[cbase + lane] = cn;
+            flush_delta(cw, cz, cn);
             cbase += 64;
             cw = w1;
             cz = z1;
@@ -472,6 +498,12 @@ void k_sample(SampleParams p) {
           const int32_t* wr = nw + (int64_t)w * KP + lane * C;
 #pragma unroll
           for (int j = 0; j < C; ++j) cfull[j] = wr[j];
+#if LDA_WIDE_DRAIN
+          // hipcc lays the 16-bit branch out as a fall-through successor of
+          // this block: without this wait, this load in flight into cfull
+          // makes it wait vmcnt(0) there too
+          __builtin_amdgcn_s_waitcnt(kVmcnt0);
+#endif
         } else {
 #pragma unroll
           for (int j = 0; j < C; ++j) cfull[j] = row16_count<C>(rows[s], j);
@@ -561,7 +593,7 @@ void k_sample(SampleParams p) {
         kp = kn;
         inc = 1;
         cn = (lane == idx) ? kn : cn;
-        if constexpr (!FROZEN) {
+        if constexpr (!FROZEN && !LDA_CHUNK_DELTA) {
 #if LDA_UPD_MASK
           // lanes 0 and 1 when the topic changed: one s_cmp + s_cselect; the
           // 32-bit cell index is valid because lda_create keeps V*Kp < 2^32
@@ -581,16 +613,29 @@ void k_sample(SampleParams p) {
 #endif
         }
 
-        // keep the pipeline full: token t+P
-        const int tp = t + P;
-        if (tp < nt) {
+        // keep the pipeline full: token t+P.  Unconditional (past the range
+        // end pw/pz hold stale but valid word / topic ids), so that every
+        // token issues the same loads and row t+1 stays in flight at token t
+        if (LDA_CHUNK_DELTA || t + P < nt) {
           const int wp = readlane_i(pw, idx);
           load_row16<C>(rows[s], nw16 + (int64_t)wp * KP, lane);
           if (!FROZEN && !kInvM1Lds) cinv_r[s] = inv_m1[readlane_i(pz, idx)];
         }
-      }
+    };
+    // Whole groups of P tokens, then the tail: no exit inside a group, so
+    // that every CFG path round the loop issues the same P row loads (an
+    // early break becomes a flag path that skips a slot's load, and the
+    // compiler's vmcnt for the next row is then 0)
+    int tb = 0;
+    for (; tb + P <= nt; tb += P) {
+#pragma unroll
+      for (int s = 0; s < P; ++s) token(tb + s, s);
     }
+#pragma unroll
+    for (int s = 0; s < P - 1; ++s)
+      if (tb + s < nt) token(tb + s, s);
     if (cbase + lane < nt) zr[cbase + lane] = cn;
+    flush_delta(cw, cz, cn);          // lanes past the range end keep cn == cz
 #pragma unroll
     for (int j = 0; j < C; ++j) nd[lane * C + j] = 0;
     wave_lds_fence();
