@@ -613,27 +613,26 @@ void k_sample(SampleParams p) {
 #endif
         }
 
-        // keep the pipeline full: token t+P.  Unconditional (past the range
-        // end pw/pz hold stale but valid word / topic ids), so that every
-        // token issues the same loads and row t+1 stays in flight at token t
-        if (LDA_CHUNK_DELTA || t + P < nt) {
-          const int wp = readlane_i(pw, idx);
-          load_row16<C>(rows[s], nw16 + (int64_t)wp * KP, lane);
-          if (!FROZEN && !kInvM1Lds) cinv_r[s] = inv_m1[readlane_i(pz, idx)];
-        }
     };
-    // Whole groups of P tokens, then the tail: no exit inside a group, so
-    // that every CFG path round the loop issues the same P row loads (an
-    // early break becomes a flag path that skips a slot's load, and the
-    // compiler's vmcnt for the next row is then 0)
-    int tb = 0;
-    for (; tb + P <= nt; tb += P) {
+    // keep the pipeline full: the row of token t+P into slot s
+    auto prefetch = [&](const int t, const int s) __attribute__((always_inline)) {
+      const int idx = (t - cbase) & 63;
+      const int wp = readlane_i(pw, idx);
+      load_row16<C>(rows[s], nw16 + (int64_t)wp * KP, lane);
+      if (!FROZEN && !kInvM1Lds) cinv_r[s] = inv_m1[readlane_i(pz, idx)];
+    };
+    // The prefetch is issued for every slot, also past the range end (pw/pz
+    // hold stale but valid word / topic ids there), and the loop has no exit
+    // inside a group: every CFG path round the loop then issues the same P
+    // row loads, and the compiler waits vmcnt(P-1) for a row instead of 0
+    // (an early break becomes a flag path that skips a slot's load)
+    for (int tb = 0; tb < nt; tb += P) {
 #pragma unroll
-      for (int s = 0; s < P; ++s) token(tb + s, s);
+      for (int s = 0; s < P; ++s) {
+        if (tb + s < nt) token(tb + s, s);
+        prefetch(tb + s, s);
+      }
     }
-#pragma unroll
-    for (int s = 0; s < P - 1; ++s)
-      if (tb + s < nt) token(tb + s, s);
     if (cbase + lane < nt) zr[cbase + lane] = cn;
     flush_delta(cw, cz, cn);          // lanes past the range end keep cn == cz
 #pragma unroll
