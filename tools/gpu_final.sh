@@ -12,7 +12,7 @@ timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.
 tail -1 $O/smoke.log
 PASSES="kt fetch write tcc sq lds" LABEL=final_c4 bash tools/profile.sh > $O/profile.log 2>&1 || { echo PROFILE FAILED; tail -20 $O/profile.log; exit 1; }
 cp gpurun_out/prof_final_c4/summary_*.json gpurun_out/prof_final_c4/*kernel_stats.csv $O/ 2>/dev/null
-python3 tools/make_traffic.py gpurun_out/prof_final_c4 "k_sample<8, 2, false>" 250000000 c4 $O/traffic_k512.json || { echo TRAFFIC FAILED; exit 1; }
+python3 tools/make_traffic.py gpurun_out/prof_final_c4 "k_sample<8, 3, false>" 250000000 c4 $O/traffic_k512.json || { echo TRAFFIC FAILED; exit 1; }
 cp $O/traffic_k512.json profiles/r01/traffic_k512.json
 for cfg in c4 c1 c2 c3 c5; do
   extra=""; [ $cfg != c4 ] && extra="--no-cpu-baseline"; [ $cfg = c1 ] && extra=""
@@ -20,3 +20,7 @@ for cfg in c4 c1 c2 c3 c5; do
   tail -1 $O/bench_$cfg.log > $O/bench_$cfg.jsonl
   python3 -c "import json;d=json.loads(open('$O/bench_$cfg.jsonl').read());r=d['roofline'];print('$cfg', round(d['value']/1e9,4),'Gtok/s', round(d['ms_per_step'],3),'ms/step kernel',round(r['kernel_ms_timed_region'],3),'traffic',r['traffic'])"
 done
+# the C4 rate after 30 burn-in sweeps (counts concentrated; no traffic file for it)
+timeout -k 10 600 python bench.py --config c4 --burnin 30 --no-cpu-baseline > $O/bench_c4_b30.log 2>&1 || { echo "BENCH c4 b30 FAILED"; tail -5 $O/bench_c4_b30.log; exit 1; }
+tail -1 $O/bench_c4_b30.log > $O/bench_c4_b30.jsonl
+python3 -c "import json;d=json.loads(open('$O/bench_c4_b30.jsonl').read());print('c4 burnin 30', round(d['value']/1e9,4),'Gtok/s')"
