@@ -313,3 +313,31 @@ def test_dense_escaped_counts(oracle, K):
     nw = g.counts()[0]
     assert (nw >= 255).sum() >= 1 and ((nw > 0) & (nw < 255)).sum() > 100
     _assert_same_state(g, o)
+
+
+@pytest.mark.parametrize("kind", KINDS)
+@pytest.mark.parametrize("K", [20, 512, 1024])
+def test_range_tails_and_chunk_edges(oracle, K, kind):
+    # one document per work range (tokens_per_range=1), so every range length
+    # below occurs: fewer tokens than the prefetch depth P (the sampler then
+    # prefetches past the range end from stale but valid word ids), and
+    # documents ending just before, at and after the 64-token chunk edges
+    lens = list(range(0, 10)) + [62, 63, 64, 65, 66, 126, 127, 128, 129, 130,
+                                 190, 191, 192, 193, 194, 255, 256, 257]
+    rng = np.random.default_rng(K)
+    lens = np.array(lens * 2, dtype=np.int64)
+    rng.shuffle(lens)
+    off = np.zeros(len(lens) + 1, dtype=np.int64)
+    np.cumsum(lens, out=off[1:])
+    V = 300
+    words = rng.integers(0, V, size=int(off[-1])).astype(np.int32)
+    corpus = Corpus(off, words, V)
+    alpha = np.full(K, 0.1)
+    g, o = _pair(oracle, corpus, K, alpha, 0.01, seed=77 + K, tokens_per_range=1, kind=kind)
+    g.sweep(0)
+    o.apply()
+    _assert_same_state(g, o)
+    for n in (1, 2):
+        g.sweep(n)
+        o.sweep(n)
+        _assert_same_state(g, o)
