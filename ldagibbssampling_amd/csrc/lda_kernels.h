@@ -15,8 +15,12 @@ constexpr uint32_t STREAM_INFER = 2u;
 // Row-prefetch depth of the sampler per C = Kp/64 (tokens in flight per wave;
 // C = 8: P = 3 is +1% over 2 on C4 once the pipeline waits vmcnt(P-1), P = 4
 // spills; C = 16: 3 is within noise of 2).
+#ifndef SAMPLE_P1
 #define SAMPLE_P1 4
+#endif
+#ifndef SAMPLE_P2
 #define SAMPLE_P2 4
+#endif
 #ifndef SAMPLE_P4
 #define SAMPLE_P4 4
 #endif
