@@ -102,6 +102,9 @@ __device__ __forceinline__ float dpp_mov(float v) {
 #ifndef LDA_CHUNK_DELTA
 #define LDA_CHUNK_DELTA 1
 #endif
+#ifndef LDA_SALU_COUNT
+#define LDA_SALU_COUNT 1
+#endif
 // s_waitcnt vmcnt(0) (gfx9 encoding: expcnt and lgkmcnt left at their maxima)
 constexpr int kVmcnt0 = 0x0F70;
 // (a != b) ? m : 0 as s_cmp + s_cselect_b64
@@ -143,6 +146,13 @@ __device__ __forceinline__ uint64_t select_mask(int jo, int j, uint64_t m) {
   jo = __builtin_amdgcn_readfirstlane(jo);
   asm("s_cmp_eq_u32 %1, %2\n\ts_cselect_b64 %0, %3, 0" : "=s"(r) : "s"(jo), "s"(j), "s"(m) : "scc");
   return r;
+}
+// c + bit l of m (s_bitcmp1_b64 sets SCC, s_addc_u32 adds it)
+__device__ __forceinline__ int add_lane_bit(int c, uint64_t m, int l) {
+  l = __builtin_amdgcn_readfirstlane(l);
+  c = __builtin_amdgcn_readfirstlane(c);
+  asm("s_bitcmp1_b64 %1, %2\n\ts_addc_u32 %0, %0, 0" : "+s"(c) : "s"(m), "s"(l) : "scc");
+  return c;
 }
 __device__ __forceinline__ float wave_incl_scan(float x) {
   x = dpp_mov<0x111, 0xf, true>(x) + x;
@@ -571,6 +581,22 @@ void k_sample(SampleParams p) {
         // T of lane lstar - 1 (0 for lane 0): the scan shifted one lane up
         const float E = readlane_f(dpp_mov<0x138, 0xf, true>(T), lstar);
         // every lane counts its own prefix against lane lstar's E; lstar's count is the one used
+#if LDA_SALU_COUNT
+        // one compare per element straight into a lane mask, and lane l*'s
+        // bit added on the scalar unit (s_bitcmp1 + s_addc): 12 VALU for the
+        // count at C = 8 instead of 21
+        int cnt = 0;
+        if constexpr (C >= 2) {
+#pragma unroll
+          for (int j = 0; j < C; j += 2) {
+            const pkf32 es = (pkf32){E, E} + (pkf32){S[j], S[j + 1]};
+            cnt = add_lane_bit(cnt, __ballot(es.x <= thr), lstar);
+            cnt = add_lane_bit(cnt, __ballot(es.y <= thr), lstar);
+          }
+        } else {
+          cnt = add_lane_bit(cnt, __ballot(E + S[0] <= thr), lstar);
+        }
+#else
         int cl = 0;
         if constexpr (C >= 2) {
           // E + S_j in packed pairs (each half an IEEE add)
@@ -584,6 +610,7 @@ void k_sample(SampleParams p) {
           cl = (E + S[0] <= thr) ? 1 : 0;
         }
         const int cnt = readlane_i(cl, lstar);
+#endif
         // cnt in [0, last valid topic of lstar] or C (padded topics add 0)
         const int lim = lstar < last_lane ? C - 1 : last_j_tail;
         const int jsel = cnt < lim ? cnt : lim;
