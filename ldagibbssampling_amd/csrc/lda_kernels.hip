@@ -486,9 +486,7 @@ void k_sample(SampleParams p) {
         float a[C];
         load_lds_f<C>(a, av + lane * C);
         const float cinv = FROZEN ? 0.0f : (kInvM1Lds ? t_invm1[zo] : cinv_r[s]);
-        // lane lo as a scalar lane mask (s_lshl), selected by inverse ballot
-        const uint64_t own_bit = 1ull << (uint32_t)__builtin_amdgcn_readfirstlane(lo);
-        const bool own_old = __builtin_amdgcn_inverse_ballot_w64(own_bit);
+        const bool own_old = (lane == lo);
 
         // word factors b = (float(c) + beta) * inv (packed fp32 pairs, each
         // half an ordinary IEEE add / mul); rows with a count > 65535 come
@@ -527,7 +525,7 @@ void k_sample(SampleParams p) {
         // one 64-bit lane mask per element: lane lo where j == jo, else none
         // (two SALU ops each; selecting under it is exact on lane lo, the
         // only lane whose value is used)
-        const uint64_t own_mask = own_bit;
+        const uint64_t own_mask = __ballot(own_old);
         uint64_t jmask[kGprIdx ? 1 : C];
         if constexpr (kGprIdx) {
           c_old = cfull[jo];
@@ -621,9 +619,7 @@ void k_sample(SampleParams p) {
         // the token goes back under kn with the next token's update
         kp = kn;
         inc = 1;
-        // lane idx <- kn (both scalar-unit results: no VALU-to-lane-select hazard)
-        // (the lane select goes through m0: one constant-bus read per VALU op)
-        asm("s_mov_b32 m0, %2\n\tv_writelane_b32 %0, %1, m0" : "+v"(cn) : "s"(kn), "s"(idx) : "m0");
+        cn = (lane == idx) ? kn : cn;
         if constexpr (!FROZEN && !LDA_CHUNK_DELTA) {
 #if LDA_UPD_MASK
           // lanes 0 and 1 when the topic changed: one s_cmp + s_cselect; the
