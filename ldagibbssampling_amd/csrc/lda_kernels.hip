@@ -105,6 +105,9 @@ __device__ __forceinline__ float dpp_mov(float v) {
 #ifndef LDA_SALU_COUNT
 #define LDA_SALU_COUNT 1
 #endif
+#ifndef LDA_WORD_FLAG
+#define LDA_WORD_FLAG 1
+#endif
 // s_waitcnt vmcnt(0) (gfx9 encoding: expcnt and lgkmcnt left at their maxima)
 constexpr int kVmcnt0 = 0x0F70;
 // (a != b) ? m : 0 as s_cmp + s_cselect_b64
@@ -383,7 +386,18 @@ void k_sample(SampleParams p) {
       w2 = wrd[128 + lane];
       z2 = zr[128 + lane];
     }
-    int cf = (int)wide_of[cw], f1 = (int)wide_of[w1];
+    // kWordFlag: the int32-row flag rides in bit 31 of the word registers
+    // (one readlane per token for both; word ids are < 2^31)
+    constexpr bool kWordFlag = LDA_WORD_FLAG;
+    constexpr int kWordMask = 0x7FFFFFFF;
+    int cf = 0, f1 = 0;
+    if constexpr (kWordFlag) {
+      cw |= (int)wide_of[cw] << 31;
+      w1 |= (int)wide_of[w1] << 31;
+    } else {
+      cf = (int)wide_of[cw];
+      f1 = (int)wide_of[w1];
+    }
     int cn = cz;
     float cu = u01(draw_u32(gbase + (uint64_t)lane, p.c2, p.c3, p.k0, p.k1));
     // word (and, for the inv_m1 prefetch, topic) of token cbase + lane + P:
@@ -412,7 +426,7 @@ void k_sample(SampleParams p) {
     float cinv_r[P];
 #pragma unroll
     for (int s = 0; s < P; ++s) {
-      const int wp = (s < nt) ? readlane_i(cw, s) : 0;
+      const int wp = (s < nt) ? (readlane_i(cw, s) & kWordMask) : 0;
       load_row16<C>(rows[s], nw16 + (int64_t)wp * KP, lane);
       if (!FROZEN && !kInvM1Lds) cinv_r[s] = inv_m1[(s < nt) ? readlane_i(cz, s) : 0];
     }
@@ -426,14 +440,15 @@ void k_sample(SampleParams p) {
             // chunk switch: publish the finished chunk's new z and count
             // changes, shift
             zr[cbase + lane] = cn;
-            flush_delta(cw, cz, cn);
+            flush_delta(cw & kWordMask, cz, cn);
             cbase += 64;
             cw = w1;
             cz = z1;
             cf = f1;
             w1 = w2;
             z1 = z2;
-            f1 = (int)wide_of[w1];
+            if constexpr (kWordFlag) w1 |= (int)wide_of[w1] << 31;
+            else f1 = (int)wide_of[w1];
             cn = cz;
             cu = u01(draw_u32(gbase + (uint64_t)(cbase + lane), p.c2, p.c3, p.k0, p.k1));
             if (cbase + 128 + lane < nt) {
@@ -461,10 +476,11 @@ void k_sample(SampleParams p) {
         }
         const int idx = t - cbase;
 
-        const int w = readlane_i(cw, idx);
+        const int wf = readlane_i(cw, idx);
+        const int w = wf & kWordMask;
         const int zo = readlane_i(cz, idx);
         const float u = readlane_f(cu, idx);
-        const bool wide = readlane_i(cf, idx) != 0;
+        const bool wide = kWordFlag ? wf < 0 : readlane_i(cf, idx) != 0;
 #if LDA_SALU_TRIM
         const int lo = (int)((uint32_t)zo / C), jo = (int)((uint32_t)zo % C);
 #else
@@ -644,7 +660,7 @@ void k_sample(SampleParams p) {
     // keep the pipeline full: the row of token t+P into slot s
     auto prefetch = [&](const int t, const int s) __attribute__((always_inline)) {
       const int idx = (t - cbase) & 63;
-      const int wp = readlane_i(pw, idx);
+      const int wp = readlane_i(pw, idx) & kWordMask;
       load_row16<C>(rows[s], nw16 + (int64_t)wp * KP, lane);
       if (!FROZEN && !kInvM1Lds) cinv_r[s] = inv_m1[readlane_i(pz, idx)];
     };
@@ -661,7 +677,7 @@ void k_sample(SampleParams p) {
       }
     }
     if (cbase + lane < nt) zr[cbase + lane] = cn;
-    flush_delta(cw, cz, cn);          // lanes past the range end keep cn == cz
+    flush_delta(cw & kWordMask, cz, cn);   // lanes past the range end keep cn == cz
 #pragma unroll
     for (int j = 0; j < C; ++j) nd[lane * C + j] = 0;
     wave_lds_fence();
