@@ -502,7 +502,9 @@ void k_sample(SampleParams p) {
         float a[C];
         load_lds_f<C>(a, av + lane * C);
         const float cinv = FROZEN ? 0.0f : (kInvM1Lds ? t_invm1[zo] : cinv_r[s]);
-        const bool own_old = (lane == lo);
+        // lane lo as a scalar lane mask (s_lshl_b64), selected by inverse ballot
+        const uint64_t own_bit = 1ull << (uint32_t)__builtin_amdgcn_readfirstlane(lo);
+        const bool own_old = __builtin_amdgcn_inverse_ballot_w64(own_bit);
 
         // word factors b = (float(c) + beta) * inv (packed fp32 pairs, each
         // half an ordinary IEEE add / mul); rows with a count > 65535 come
@@ -541,7 +543,7 @@ void k_sample(SampleParams p) {
         // one 64-bit lane mask per element: lane lo where j == jo, else none
         // (two SALU ops each; selecting under it is exact on lane lo, the
         // only lane whose value is used)
-        const uint64_t own_mask = __ballot(own_old);
+        const uint64_t own_mask = own_bit;
         uint64_t jmask[kGprIdx ? 1 : C];
         if constexpr (kGprIdx) {
           c_old = cfull[jo];
@@ -635,7 +637,8 @@ void k_sample(SampleParams p) {
         // the token goes back under kn with the next token's update
         kp = kn;
         inc = 1;
-        cn = (lane == idx) ? kn : cn;
+        // lane idx <- kn under a scalar lane mask (no per-lane compare)
+        cn = __builtin_amdgcn_inverse_ballot_w64(1ull << (uint32_t)idx) ? kn : cn;
         if constexpr (!FROZEN && !LDA_CHUNK_DELTA) {
 #if LDA_UPD_MASK
           // lanes 0 and 1 when the topic changed: one s_cmp + s_cselect; the
