@@ -138,12 +138,15 @@ lda_status lda_set_alpha_beta(lda_ctx* ctx, const double* alpha, double beta);
 lda_status lda_log_likelihood_parts(lda_ctx* ctx, double* doc_part, double* word_part);
 lda_status lda_log_likelihood(lda_ctx* ctx, double* out); /* doc_part + word_part */
 
-/* TopicInferencer.getSampledDistribution(instance, n_iter, thin, burn_in)
- * [src/cmu_ron/TrainAndPredict.java:144] batched over Dh held-out documents
- * against the frozen model (out-of-vocabulary tokens removed by the caller).
+/* TopicInferencer.getSampledDistribution(instance, numIterations, thinning,
+ * burnIn) [src/cmu_ron/TrainAndPredict.java:144, src/cmu/TrainAndPredict.java:114]
+ * batched over Dh held-out documents against the frozen model; the arguments
+ * are in Mallet's order.  Word ids must be < V (out-of-vocabulary tokens are
+ * removed by the caller); tokens whose type has no training tokens (an empty
+ * typeTopicCounts row) are skipped, as Mallet's inferencer skips them.
  * theta[Dh*K] (fp64, rows sum to 1). */
 lda_status lda_infer(lda_ctx* ctx, int64_t Dh, const int64_t* doc_off, const int32_t* words,
-                     int32_t n_iter, int32_t burn_in, int32_t thin, uint64_t seed,
+                     int32_t num_iterations, int32_t thinning, int32_t burn_in, uint64_t seed,
                      double* theta);
 
 /* Mallet-layout adapter: typeTopicCounts as packed (count << topic_bits) |

@@ -715,25 +715,45 @@ lda_status lda_row_stats(lda_ctx* c, double* mean_row_nnz) {
   return LDA_OK;
 }
 
-lda_status lda_infer(lda_ctx* c, int64_t Dh, const int64_t* doc_off, const int32_t* words,
-                     int32_t n_iter, int32_t burn_in, int32_t thin, uint64_t seed, double* theta) {
+lda_status lda_infer(lda_ctx* c, int64_t Dh, const int64_t* doc_off, const int32_t* words_in,
+                     int32_t n_iter, int32_t thin, int32_t burn_in, uint64_t seed, double* theta) {
   if (!c || !doc_off || !theta) return fail(LDA_ERR_INVALID_ARG, "null argument");
   if (Dh < 0 || n_iter < 0 || burn_in < 0 || thin < 1) return fail(LDA_ERR_INVALID_ARG, "bad sizes");
   if (c->pending) return fail(LDA_ERR_STATE, "inference with a pending delta: call lda_apply first");
+  for (int64_t d = 1; d <= Dh; ++d)
+    if (doc_off[d] < doc_off[d - 1]) return fail(LDA_ERR_INVALID_ARG, "doc_off not monotone");
+  const int64_t N_in = doc_off[Dh] - doc_off[0];
+  if (N_in > 0 && !words_in) return fail(LDA_ERR_INVALID_ARG, "words is null");
+  for (int64_t i = 0; i < N_in; ++i)
+    if (words_in[i] < 0 || words_in[i] >= c->V) return fail(LDA_ERR_INVALID_ARG, "word id out of range (OOV must be removed)");
+  HIP_TRY(hipSetDevice(c->device));
+  // TopicInferencer skips tokens whose type has no training tokens (an empty
+  // typeTopicCounts row): drop them here (row totals of the global snapshot)
   std::vector<int64_t> off(Dh + 1);
-  for (int64_t d = 0; d <= Dh; ++d) {
-    off[d] = doc_off[d] - doc_off[0];
-    if (d > 0 && off[d] < off[d - 1]) return fail(LDA_ERR_INVALID_ARG, "doc_off not monotone");
+  std::vector<int32_t> kept;
+  {
+    int32_t* caps = nullptr;
+    HIP_TRY(dalloc(&caps, c->V));
+    std::vector<int32_t> h(c->V);
+    hipError_t e = lda::launch_row_caps(c->nw, c->V, c->Kp, caps, c->stream);
+    if (e == hipSuccess) e = hipMemcpyAsync(h.data(), caps, sizeof(int32_t) * c->V, hipMemcpyDeviceToHost, c->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    (void)hipFree(caps);
+    HIP_TRY(e);
+    kept.reserve((size_t)N_in);
+    off[0] = 0;
+    for (int64_t d = 0; d < Dh; ++d) {
+      for (int64_t i = doc_off[d] - doc_off[0]; i < doc_off[d + 1] - doc_off[0]; ++i)
+        if (h[words_in[i]] > 0) kept.push_back(words_in[i]);
+      off[d + 1] = (int64_t)kept.size();
+    }
   }
+  const int32_t* words = kept.data();
   const int64_t N = off[Dh];
-  if (N > 0 && !words) return fail(LDA_ERR_INVALID_ARG, "words is null");
-  for (int64_t i = 0; i < N; ++i)
-    if (words[i] < 0 || words[i] >= c->V) return fail(LDA_ERR_INVALID_ARG, "word id out of range (OOV must be removed)");
   if (c->Kp > 1024)
     for (int64_t d = 0; d < Dh; ++d)
       if (off[d + 1] - off[d] > LDA_MAX_DOC_TOKENS_BIGK)
         return fail(LDA_ERR_UNSUPPORTED, "document longer than 65535 tokens with num_topics > 1024");
-  HIP_TRY(hipSetDevice(c->device));
   int32_t *dw = nullptr, *dz = nullptr, *acc = nullptr, *q = nullptr;
   int64_t *doff = nullptr, *drange = nullptr;
   std::vector<int64_t> ranges = make_ranges(off, std::max<int64_t>(16, std::min<int64_t>(c->tokens_per_range, N / std::max<int64_t>(1, (int64_t)c->sample_blocks_frozen * c->waves_per_block * 8))));

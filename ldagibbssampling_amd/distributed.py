@@ -89,6 +89,13 @@ class ADLDATrainer:
             if self.sync_before_reduce:
                 self.engine.synchronize()
             self.dist.all_reduce(self._delta, op=self.dist.ReduceOp.SUM, group=self.group)
+            if self.sync_before_reduce and self._delta.device.type == "cuda":
+                # RCCL returns once the collective is enqueued (torch's current
+                # stream waits for it, the engine's own stream does not): the
+                # apply that follows must not read the delta before the sum
+                # has landed
+                import torch
+                torch.cuda.current_stream(self._delta.device).synchronize()
 
     def init_counts(self):
         """Global nw/nwsum from every rank's local counts (addInstances)."""

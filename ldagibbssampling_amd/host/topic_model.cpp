@@ -583,7 +583,8 @@ void ParallelTopicModel::infer(int64_t Dh, const int64_t* doc_off, const int32_t
   ensureShards();
   if (Dh < 0 || (Dh > 0 && (!doc_off || !theta))) raise(LDA_ERR_INVALID_ARG, "bad documents");
   // tokens of types unknown to the model are dropped (Mallet's inferencer
-  // skips type indices beyond its typeTopicCounts)
+  // skips type indices beyond its typeTopicCounts); lda_infer also skips
+  // known types without training tokens
   std::vector<int64_t> off((size_t)Dh + 1, 0);
   std::vector<int32_t> kept;
   for (int64_t d = 0; d < Dh; ++d) {
@@ -592,7 +593,7 @@ void ParallelTopicModel::infer(int64_t Dh, const int64_t* doc_off, const int32_t
     off[(size_t)d + 1] = (int64_t)kept.size();
   }
   check(lda_infer(shards_->ctx[0], Dh, off.data(), kept.empty() ? nullptr : kept.data(),
-                  num_iterations, burn_in, thinning, seed, theta),
+                  num_iterations, thinning, burn_in, seed, theta),
         "lda_infer");
 }
 

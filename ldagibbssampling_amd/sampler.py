@@ -37,8 +37,14 @@ class GibbsSampler:
         self.V = int(num_types)
         doc_off = np.ascontiguousarray(doc_off, dtype=np.int64)
         words = np.ascontiguousarray(words, dtype=np.int32)
+        if len(doc_off) < 1:
+            raise ValueError("doc_off needs at least one entry")
         self.D = len(doc_off) - 1
         self.N = int(doc_off[-1] - doc_off[0])
+        if len(words) < self.N:
+            raise ValueError(f"words holds {len(words)} ids, doc_off spans {self.N}")
+        if z_init is not None and len(z_init) != self.N:
+            raise ValueError(f"z_init must hold {self.N} topics")
         alpha = np.ascontiguousarray(np.broadcast_to(np.asarray(alpha, dtype=np.float64), (self.K,)))
         self._alpha = alpha
         cfg = capi.lda_config()
@@ -154,6 +160,8 @@ class GibbsSampler:
 
     def set_z(self, z):
         z = np.ascontiguousarray(z, dtype=np.int32)
+        if z.shape != (self.N,):
+            raise ValueError(f"z must hold {self.N} topics, got shape {z.shape}")
         capi.check(self._L.lda_set_z(self._h, z), "lda_set_z")
 
     def counts(self, with_nd: bool = False):
@@ -187,14 +195,20 @@ class GibbsSampler:
         capi.check(self._L.lda_log_likelihood(self._h, C.byref(out)), "lda_log_likelihood")
         return out.value
 
-    def infer(self, doc_off, words, n_iter: int = 100, burn_in: int = 10, thin: int = 10,
+    def infer(self, doc_off, words, n_iter: int = 100, thin: int = 10, burn_in: int = 10,
               seed: int = 0) -> np.ndarray:
+        """TopicInferencer.getSampledDistribution(inst, numIterations, thinning,
+        burnIn) over a batch of documents (positional order as Mallet's)."""
         doc_off = np.ascontiguousarray(doc_off, dtype=np.int64)
         words = np.ascontiguousarray(words, dtype=np.int32)
+        if len(doc_off) < 1:
+            raise ValueError("doc_off needs at least one entry")
+        if len(words) < int(doc_off[-1] - doc_off[0]):
+            raise ValueError("words is shorter than doc_off says")
         Dh = len(doc_off) - 1
         theta = np.zeros((Dh, self.K), dtype=np.float64)
-        capi.check(self._L.lda_infer(self._h, Dh, doc_off, words, int(n_iter), int(burn_in),
-                                     int(thin), int(seed) & (2**64 - 1), theta), "lda_infer")
+        capi.check(self._L.lda_infer(self._h, Dh, doc_off, words, int(n_iter), int(thin),
+                                     int(burn_in), int(seed) & (2**64 - 1), theta), "lda_infer")
         return theta
 
     # ------------------------------------------- hyperparameter statistics

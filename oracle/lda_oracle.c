@@ -16,6 +16,7 @@
 #include <pthread.h>
 #include <stdlib.h>
 #include <string.h>
+#include <unistd.h>
 
 /* ======================================================================== */
 /* Philox4x32-10 — Salmon, Moraes, Dror, Shaw, "Parallel random numbers: as  */
@@ -320,6 +321,18 @@ void orc_exact_apply(orc_exact* s) {
   exact_prepare_topics(s);
 }
 
+/* Replace the snapshot by an external global one (nw[V*K] unpadded, nwsum[K]):
+ * checks a slice of a larger corpus against the GPU's state of that corpus. */
+void orc_exact_load_snapshot(orc_exact* s, const int32_t* nw, const int32_t* nwsum) {
+  memset(s->nw, 0, sizeof(int32_t) * (size_t)s->V * s->Kp);
+  memset(s->nwsum, 0, sizeof(int32_t) * s->Kp);
+  memset(s->delta, 0, sizeof(int32_t) * ((size_t)s->V * s->Kp + s->Kp));
+  for (int w = 0; w < s->V; ++w)
+    memcpy(s->nw + (size_t)w * s->Kp, nw + (size_t)w * s->K, sizeof(int32_t) * s->K);
+  memcpy(s->nwsum, nwsum, sizeof(int32_t) * s->K);
+  exact_prepare_topics(s);
+}
+
 void orc_exact_set_alpha_beta(orc_exact* s, const double* alpha, double beta) {
   memcpy(s->alpha, alpha, sizeof(double) * s->K);
   s->beta = beta;
@@ -508,15 +521,17 @@ static int exact_draw_sparse(const orc_exact* s, const int32_t* nwrow, const int
   return lstar * C + jsel;
 }
 
-/* Sample the docs [d0, d1) of a token stream against the snapshot. */
+/* Sample the docs [d0, d1) of a token stream against the snapshot.  frozen:
+ * no self-correction (inference).  The snapshot is read-only and nd is per
+ * document, so disjoint document blocks are independent; the count changes
+ * are derived afterwards from the old and new z (exact_sample_stream). */
 static void exact_sample_docs(const orc_exact* s, const int64_t* doc_off, const int32_t* words,
                               int32_t* z, int64_t d0, int64_t d1, int frozen, uint32_t c2,
-                              uint32_t c3, int64_t token_base, int32_t* delta) {
+                              uint32_t c3, int64_t token_base) {
   int32_t* nd = (int32_t*)calloc(s->Kp, sizeof(int32_t));
   float* S = (float*)malloc(sizeof(float) * s->Kp);
   int32_t* et = (int32_t*)malloc(sizeof(int32_t) * s->Kp);
   int32_t* ec = (int32_t*)malloc(sizeof(int32_t) * s->Kp);
-  int32_t* dsum = delta ? delta + (size_t)s->V * s->Kp : NULL;
   for (int64_t d = d0; d < d1; ++d) {
     memset(nd, 0, sizeof(int32_t) * s->Kp);
     for (int64_t i = doc_off[d]; i < doc_off[d + 1]; ++i) nd[z[i]]++;
@@ -530,12 +545,6 @@ static void exact_sample_docs(const orc_exact* s, const int64_t* doc_off, const 
                    : exact_draw(s, s->nw + (size_t)w * s->Kp, nd, frozen ? -1 : zo, u, S);
       nd[kn]++;
       z[i] = kn;
-      if (!frozen && kn != zo) {
-        delta[(size_t)w * s->Kp + zo] -= 1;
-        delta[(size_t)w * s->Kp + kn] += 1;
-        dsum[zo] -= 1;
-        dsum[kn] += 1;
-      }
     }
   }
   free(nd);
@@ -544,9 +553,85 @@ static void exact_sample_docs(const orc_exact* s, const int64_t* doc_off, const 
   free(ec);
 }
 
+/* Worker threads over contiguous document blocks (ORACLE_THREADS, default
+ * min(16, online CPUs)): the result does not depend on the split. */
+typedef struct {
+  const orc_exact* s;
+  const int64_t* doc_off;
+  const int32_t* words;
+  int32_t* z;
+  int64_t d0, d1;
+  int frozen;
+  uint32_t c2, c3;
+  int64_t token_base;
+} exact_job;
+
+static void* exact_job_run(void* arg) {
+  exact_job* j = (exact_job*)arg;
+  exact_sample_docs(j->s, j->doc_off, j->words, j->z, j->d0, j->d1, j->frozen, j->c2, j->c3,
+                    j->token_base);
+  return NULL;
+}
+
+static int oracle_threads(void) {
+  const char* e = getenv("ORACLE_THREADS");
+  long t = e ? atol(e) : sysconf(_SC_NPROCESSORS_ONLN);
+  if (t < 1) t = 1;
+  if (t > 16) t = 16;
+  return (int)t;
+}
+
+static void exact_sample_stream(const orc_exact* s, const int64_t* doc_off, const int32_t* words,
+                                int32_t* z, int64_t D, int frozen, uint32_t c2, uint32_t c3,
+                                int64_t token_base, int32_t* delta) {
+  const int64_t N = doc_off[D] - doc_off[0];
+  int32_t* zold = NULL;
+  if (delta) {
+    zold = (int32_t*)malloc(sizeof(int32_t) * (N ? N : 1));
+    memcpy(zold, z + doc_off[0], sizeof(int32_t) * N);
+  }
+  int T = oracle_threads();
+  if ((int64_t)T > D) T = (int)(D > 0 ? D : 1);
+  if (T <= 1 || N < 4096) {
+    exact_sample_docs(s, doc_off, words, z, 0, D, frozen, c2, c3, token_base);
+  } else {
+    pthread_t* th = (pthread_t*)malloc(sizeof(pthread_t) * T);
+    exact_job* jobs = (exact_job*)malloc(sizeof(exact_job) * T);
+    int64_t d = 0;
+    for (int t = 0; t < T; ++t) {
+      /* token-balanced cut: the first document starting at or after t*N/T */
+      const int64_t target = doc_off[0] + N * (t + 1) / T;
+      int64_t e = d;
+      while (e < D && doc_off[e] < target) ++e;
+      if (t == T - 1) e = D;
+      exact_job j = {s, doc_off, words, z, d, e, frozen, c2, c3, token_base};
+      jobs[t] = j;
+      d = e;
+    }
+    for (int t = 0; t < T; ++t) pthread_create(&th[t], NULL, exact_job_run, &jobs[t]);
+    for (int t = 0; t < T; ++t) pthread_join(th[t], NULL);
+    free(th);
+    free(jobs);
+  }
+  if (delta) {
+    int32_t* dsum = delta + (size_t)s->V * s->Kp;
+    for (int64_t i = 0; i < N; ++i) {
+      const int zo = zold[i], kn = z[doc_off[0] + i];
+      if (kn != zo) {
+        const size_t row = (size_t)words[doc_off[0] + i] * s->Kp;
+        delta[row + zo] -= 1;
+        delta[row + kn] += 1;
+        dsum[zo] -= 1;
+        dsum[kn] += 1;
+      }
+    }
+    free(zold);
+  }
+}
+
 void orc_exact_sample(orc_exact* s, int frozen) {
-  exact_sample_docs(s, s->doc_off, s->words, s->z, 0, s->D, frozen, s->sweep, STREAM_SAMPLE,
-                    s->token_base, frozen ? NULL : s->delta);
+  exact_sample_stream(s, s->doc_off, s->words, s->z, s->D, frozen, s->sweep, STREAM_SAMPLE,
+                      s->token_base, frozen ? NULL : s->delta);
   s->sweep++;
 }
 
@@ -628,10 +713,22 @@ double orc_exact_log_likelihood(const orc_exact* s) {
 
 void orc_exact_infer(const orc_exact* s, int64_t Dh, const int64_t* doc_off, const int32_t* words,
                      int32_t n_iter, int32_t burn_in, int32_t thin, uint64_t seed, double* theta) {
-  int64_t N = doc_off[Dh] - doc_off[0];
+  /* TopicInferencer skips tokens whose type has no training tokens (an empty
+   * typeTopicCounts row): keep only tokens of words with a nonzero total */
+  const int64_t N_in = doc_off[Dh] - doc_off[0];
   int64_t* off = (int64_t*)malloc(sizeof(int64_t) * (Dh + 1));
-  for (int64_t d = 0; d <= Dh; ++d) off[d] = doc_off[d] - doc_off[0];
-  const int32_t* w = words;
+  int32_t* w = (int32_t*)malloc(sizeof(int32_t) * (N_in ? N_in : 1));
+  int64_t N = 0;
+  off[0] = 0;
+  for (int64_t d = 0; d < Dh; ++d) {
+    for (int64_t i = doc_off[d] - doc_off[0]; i < doc_off[d + 1] - doc_off[0]; ++i) {
+      const int32_t* row = s->nw + (size_t)words[i] * s->Kp;
+      int64_t tot = 0;
+      for (int k = 0; k < s->K; ++k) tot += row[k];
+      if (tot > 0) w[N++] = words[i];
+    }
+    off[d + 1] = N;
+  }
   int32_t* z = (int32_t*)malloc(sizeof(int32_t) * (N ? N : 1));
   /* TopicInferencer init: the most frequent topic of the word in the model
    * (packed rows are sorted by (count << bits | topic), so ties go to the
@@ -648,7 +745,7 @@ void orc_exact_infer(const orc_exact* s, int64_t Dh, const int64_t* doc_off, con
   orc_exact tmp = *s;
   tmp.seed = seed;
   for (int32_t it = 1; it <= n_iter; ++it) {
-    exact_sample_docs(&tmp, off, w, z, 0, Dh, 1, (uint32_t)(it - 1), STREAM_INFER, 0, NULL);
+    exact_sample_stream(&tmp, off, w, z, Dh, 1, (uint32_t)(it - 1), STREAM_INFER, 0, NULL);
     if (it > burn_in && (it - burn_in) % thin == 0) {
       nsamples++;
       for (int64_t d = 0; d < Dh; ++d)
@@ -671,6 +768,7 @@ void orc_exact_infer(const orc_exact* s, int64_t Dh, const int64_t* doc_off, con
   }
   free(acc);
   free(z);
+  free(w);
   free(off);
 }
 

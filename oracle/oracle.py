@@ -72,6 +72,7 @@ def lib():
     L.orc_exact_apply.argtypes = [C.c_void_p]
     L.orc_exact_set_alpha_beta.argtypes = [C.c_void_p, _f64p, C.c_double]
     L.orc_exact_set_sweep.argtypes = [C.c_void_p, C.c_uint32]
+    L.orc_exact_load_snapshot.argtypes = [C.c_void_p, _i32p, _i32p]
     L.orc_exact_set_kind.argtypes = [C.c_void_p, C.c_int]
     L.orc_exact_get_sweep.restype = C.c_uint32
     L.orc_exact_get_sweep.argtypes = [C.c_void_p]
@@ -220,6 +221,20 @@ class ExactSampler:
     @property
     def sweep_index(self) -> int:
         return int(lib().orc_exact_get_sweep(self._h))
+
+    @sweep_index.setter
+    def sweep_index(self, v: int):
+        lib().orc_exact_set_sweep(self._h, int(v))
+
+    def load_snapshot(self, nw, nwsum):
+        """Replace the snapshot by a global one (nw [V, K], nwsum [K]); drops
+        the pending delta (a slice of a larger corpus, checked against the
+        GPU's state of that corpus)."""
+        nw = np.ascontiguousarray(nw, dtype=np.int32)
+        nwsum = np.ascontiguousarray(nwsum, dtype=np.int32)
+        assert nw.shape == (self.V, self.K) and nwsum.shape == (self.K,)
+        lib().orc_exact_load_snapshot(self._h, nw, nwsum)
+        self._pending = False
 
     def set_alpha_beta(self, alpha, beta):
         a = np.ascontiguousarray(np.broadcast_to(np.asarray(alpha, dtype=np.float64), (self.K,)))

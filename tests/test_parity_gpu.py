@@ -297,22 +297,41 @@ def test_wide_rows_escape(oracle, kind):
 
 
 @pytest.mark.parametrize("K", [20, 512, 1024])
-def test_dense_escaped_counts(oracle, K):
-    """Counts from 255 up: the dense sampler's 8-bit rows mark them 255 and
-    the lane reads its exact int32 slice (mixed escaped / plain lanes)."""
+def test_dense_16bit_row_boundary(oracle, K):
+    """Counts at the 16-bit row's edge: a cell of exactly 65535 (the largest
+    count the 16-bit row holds; its own-token correction reads 65534) beside
+    cells of 65536-65538 (the word's row is flagged wide and read from the
+    int32 row), with counts crossing the boundary in both directions over the
+    sweeps."""
     from ldagibbssampling_amd.corpus import Corpus
-    D, L = 60, 500
+    D, L = 4, 50000
     rng = np.random.default_rng(K)
-    words = np.where(rng.random(D * L) < 0.5, rng.integers(0, 3, D * L),
-                     rng.integers(3, 200, D * L)).astype(np.int32)
-    c = Corpus(np.arange(D + 1, dtype=np.int64) * L, words, 200)
-    z0 = np.where(rng.random(D * L) < 0.7, 7, rng.integers(0, K, D * L)).astype(np.int32)
-    g, o = _pair(oracle, c, K, np.full(K, 0.1), 0.01, seed=K + 5, z_init=z0)
-    g.sweep(3)
-    o.sweep(3)
+    n0, n1 = 65535 + 40, 65537 + 40          # tokens of word 0 and word 1
+    words = np.concatenate([np.zeros(n0, np.int32), np.ones(n1, np.int32),
+                            rng.integers(2, 300, D * L - n0 - n1).astype(np.int32)])
+    z0 = np.concatenate([np.full(n0, 3), np.full(n1, 5),
+                         rng.integers(0, K, D * L - n0 - n1)]).astype(np.int32)
+    z0[:40] = 4                                # word 0: topic 3 holds exactly 65535
+    z0[n0:n0 + 40] = 6                         # word 1: topic 5 holds 65537
+    perm = rng.permutation(D * L)
+    c = Corpus(np.arange(D + 1, dtype=np.int64) * L, words[perm], 300)
+    # a tiny alpha and beta keep most tokens on their topic: the cells move a
+    # few counts per sweep around the boundary
+    g, o = _pair(oracle, c, K, np.full(K, 1e-3), 1e-4, seed=K + 5, z_init=z0[perm])
+    g.sweep(0)
+    o.apply()
     nw = g.counts()[0]
-    assert (nw >= 255).sum() >= 1 and ((nw > 0) & (nw < 255)).sum() > 100
-    _assert_same_state(g, o)
+    assert nw[0, 3] == 65535 and nw[1, 5] == 65537
+    _assert_same_state(g, o, with_nd=False)
+    seen_lo = seen_hi = False
+    for _ in range(4):
+        g.sweep(1)
+        o.sweep(1)
+        _assert_same_state(g, o, with_nd=False)
+        nw = g.counts()[0]
+        seen_lo |= nw[1, 5] <= 65535
+        seen_hi |= nw[0, 3] > 65535 or nw[1, 5] > 65535
+    assert seen_hi
 
 
 @pytest.mark.parametrize("kind", KINDS)
@@ -341,3 +360,43 @@ def test_range_tails_and_chunk_edges(oracle, K, kind):
         g.sweep(n)
         o.sweep(n)
         _assert_same_state(g, o)
+
+
+@pytest.mark.parametrize("kind", KINDS)
+def test_inference_skips_types_without_training_tokens(oracle, kind):
+    """Held-out tokens of in-vocabulary types that have no training tokens
+    (Mallet allocates them an empty typeTopicCounts row, and its inferencer
+    skips them): dropped on the GPU as in cpu_exact; a document made only of
+    such tokens gets theta = alpha / alphaSum, as in cpu_mallet."""
+    c = synthetic_lda(num_docs=120, num_types=800, num_topics=32, doc_len=None, mean_len=50,
+                      min_len=2, max_len=120, seed=12)
+    V = c.num_types + 50                       # 50 types never seen in training
+    K = 32
+    alpha = np.full(K, 0.1)
+    from ldagibbssampling_amd.sampler import GibbsSampler
+    g = GibbsSampler(K, V, c.doc_off, c.words, alpha, 0.01, seed=2, sampler=kind)
+    o = oracle.ExactSampler(K, V, c.doc_off, c.words, alpha, 0.01, 2,
+                            kind="sparse" if kind == "sparse" else "dense")
+    g.sweep(5)
+    o.sweep(5)
+    rng = np.random.default_rng(3)
+    unseen = np.arange(c.num_types, V, dtype=np.int32)
+    docs = [rng.choice(unseen, 9),                                          # only unseen types
+            np.concatenate([rng.integers(0, c.num_types, 30), rng.choice(unseen, 10)]),
+            rng.integers(0, c.num_types, 25)]
+    docs = [d.astype(np.int32) for d in docs]
+    off = np.zeros(len(docs) + 1, np.int64)
+    np.cumsum([len(d) for d in docs], out=off[1:])
+    words = np.concatenate(docs)
+    tg = g.infer(off, words, n_iter=20, burn_in=4, thin=4, seed=5)
+    to = o.infer(off, words, n_iter=20, burn_in=4, thin=4, seed=5)
+    np.testing.assert_allclose(tg, to, rtol=0, atol=1e-12)
+    np.testing.assert_allclose(tg[0], alpha / alpha.sum(), rtol=0, atol=1e-15)
+    # the mixed document equals the same document with its unseen tokens removed
+    t_clean = g.infer(np.array([0, 30], np.int64), docs[1][:30], n_iter=20, burn_in=4, thin=4,
+                      seed=5)
+    m = oracle.MalletModel(K, alpha.sum(), 0.01, V, c.doc_off, c.words, seed=1)
+    m.estimate(5)
+    tm = m.infer(off[:2], docs[0], n_iter=20, burn_in=4, thin=4, seed=5)
+    np.testing.assert_allclose(tm[0], alpha / alpha.sum(), rtol=0, atol=1e-15)
+    np.testing.assert_array_equal(tg[1], t_clean[0])
