@@ -59,7 +59,18 @@ lda_status ldatm_set_random_seed(ldatm* m, int64_t seed);      /* setRandomSeed 
  * min(n, visible devices) GPUs, RCCL all-reduce of the delta between them.
  * Results do not depend on it (integer deltas, global Philox counters). */
 lda_status ldatm_set_num_threads(ldatm* m, int32_t n);
-lda_status ldatm_set_sampler(ldatm* m, int32_t sampler);       /* LDA_SAMPLER_*      */
+/* LDA_SAMPLER_* (default: DENSE for K <= 1024, SPARSE above) */
+lda_status ldatm_set_sampler(ldatm* m, int32_t sampler);
+/* State a Java-side ParallelTopicModel already holds, for GpuParallelTopicModel
+ * (integration/): the topics Mallet's own addInstances drew (z[n], n = every
+ * token of the model), alpha[K] / alphaSum / beta after an earlier optimisation,
+ * and the Philox sweep counter, which must continue across estimate() calls
+ * (updateModel, src/cmu_ron/TrainAndPredict.java:173-177) so that a second
+ * estimate() does not replay the first one's uniforms. */
+lda_status ldatm_set_topics(ldatm* m, int64_t n, const int32_t* z);
+lda_status ldatm_set_hyper(ldatm* m, const double* alpha, double alpha_sum, double beta);
+lda_status ldatm_get_sweep(ldatm* m, uint32_t* sweep);
+lda_status ldatm_set_sweep(ldatm* m, uint32_t sweep);
 /* printLogLikelihood / logging: 0 = silent, 1 = Mallet's INFO lines on stderr */
 lda_status ldatm_set_verbosity(ldatm* m, int32_t level);
 lda_status ldatm_set_print_log_likelihood(ldatm* m, int32_t on);

@@ -1,56 +1,73 @@
 package cmu_gpu;
 
 import java.io.IOException;
+import java.text.DecimalFormat;
 import java.util.logging.Logger;
 
 import cc.mallet.topics.ParallelTopicModel;
 import cc.mallet.topics.TopicAssignment;
-import cc.mallet.types.Dirichlet;
 import cc.mallet.types.FeatureSequence;
-import cc.mallet.types.LabelSequence;
 
 /**
- * Drop-in for cc.mallet.topics.ParallelTopicModel whose estimate() runs the
- * collapsed-Gibbs sweeps on an MI355X through liblda_mi355x.so (C ABI:
- * include/lda_mi355x.h).  Replace
- *   new ParallelTopicModel(500, 100, 1)   (src/cmu_ron/TrainAndPredict.java:160)
+ * Drop-in for cc.mallet.topics.ParallelTopicModel whose estimate() runs on
+ * MI355X GPUs through liblda_mi355x_jni.so (JNI glue: integration/jni/lda_jni.c;
+ * native logic: integration/jni/lda_jni_core.c over include/lda_topic_model.h).
+ * Replace
+ *   new ParallelTopicModel(500, 100, 1)    (src/cmu_ron/TrainAndPredict.java:160)
  *   new ParallelTopicModel(100, 10, 0.001) (src/cmu/TrainAndPredict.java:259)
- * with new GpuParallelTopicModel(...); everything downstream
- * (getTopicProbabilities, modelLogLikelihood, getInferencer, printTopWords,
- * printDocumentTopics, Java serialization) reads the Mallet fields this class
- * writes back after the sweeps.
+ * with new GpuParallelTopicModel(...).  estimate() replaces the sweeps, the
+ * alpha/beta optimisation and the LL/token log; afterwards the Mallet fields
+ * (topicSequence of every document, typeTopicCounts, tokensPerTopic, alpha,
+ * alphaSum, beta, betaSum) hold the GPU's state, so getTopicProbabilities,
+ * modelLogLikelihood, getInferencer, printTopWords, printDocumentTopics and
+ * Java serialization keep working.
  *
- * Written against Mallet 2.0.7 (pom.xml:107-111).  NOT compiled in the build
- * image (no JDK); see INTEGRATION.md.
+ * - setNumThreads(n): Mallet's document blocks become GPU shards
+ *   (min(n, visible GPUs)) with an RCCL all-reduce of the count delta per
+ *   sweep; the result does not depend on n.
+ * - K > 1024 runs the large-K sparse sampler (chosen natively).
+ * - The Philox sweep counter is a field of this object (serialized with it):
+ *   a second estimate() (updateModel, src/cmu_ron/TrainAndPredict.java:173-177)
+ *   continues the random stream instead of replaying the first one's draws.
+ *
+ * Written against Mallet 2.0.7 (pom.xml:107-111) using only its public fields
+ * and setters.  NOT compiled in the build image (no JDK); the native call it
+ * makes is compiled and GPU-tested there (tests/jni/estimate_harness.c).
  */
 public class GpuParallelTopicModel extends ParallelTopicModel {
+  private static final long serialVersionUID = 1L;
   private static final Logger logger = Logger.getLogger(GpuParallelTopicModel.class.getName());
   static { System.loadLibrary("lda_mi355x_jni"); }
 
-  private int device = 0;
+  private int gpuShards = 1;        // setNumThreads
+  private long gpuSeed = -1;        // setRandomSeed (-1: time-seeded, as Mallet)
+  private long gpuSweep = 0;        // Philox sweep counter carried across estimate() calls
+  private int verbosity = 0;
 
   public GpuParallelTopicModel(int numberOfTopics, double alphaSum, double beta) {
     super(numberOfTopics, alphaSum, beta);
   }
 
-  public void setDevice(int device) { this.device = device; }
+  @Override
+  public void setNumThreads(int threads) {
+    super.setNumThreads(threads);
+    gpuShards = threads;
+  }
+
+  @Override
+  public void setRandomSeed(int seed) {
+    super.setRandomSeed(seed);
+    gpuSeed = seed;
+  }
+
+  /** 1: the native side prints Mallet's INFO lines on stderr as well. */
+  public void setNativeVerbosity(int level) { verbosity = level; }
 
   // --- JNI (integration/jni/lda_jni.c) -------------------------------------
-  private static native long nativeCreate(int K, int V, long[] docOff, int[] words, int[] z,
-                                          double[] alpha, double beta, long seed, int device);
-  private static native void nativeSweep(long ctx, int n);
-  private static native void nativeGetZ(long ctx, int[] z);
-  private static native void nativeSetAlphaBeta(long ctx, double[] alpha, double beta);
-  private static native double nativeLogLikelihood(long ctx);
-  /** packed rows (count << topicBits | topic), row offsets [V+1] */
-  private static native void nativeMalletPacked(long ctx, int[] rows, long[] rowOff);
-  private static native void nativeGetTokensPerTopic(long ctx, int[] tokensPerTopic);
-  /** adds docLengthCounts[maxLen+1] and topicDocCounts[K*(maxLen+1)] (flattened) */
-  private static native void nativeDocTopicHistograms(long ctx, int maxLen, int[] docLen,
-                                                      int[] topicDocFlat);
-  /** adds countHistogram[maxCount+1] of the nw cells */
-  private static native void nativeCountHistogram(long ctx, long maxCount, int[] hist);
-  private static native void nativeDestroy(long ctx);
+  private static native int nativeEstimate(int K, int V, long[] docOff, int[] words, int[] z,
+                                           double[] alpha, double[] hyper, long[] sweep,
+                                           int[] options, long seed, long[] rowOff, int[] rows,
+                                           int[] tokensPerTopic, int[] llIter, double[] llValue);
 
   @Override
   public void estimate() throws IOException {
@@ -69,76 +86,37 @@ public class GpuParallelTopicModel extends ParallelTopicModel {
       int[] topics = t.topicSequence.getFeatures();
       for (int i = 0; i < fs.getLength(); i++) {
         words[(int) docOff[d] + i] = fs.getIndexAtPosition(i);
-        z[(int) docOff[d] + i] = topics[i];          // addInstances' random init is kept
+        z[(int) docOff[d] + i] = topics[i];          // addInstances' random topics are kept
       }
     }
-    long seed = randomSeed == -1 ? System.nanoTime() : randomSeed;
-    long ctx = nativeCreate(numTopics, numTypes, docOff, words, z, alpha, beta, seed, device);
-    int maxLen = 0;
-    for (int d = 0; d < D; d++) maxLen = Math.max(maxLen, (int) (docOff[d + 1] - docOff[d]));
-    int[] docLen = new int[maxLen + 1];
-    int[] topicDocFlat = new int[numTopics * (maxLen + 1)];
-    int maxTypeCount = 0;
-    for (int w = 0; w < numTypes; w++) maxTypeCount = Math.max(maxTypeCount, typeTotals[w]);
-    try {
-      for (int iteration = 1; iteration <= numIterations; iteration++) {
-        nativeSweep(ctx, 1);
-        boolean opt = iteration > burninPeriod && optimizeInterval != 0;
-        if (opt && iteration % saveSampleInterval == 0) {
-          nativeDocTopicHistograms(ctx, maxLen, docLen, topicDocFlat);   // collectAlphaStatistics
-        }
-        if (opt && iteration % optimizeInterval == 0) {
-          // optimizeAlpha: Mallet's own estimator on the GPU's histograms
-          int[][] topicDoc = new int[numTopics][];
-          for (int k = 0; k < numTopics; k++) {
-            topicDoc[k] = java.util.Arrays.copyOfRange(topicDocFlat, k * (maxLen + 1), (k + 1) * (maxLen + 1));
-          }
-          if (usingSymmetricAlpha) {
-            int[] pooled = new int[maxLen + 1];
-            for (int k = 0; k < numTopics; k++)
-              for (int i = 0; i <= maxLen; i++) pooled[i] += topicDoc[k][i];
-            alphaSum = Dirichlet.learnSymmetricConcentration(pooled, docLen, numTopics, alphaSum);
-            java.util.Arrays.fill(alpha, alphaSum / numTopics);
-          } else {
-            alphaSum = Dirichlet.learnParameters(alpha, topicDoc, docLen, 1.001, 1.0, 1);
-          }
-          java.util.Arrays.fill(docLen, 0);
-          java.util.Arrays.fill(topicDocFlat, 0);
-          // optimizeBeta: countHistogram from the GPU, topic sizes from tokensPerTopic
-          int[] countHistogram = new int[maxTypeCount + 1];
-          nativeCountHistogram(ctx, maxTypeCount, countHistogram);
-          nativeGetTokensPerTopic(ctx, tokensPerTopic);
-          int maxTopicSize = 0;
-          for (int k = 0; k < numTopics; k++) maxTopicSize = Math.max(maxTopicSize, tokensPerTopic[k]);
-          int[] topicSizeHistogram = new int[maxTopicSize + 1];
-          for (int k = 0; k < numTopics; k++) topicSizeHistogram[tokensPerTopic[k]]++;
-          betaSum = Dirichlet.learnSymmetricConcentration(countHistogram, topicSizeHistogram, numTypes, betaSum);
-          beta = betaSum / numTypes;
-          nativeSetAlphaBeta(ctx, alpha, beta);
-        }
-        if (iteration % 10 == 0) {
-          logger.info("<" + iteration + "> LL/token: " + nativeLogLikelihood(ctx) / N);
-        }
-      }
-      // write the sampler state back into Mallet's fields
-      nativeGetZ(ctx, z);
-      for (int d = 0; d < D; d++) {
-        int[] topics = data.get(d).topicSequence.getFeatures();
-        System.arraycopy(z, (int) docOff[d], topics, 0, topics.length);
-      }
-      long[] rowOff = new long[numTypes + 1];
-      int[] rows = new int[0];
-      nativeMalletPacked(ctx, null, rowOff);
-      rows = new int[(int) rowOff[numTypes]];
-      nativeMalletPacked(ctx, rows, rowOff);
-      for (int w = 0; w < numTypes; w++) {
-        int[] dst = typeTopicCounts[w];               // length min(K, typeTotal), as allocated
-        java.util.Arrays.fill(dst, 0);
-        System.arraycopy(rows, (int) rowOff[w], dst, 0, (int) (rowOff[w + 1] - rowOff[w]));
-      }
-      nativeGetTokensPerTopic(ctx, tokensPerTopic);
-    } finally {
-      nativeDestroy(ctx);
+    // typeTopicCounts rows as addInstances allocated them: min(K, typeTotal)
+    long[] rowOff = new long[numTypes + 1];
+    for (int w = 0; w < numTypes; w++) rowOff[w + 1] = rowOff[w] + typeTopicCounts[w].length;
+    int[] rows = new int[(int) rowOff[numTypes]];
+    double[] hyper = {alphaSum, beta, betaSum};
+    long[] sweep = {gpuSweep};
+    int[] options = {numIterations, burninPeriod, optimizeInterval, saveSampleInterval,
+                     usingSymmetricAlpha ? 1 : 0, gpuShards, verbosity};
+    long seed = gpuSeed == -1 ? System.nanoTime() : gpuSeed;
+    int[] llIter = new int[numIterations / 10 + 1];
+    double[] llValue = new double[llIter.length];
+
+    int nll = nativeEstimate(numTopics, numTypes, docOff, words, z, alpha, hyper, sweep, options,
+                             seed, rowOff, rows, tokensPerTopic, llIter, llValue);
+
+    DecimalFormat fmt = new DecimalFormat("0.#####");
+    for (int i = 0; i < Math.min(nll, llIter.length); i++)
+      logger.info("<" + llIter[i] + "> LL/token: " + fmt.format(llValue[i]));
+    // write the sampler state back into Mallet's fields
+    for (int d = 0; d < D; d++) {
+      int[] topics = data.get(d).topicSequence.getFeatures();
+      System.arraycopy(z, (int) docOff[d], topics, 0, topics.length);
     }
+    for (int w = 0; w < numTypes; w++)
+      System.arraycopy(rows, (int) rowOff[w], typeTopicCounts[w], 0, typeTopicCounts[w].length);
+    alphaSum = hyper[0];
+    beta = hyper[1];
+    betaSum = hyper[2];
+    gpuSweep = sweep[0];
   }
 }

@@ -94,6 +94,38 @@ ParallelTopicModel::ParallelTopicModel(int32_t num_topics, double alpha_sum, dou
   if (num_topics < 1 || num_topics > LDA_MAX_TOPICS) raise(LDA_ERR_UNSUPPORTED, "num_topics out of range");
   if (!(alpha_sum > 0.0) || !(beta > 0.0)) raise(LDA_ERR_INVALID_ARG, "alphaSum and beta must be > 0");
   alpha_.assign((size_t)K_, alpha_sum / K_);
+  // the dense sampler holds K <= 1024; above that the large-K sparse one
+  sampler_ = K_ > LDA_MAX_TOPICS_DENSE ? LDA_SAMPLER_SPARSE : LDA_SAMPLER_DENSE;
+}
+
+void ParallelTopicModel::setTopics(const int32_t* z, int64_t n) {
+  if (n != numTokens()) raise(LDA_ERR_INVALID_ARG, "setTopics needs one topic per token");
+  for (int64_t i = 0; i < n; ++i)
+    if (z[i] < 0 || z[i] >= K_) raise(LDA_ERR_INVALID_ARG, "topic out of range [0, K)");
+  markDirty();
+  z_cache_.assign(z, z + n);
+}
+
+void ParallelTopicModel::setHyper(const double* alpha, double alpha_sum, double beta) {
+  for (int k = 0; k < K_; ++k)
+    if (!(alpha[k] > 0.0)) raise(LDA_ERR_INVALID_ARG, "alpha must be > 0");
+  if (!(beta > 0.0) || !(alpha_sum > 0.0)) raise(LDA_ERR_INVALID_ARG, "alphaSum and beta must be > 0");
+  alpha_.assign(alpha, alpha + K_);
+  alpha_sum_ = alpha_sum;
+  beta_ = beta;
+  if (shards_ && !shards_dirty_)
+    for (auto c : shards_->ctx) check(lda_set_alpha_beta(c, alpha_.data(), beta_), "lda_set_alpha_beta");
+}
+
+uint32_t ParallelTopicModel::sweep() {
+  if (shards_ && !shards_dirty_) check(lda_get_sweep(shards_->ctx[0], &sweep_), "lda_get_sweep");
+  return sweep_;
+}
+
+void ParallelTopicModel::setSweep(uint32_t s) {
+  sweep_ = s;
+  if (shards_ && !shards_dirty_)
+    for (auto c : shards_->ctx) check(lda_set_sweep(c, sweep_), "lda_set_sweep");
 }
 
 ParallelTopicModel::~ParallelTopicModel() = default;
@@ -728,6 +760,27 @@ lda_status ldatm_set_topic_display(ldatm* m, int32_t interval, int32_t n) {
 lda_status ldatm_set_random_seed(ldatm* m, int64_t seed) {
   TM_CHECK(m);
   return guard([&] { m->model.setRandomSeed(seed); });
+}
+
+lda_status ldatm_set_topics(ldatm* m, int64_t n, const int32_t* z) {
+  TM_CHECK(m);
+  TM_CHECK(z || n == 0);
+  return guard([&] { m->model.setTopics(z, n); });
+}
+
+lda_status ldatm_set_hyper(ldatm* m, const double* alpha, double alpha_sum, double beta) {
+  TM_CHECK(m && alpha);
+  return guard([&] { m->model.setHyper(alpha, alpha_sum, beta); });
+}
+
+lda_status ldatm_get_sweep(ldatm* m, uint32_t* sweep) {
+  TM_CHECK(m && sweep);
+  return guard([&] { *sweep = m->model.sweep(); });
+}
+
+lda_status ldatm_set_sweep(ldatm* m, uint32_t sweep) {
+  TM_CHECK(m);
+  return guard([&] { m->model.setSweep(sweep); });
 }
 
 lda_status ldatm_estimate(ldatm* m) {

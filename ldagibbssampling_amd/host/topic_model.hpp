@@ -49,6 +49,13 @@ class ParallelTopicModel {
   void setNumThreads(int32_t n);
   void setSampler(int32_t sampler);
   void setVerbosity(int32_t v) { verbosity_ = v; }
+  // state a Java-side ParallelTopicModel already holds (GpuParallelTopicModel:
+  // Mallet's own addInstances topics, alpha/beta optimised in an earlier
+  // estimate(), the Philox sweep counter of the previous estimate())
+  void setTopics(const int32_t* z, int64_t n);
+  void setHyper(const double* alpha, double alpha_sum, double beta);
+  uint32_t sweep();
+  void setSweep(uint32_t s);
   void setPrintLogLikelihood(bool on) { print_log_likelihood_ = on; }
 
   // ---- training ------------------------------------------------------
