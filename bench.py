@@ -35,6 +35,9 @@ CONFIGS = {
                desc="C1: changelist-shaped corpus, 2000 docs x Poisson(8) tok, Zipf(1.1) over 5000 paths, K=20"),
     "c4": dict(docs=1_250_000, doc_len=200, V=100_000, K=512,
                desc="C4 shard: 1.25M docs x 200 tok per GPU, V=100k, K=512 (N=8 == C4: 10M docs)"),
+    # the whole C4 corpus in one context (2e9 tokens: int64 offsets, a DESIGN figure)
+    "c4full": dict(docs=10_000_000, doc_len=200, V=100_000, K=512,
+                   desc="C4 whole corpus on one GPU: 10M docs x 200 tok, V=100k, K=512"),
     "c2": dict(docs=100_000, doc_len=200, V=50_000, K=128, desc="C2: 100k docs x 200 tok, V=50k, K=128"),
     "c3": dict(docs=100_000, doc_len=200, V=50_000, K=1024, desc="C3: 100k docs x 200 tok, V=50k, K=1024"),
     "c5": dict(docs=1_250_000, doc_len=200, V=262_144, K=4096, sampler="sparse",
@@ -49,26 +52,70 @@ def bytes_per_token(K: int) -> int:
     return 4 * K + 16
 
 
-def pmc_traffic(K: int, tokens_per_launch: int, kernel_prefix: str):
-    """HBM bytes per sampler launch from the newest committed rocprofv3 PMC
-    summary (profiles/rNN/traffic_k{K}.json, written by tools/make_traffic.py
-    from separate FETCH_SIZE / WRITE_SIZE passes over this same command).
-    Used only when it was measured on exactly the library loaded now (sha256)
-    for this workload and kernel; None otherwise."""
+def encoding_bytes_per_token(Kp: int) -> int:
+    """Bytes the shipped dense encoding needs per token: the word's 16-bit row
+    over the Kp padded topics (2 Kp), word id, z read, z write and the
+    amortised delta (4 each) — the contract's terms with 2-byte cells."""
+    return 2 * Kp + 16
+
+
+def _newest(pattern):
     import glob
+    return sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", pattern)))[::-1]
+
+
+def pmc_record(tokens_per_launch: int, kernel_prefix: str, K: int):
+    """The newest committed rocprofv3 summary (profiles/rNN/traffic_*.json,
+    tools/make_traffic.py over separate FETCH_SIZE / WRITE_SIZE / SQ passes of
+    this same command) measured on exactly the library loaded now (sha256),
+    for this workload and kernel; (None, None) otherwise."""
     import hashlib
     from ldagibbssampling_amd import capi
     lib = os.environ.get("LDA_MI355X_LIB") or capi.LIB_PATH
     with open(lib, "rb") as f:
         lib_sha = hashlib.sha256(f.read()).hexdigest()
-    paths = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", f"traffic_k{K}.json")))
-    for path in reversed(paths):
+    for path in _newest("traffic_*.json"):
         with open(path) as f:
             t = json.load(f)
         if (t.get("tokens_per_launch") == tokens_per_launch and t.get("lib_sha256") == lib_sha
-                and t.get("kernel", "").startswith(kernel_prefix)):
-            return t["hbm_bytes_per_launch"] / 1e9, os.path.relpath(path, ROOT)
+                and t.get("kernel", "").startswith(kernel_prefix)
+                and t.get("num_topics", K) == K):
+            return t, os.path.relpath(path, ROOT)
     return None, None
+
+
+def issue_roofline(rec, tokens_per_s_kernel: float):
+    """Instruction-issue bound of the sampler: its measured VALU and SALU
+    wave-instructions per token (SQ_INSTS_VALU / SQ_INSTS_SALU of the PMC
+    record) times the kernel's token rate, against the chip's measured issue
+    peaks (tools/issue_peak.hip: independent s_add / v_add chains at 32 waves
+    per CU, profiles/rNN/issue_peak.json).  frac = the larger of the two."""
+    if not rec or "per_token" not in rec:
+        return None
+    peaks = _newest("issue_peak.json")
+    if not peaks:
+        return None
+    with open(peaks[0]) as f:
+        pk = json.load(f)
+    pt = rec["per_token"]
+    out = {"peaks_source": os.path.relpath(peaks[0], ROOT), "unit": "wave-instructions/s"}
+    for kind, ctr, peak in (("valu", "SQ_INSTS_VALU", pk["valu_per_s"]),
+                            ("salu", "SQ_INSTS_SALU", pk["salu_per_s"])):
+        if ctr in pt:
+            ach = pt[ctr] * tokens_per_s_kernel
+            out[kind] = {"per_token": pt[ctr], "achieved": ach, "peak": peak, "frac": ach / peak}
+    parts = [(v["frac"], k) for k, v in out.items() if isinstance(v, dict)]
+    if not parts:
+        return None
+    out["frac"], out["binding"] = max(parts)
+    if "SQ_INSTS_LDS" in pt:
+        out["lds_per_token"] = pt["SQ_INSTS_LDS"]
+    for c in ("SQ_WAVE_CYCLES", "SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY"):
+        if c in pt:
+            out.setdefault("quad_cycles_per_token", {})[c] = pt[c]
+    if "effective_clock_ghz" in rec:
+        out["effective_clock_ghz"] = rec["effective_clock_ghz"]
+    return out
 
 
 def stream_copy_gbs(device: int, nbytes: int = 2 << 30, reps: int = 10) -> float:
@@ -102,11 +149,25 @@ def _cpu_model() -> str:
     return platform.processor() or platform.machine()
 
 
+def cpu_share() -> int:
+    """The host cores this job may use: OMP_NUM_THREADS where the box sets it
+    (the GPU box gives each GPU a 16-core share of a 256-CPU host), else the
+    CPUs in this process's affinity mask."""
+    env = os.environ.get("OMP_NUM_THREADS")
+    if env and env.isdigit() and int(env) > 0:
+        return int(env)
+    try:
+        return len(os.sched_getaffinity(0))
+    except AttributeError:
+        return os.cpu_count() or 1
+
+
 def cpu_baseline(corpus, K, alpha_sum, beta, budget_s=15.0, threads=4):
     """cpu_mallet (oracle/, the Mallet 2.0.7 SparseLDA restatement) timed on a
-    bounded sample of the same workload on this host's cores: `threads`
-    workers (the reference's setNumThreads(4)) for ~budget_s, plus a short
-    single-thread run (T = 1 and T = threads)."""
+    bounded sample of the same workload on this host's cores (SURVEY.md §8d,
+    BASELINE.md: T = 1 and T = nproc): `threads` workers (the reference's
+    setNumThreads(4)) for ~budget_s, a single-thread run, and a run on every
+    core of this job's CPU share."""
     from oracle import oracle as O
     O.build()
     ndocs = min(corpus.num_docs, 20_000)
@@ -127,17 +188,23 @@ def cpu_baseline(corpus, K, alpha_sum, beta, budget_s=15.0, threads=4):
 
     v, sweeps = timed(threads, budget_s, 50)
     v1, sweeps1 = timed(1, budget_s / 3, 20)
+    tn = cpu_share()
+    vn, sweepsn = timed(tn, budget_s / 2, 50)
     return {
         "value": v,
         "unit": "tokens/s",
         "cores": threads,
         "kind": "port",
         "t1_value": v1,
+        "tnproc_value": vn,
+        "tnproc_cores": tn,
         "sample": (f"cpu_mallet (Mallet 2.0.7 SparseLDA restatement, oracle/lda_oracle.c), "
                    f"{threads} threads (= setNumThreads(4), src/cmu_ron/TrainAndPredict.java:164), "
                    f"first {ndocs} docs ({sub.num_tokens} tokens) of this workload, "
                    f"{sweeps} timed sweeps after 2 warm-up; t1_value: 1 thread, {sweeps1} sweeps; "
-                   f"host {_cpu_model()}, {os.cpu_count()} logical CPUs visible"),
+                   f"tnproc_value: {tn} threads = this job's CPU share (OMP_NUM_THREADS, else the "
+                   f"affinity mask), {sweepsn} sweeps; host {_cpu_model()}, "
+                   f"{os.cpu_count()} logical CPUs visible"),
     }
 
 
@@ -215,7 +282,7 @@ def main():
     torch.cuda.set_stream(stream)
     sampler.set_stream(stream.cuda_stream)
     # AD-LDA: sample; all-reduce (SUM) of every rank's int32 nw/nwsum delta; apply
-    trainer = ADLDATrainer(sampler, sync_before_reduce=False)
+    trainer = ADLDATrainer(sampler, sync_before_reduce=False, time_reduce=True)
     trainer.init_counts()
 
     def step():
@@ -255,10 +322,33 @@ def main():
 
     if rank == 0:
         bpt = bytes_per_token(K)
-        achieved = n_local * bpt / (kern_ms * 1e-3) / 1e9      # GB/s, algorithmic
-        traffic_gb, traffic_src = pmc_traffic(K, n_local, ("k_sample_sparse_big<" if K > 1024 else "k_sample_sparse<") if args.sampler == "sparse" else "k_sample<")
+        kname = (("k_sample_sparse_big" if K > 1024 else "k_sample_sparse")
+                 if args.sampler == "sparse" else "k_sample")
+        if nnz0 is not None:
+            # the sparse samplers read 4 B per nonzero entry of the token's word
+            # row (token-weighted mean over the timed region's snapshots) + 16 B
+            mean_nnz = 0.5 * (nnz0 + nnz1)
+            enc = 4.0 * mean_nnz + 16.0
+            enc_model = (f"4 B per nonzero (count, topic) entry of the word's row (mean "
+                         f"{mean_nnz:.1f} entries, lda_row_stats) + word + z read + z write + "
+                         f"amortised delta (4 each)")
+        else:
+            enc = float(encoding_bytes_per_token(sampler.Kp))
+            enc_model = (f"16-bit row over Kp={sampler.Kp} topics (2 Kp) + word + z read + z write "
+                         f"+ amortised delta (4 each)")
+        achieved = n_local * enc / (kern_ms * 1e-3) / 1e9          # GB/s, shipped encoding
+        rec, rec_src = pmc_record(n_local, kname + "<", K)
+        traffic_gb = rec["hbm_bytes_per_launch"] / 1e9 if rec else None
+        tok_s_kernel = n_local / (kern_ms * 1e-3)
+        coll = None
+        if world > 1:
+            nbytes = 4 * (V * sampler.Kp + sampler.Kp)
+            coll = {"op": "all_reduce(SUM, int32) of the nw/nwsum delta, once per sweep",
+                    "bytes_per_sweep": nbytes,
+                    "ring_bytes_per_rank_per_sweep": 2 * (world - 1) * nbytes // world,
+                    "ms_per_sweep": trainer.reduce_ms(args.steps)}
         result = {
-            "metric": "Gibbs tokens sampled/sec at K=512",
+            "metric": f"Gibbs tokens sampled/sec at K={K}",
             "value": value,
             "unit": "tokens/s",
             "n_gpus": world,
@@ -292,31 +382,30 @@ def main():
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBS,
-                "measured_copy_gbs": copy_gbs,
-                "kernel_ms_timed_region": kern_ms,
                 "traffic": traffic_gb,
+                "bytes_per_token": enc,
+                "bytes_model": enc_model,
+                "kernel_ms_timed_region": kern_ms,
+                "measured_copy_gbs": copy_gbs,
                 # the bandwidth the kernel really moves (PMC bytes / its time)
                 "traffic_gbs": (traffic_gb / (kern_ms * 1e-3)) if traffic_gb else None,
                 "traffic_frac": (traffic_gb / (kern_ms * 1e-3) / HBM_PEAK_GBS) if traffic_gb else None,
                 "traffic_unit": "GB per launch (rocprofv3 PMC, gfx950-corrected)",
-                "traffic_source": traffic_src,
-                "algorithmic_gb_per_launch": n_local * bpt / 1e9,
-                "kernel": f"{('k_sample_sparse_big' if K > 1024 else 'k_sample_sparse') if args.sampler == 'sparse' else 'k_sample'}<C={sampler.Kp // 64}> avg {kern_ms:.3f} ms/launch over "
-                          f"{n_local} tokens, B(K)={bpt} B/token",
+                "traffic_source": rec_src,
+                # SURVEY.md §8d's fixed contract B(K) = 4K + 16 (int32 rows)
+                "contract_bytes_per_token": bpt,
+                "contract_gb_per_launch": n_local * bpt / 1e9,
+                "contract_frac": n_local * bpt / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                "kernel": f"{kname}<C={sampler.Kp // 64}> avg {kern_ms:.3f} ms/launch over "
+                          f"{n_local} tokens",
+                "issue": issue_roofline(rec, tok_s_kernel),
             },
+            "collective": coll,
             "ll_per_token": ll / (n_local * world),
             "corpus_gen_s": t_gen,
         }
         if nnz0 is not None:
-            # the sparse variant also against its own bytes per
-            # token: 4 B per nonzero entry of the token's word row (token-
-            # weighted mean over the timed region's snapshots) + 16 B stream
-            mean_nnz = 0.5 * (nnz0 + nnz1)
-            b_sparse = 4.0 * mean_nnz + 16.0
-            ach = n_local * b_sparse / (kern_ms * 1e-3) / 1e9
-            result["roofline_sparse"] = {
-                "bound": "hbm", "bytes_per_token": b_sparse, "mean_row_nnz": [nnz0, nnz1],
-                "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": ach / HBM_PEAK_GBS}
+            result["roofline"]["mean_row_nnz"] = [nnz0, nnz1]
         if world == 1 and not args.no_cpu_baseline:
             result["cpu_baseline"] = cpu_baseline(corpus, K, alpha_sum, beta, args.cpu_budget)
         print(json.dumps(result), flush=True)

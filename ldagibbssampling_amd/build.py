@@ -13,6 +13,14 @@ def build_library(jobs: int = 2) -> str:
     return os.path.join(HERE, "lib", "liblda_mi355x.so")
 
 
+def build_jni_harness() -> str:
+    """The Java drop-in's native half (integration/jni/lda_jni_core.c) linked
+    into the C harness that tests it (tests/jni/estimate_harness.c)."""
+    subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "integration", "jni"), "harness"],
+                   check=True)
+    return os.path.join(ROOT, "tests", "jni", "bin", "estimate_harness")
+
+
 def build_oracle() -> str:
     subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle")], check=True)
     return os.path.join(ROOT, "oracle", "lib", "liblda_oracle.so")
@@ -20,4 +28,5 @@ def build_oracle() -> str:
 
 if __name__ == "__main__":
     print(build_library())
+    print(build_jni_harness())
     print(build_oracle())

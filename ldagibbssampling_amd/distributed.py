@@ -54,13 +54,18 @@ class ADLDATrainer:
     GibbsSampler (GPU) is the product engine; tests inject a CPU one.
     """
 
-    def __init__(self, engine, group=None, sync_before_reduce: bool = True):
+    def __init__(self, engine, group=None, sync_before_reduce: bool = True,
+                 time_reduce: bool = False):
         """sync_before_reduce=False when the engine already launches on the
         stream the collective runs behind (GibbsSampler.set_stream(torch's
-        current stream)): then no host synchronisation per sweep is needed."""
+        current stream)): then no host synchronisation per sweep is needed.
+        time_reduce: record CUDA events around every all-reduce on torch's
+        current stream (reduce_ms reads them after a synchronize)."""
         import torch.distributed as dist
 
         self.engine = engine
+        self.time_reduce = time_reduce
+        self._events = []
         self.sync_before_reduce = sync_before_reduce
         self.group = group
         self.dist = dist
@@ -88,7 +93,15 @@ class ADLDATrainer:
         if self.world > 1:
             if self.sync_before_reduce:
                 self.engine.synchronize()
+            ev = None
+            if self.time_reduce and self._delta.device.type == "cuda":
+                import torch
+                ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                ev[0].record()
             self.dist.all_reduce(self._delta, op=self.dist.ReduceOp.SUM, group=self.group)
+            if ev is not None:
+                ev[1].record()
+                self._events = (self._events + [ev])[-256:]
             if self.sync_before_reduce and self._delta.device.type == "cuda":
                 # RCCL returns once the collective is enqueued (torch's current
                 # stream waits for it, the engine's own stream does not): the
@@ -96,6 +109,15 @@ class ADLDATrainer:
                 # has landed
                 import torch
                 torch.cuda.current_stream(self._delta.device).synchronize()
+
+    def reduce_ms(self, last: int):
+        """Mean duration (ms, CUDA events on torch's stream) of the last `last`
+        all-reduces (time_reduce=True; None when none were recorded)."""
+        evs = self._events[-last:] if last > 0 else []
+        if not evs:
+            return None
+        evs[-1][1].synchronize()
+        return sum(a.elapsed_time(b) for a, b in evs) / len(evs)
 
     def init_counts(self):
         """Global nw/nwsum from every rank's local counts (addInstances)."""

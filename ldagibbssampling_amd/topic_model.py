@@ -50,6 +50,10 @@ TM_SIGNATURES = {
     "ldatm_set_random_seed": (_i32, [_vp, C.c_int64]),
     "ldatm_set_num_threads": (_i32, [_vp, _i32]),
     "ldatm_set_sampler": (_i32, [_vp, _i32]),
+    "ldatm_set_topics": (_i32, [_vp, C.c_int64, _vp]),
+    "ldatm_set_hyper": (_i32, [_vp, _vp, C.c_double, C.c_double]),
+    "ldatm_get_sweep": (_i32, [_vp, C.POINTER(C.c_uint32)]),
+    "ldatm_set_sweep": (_i32, [_vp, C.c_uint32]),
     "ldatm_set_verbosity": (_i32, [_vp, _i32]),
     "ldatm_set_print_log_likelihood": (_i32, [_vp, _i32]),
     "ldatm_estimate": (_i32, [_vp]),

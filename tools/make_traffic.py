@@ -2,7 +2,7 @@
 """Write profiles/rNN/traffic_k{K}.json (what bench.py reports as
 roofline.traffic) from the rocprofv3 summaries of one profile run.
 
-  make_traffic.py <summary_dir> <kernel> <tokens_per_launch> <workload> <out.json>
+  make_traffic.py <summary_dir> <kernel> <tokens_per_launch> <workload> <out.json> [K]
 
 summary_dir holds summary_kt.json (--kernel-trace --stats), summary_fetch.json
 (--pmc FETCH_SIZE) and summary_write.json (--pmc WRITE_SIZE), each its own
@@ -10,6 +10,9 @@ rocprofv3 pass over the same bench command (tools/profile.sh).  Bytes follow
 MI355X_MICROARCH.md §HBM for gfx950: FETCH_SIZE/WRITE_SIZE are KiB and
 FETCH_SIZE counts half of a 16 B/lane coalesced read stream (the sampler's row
 gathers), so hbm = (2*FETCH_SIZE + WRITE_SIZE) * 1024.
+When the SQ passes (summary_sq.json / summary_lds.json / summary_grbm.json)
+are there too, the per-token instruction mix and the effective clock are
+recorded as well: bench.py's issue-bound roofline reads them.
 """
 import json
 import os
@@ -22,7 +25,15 @@ def lib_sha256(path):
         return hashlib.sha256(f.read()).hexdigest()
 
 
-def main(d, kernel, tokens, workload, out):
+def _ctr(d, name, kernel, counter):
+    p = os.path.join(d, f"summary_{name}.json")
+    if not os.path.exists(p):
+        return None
+    c = json.load(open(p))["counters"].get(kernel, {}).get(counter)
+    return c["avg_per_dispatch"] if c else None
+
+
+def main(d, kernel, tokens, workload, out, K=None):
     kt = json.load(open(os.path.join(d, "summary_kt.json")))
     fe = json.load(open(os.path.join(d, "summary_fetch.json")))["counters"][kernel]["FETCH_SIZE"]
     wr = json.load(open(os.path.join(d, "summary_write.json")))["counters"][kernel]["WRITE_SIZE"]
@@ -47,6 +58,22 @@ def main(d, kernel, tokens, workload, out):
             h, m = c["TCC_HIT_sum"]["avg_per_dispatch"], c["TCC_MISS_sum"]["avg_per_dispatch"]
             t["l2_hit_rate"] = h / (h + m) if h + m else None
     t["bytes_per_token"] = t["hbm_bytes_per_launch"] / t["tokens_per_launch"]
+    if K is not None:
+        t["num_topics"] = int(K)
+    # instruction mix per token (wave-instructions: SQ_INSTS_* sum over all waves)
+    mix = {}
+    for name, counter in (("sq", "SQ_INSTS_VALU"), ("lds", "SQ_INSTS_SALU"), ("lds", "SQ_INSTS_LDS"),
+                          ("lds", "SQ_INSTS_SMEM"), ("sq", "SQ_WAVE_CYCLES"), ("sq", "SQ_WAIT_ANY"),
+                          ("sq", "SQ_WAIT_INST_ANY"), ("sq", "SQ_ACTIVE_INST_ANY")):
+        v = _ctr(d, name, kernel, counter)
+        if v is not None:
+            mix[counter] = v / float(tokens)
+    if mix:
+        t["per_token"] = mix
+    g = _ctr(d, "grbm", kernel, "GRBM_GUI_ACTIVE")
+    if g is not None:
+        # GRBM_GUI_ACTIVE sums the 8 XCDs' busy cycles (MI355X_MICROARCH.md, DVFS item)
+        t["effective_clock_ghz"] = g / 8.0 / (t["avg_ns_kernel_trace"])
     # the library these counters belong to: bench.py uses the file only for it
     lib = os.environ.get("LDA_MI355X_LIB") or os.path.join(
         os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "ldagibbssampling_amd", "lib",
@@ -58,4 +85,4 @@ def main(d, kernel, tokens, workload, out):
 
 
 if __name__ == "__main__":
-    main(*sys.argv[1:6])
+    main(*sys.argv[1:7])
