@@ -119,13 +119,29 @@ lda_status lda_learn_symmetric_concentration(const int32_t* count_hist, int64_t 
       cnt.push_back(length_counts[j]);
     }
   }
+  // non-zero counts, ascending: the numerator walks them the way Mallet's
+  // denominator walks the observation lengths (term by term across short
+  // gaps, a digamma difference across gaps > 20), so its cost is the number
+  // of distinct counts, not the largest count (C4: cells of ~1e5-1e6)
+  std::vector<int64_t> cidx;
+  for (int64_t c = 1; c <= top; ++c)
+    if (count_hist[c] > 0) cidx.push_back(c);
   double value = current;
   for (int it = 1; it <= 200; ++it) {
     const double per_dim = value / num_dims;
     double dig = 0.0, num = 0.0;
-    for (int64_t c = 1; c <= top; ++c) {
-      dig += 1.0 / (per_dim + (double)(c - 1));
-      num += (double)count_hist[c] * dig;
+    {
+      const double pbase = digamma(per_dim);
+      int64_t prev = 0;
+      for (int64_t c : cidx) {
+        if (c - prev > 20) {
+          dig = digamma(per_dim + (double)c) - pbase;
+        } else {
+          for (int64_t i = prev + 1; i <= c; ++i) dig += 1.0 / (per_dim + (double)(i - 1));
+        }
+        num += (double)count_hist[c] * dig;
+        prev = c;
+      }
     }
     // sum over lengths n of count(n) * (psi(value + n) - psi(value)); far
     // jumps (> 20) restart from digamma differences, near ones step term by term

@@ -184,9 +184,19 @@ double orc_learn_symmetric_concentration(const int32_t* counts, int64_t max_coun
   for (int it = 0; it < 200; ++it) {
     const double p = value / dims;
     double num = 0.0, d = 0.0;
+    /* the numerator over the non-zero counts, with Mallet's denominator rule
+     * (digamma difference across gaps > 20, term by term otherwise): equal
+     * to Mallet's literal loop for histograms without such gaps */
+    const double pbase = orc_digamma(p);
+    int64_t prevc = 0;
     for (int64_t c = 1; c <= top; ++c) {
-      d += 1.0 / (p + (double)(c - 1));
+      if (counts[c] <= 0) continue;
+      if (c - prevc > 20)
+        d = orc_digamma(p + (double)c) - pbase;
+      else
+        for (int64_t i = prevc + 1; i <= c; ++i) d += 1.0 / (p + (double)(i - 1));
       num += counts[c] * d;
+      prevc = c;
     }
     const double psi0 = orc_digamma(value);
     double den = 0.0;

@@ -138,3 +138,53 @@ def test_dead_topics_stay_finite(oracle):
         ao, so = oracle.learn_parameters(alpha, hist, lens)
         np.testing.assert_array_equal(ap, ao)
         assert np.all(np.isfinite(ap)) and np.all(ap >= 1e-300) and np.isfinite(sp)
+
+
+def _learn_symmetric_literal(counts, lens, dims, value):
+    """Mallet's learnSymmetricConcentration with the numerator as the literal
+    loop over every count 1..max (denominator: its own gap rule)."""
+    top = int(np.nonzero(counts)[0].max())
+    nz_len = np.nonzero(lens)[0]
+    for _ in range(200):
+        p = value / dims
+        d = num = 0.0
+        for c in range(1, top + 1):
+            d += 1.0 / (p + (c - 1))
+            num += counts[c] * d
+        base = float(sp_digamma(value))
+        d = den = 0.0
+        prev = 0
+        for n in nz_len:
+            if n - prev > 20:
+                d = float(sp_digamma(value + n)) - base
+            else:
+                for i in range(prev, n):
+                    d += 1.0 / (value + i)
+            den += d * lens[n]
+            prev = n
+        value = p * num / den
+    return value
+
+
+def test_learn_symmetric_sparse_counts(oracle):
+    """optimizeBeta's countHistogram at scale is sparse at the top (cells of
+    ~1e5 beside empty stretches): the numerator walks the non-zero counts with
+    the denominator's gap rule.  Product == oracle to the bit, and within
+    1e-12 of Mallet's literal loop."""
+    rng = np.random.default_rng(7)
+    counts = np.zeros(200_001, np.int32)
+    counts[1:60] = rng.integers(100, 5000, 59)
+    counts[rng.integers(60, 200_000, 300)] += 1
+    sizes = np.zeros(2_000_001, np.int32)
+    sizes[rng.integers(500_000, 2_000_000, 40)] += 1
+    vp = _learn_symmetric_product(counts, sizes, 100_000, 1000.0)
+    vo = oracle.learn_symmetric_concentration(counts, sizes, 100_000, 1000.0)
+    assert vp == vo
+    small = np.zeros(3001, np.int32)
+    small[1:30] = rng.integers(10, 400, 29)
+    small[rng.integers(30, 3000, 40)] += 1
+    ssz = np.zeros(20001, np.int32)
+    ssz[rng.integers(1000, 20000, 12)] += 1
+    lit = _learn_symmetric_literal(small, ssz, 2000, 20.0)
+    got = _learn_symmetric_product(small, ssz, 2000, 20.0)
+    assert abs(got - lit) <= 1e-12 * abs(lit), (got, lit)
