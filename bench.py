@@ -226,6 +226,11 @@ def main():
                     help="collective backend for N > 1 (nccl = RCCL over xGMI; gloo only to "
                          "rehearse several ranks on one GPU)")
     ap.add_argument("--cpu-budget", type=float, default=15.0)
+    ap.add_argument("--exchange-parts", type=int, default=None,
+                    help="N > 1: split every sweep into P parts whose all-reduces overlap the "
+                         "next part's sampling (default 1: DESIGN.md §5)")
+    ap.add_argument("--reserve-cus", type=int, default=8,
+                    help="split sweeps: CUs' worth of sampler blocks left free for RCCL")
     args = ap.parse_args()
 
     import torch
@@ -281,7 +286,12 @@ def main():
     stream = torch.cuda.Stream(device=device)
     torch.cuda.set_stream(stream)
     sampler.set_stream(stream.cuda_stream)
-    # AD-LDA: sample; all-reduce (SUM) of every rank's int32 nw/nwsum delta; apply
+    # AD-LDA: sample; all-reduce (SUM) of every rank's int32 nw/nwsum delta; apply.
+    # With N > 1 the sweep is split so that the exchange overlaps sampling.
+    if args.exchange_parts is None:
+        args.exchange_parts = 1
+    if args.exchange_parts > 1:
+        sampler.set_exchange_parts(args.exchange_parts, args.reserve_cus)
     trainer = ADLDATrainer(sampler, sync_before_reduce=False, time_reduce=True)
     trainer.init_counts()
 
@@ -306,10 +316,12 @@ def main():
     # per-launch duration of the sampler kernel over the timed region: HIP
     # events recorded around every launch on the sampler's stream, read back
     # after the closing synchronize (no host sync inside the timed loop)
-    ks = sampler.sample_times(args.steps)
+    parts = sampler.exchange_parts
+    ks = sampler.sample_times(args.steps * parts)
     nnz1 = sampler.row_stats() if nnz0 is not None else None
-    assert len(ks) == min(args.steps, 256)
-    kern_ms = float(np.mean(ks))
+    assert len(ks) == min(args.steps * parts, 256)
+    # a split sweep is `parts` launches: the sampler's time per sweep is their sum
+    kern_ms = float(np.mean(ks)) * parts
     copy_gbs = stream_copy_gbs(device) if rank == 0 else None
 
     t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{device}")
@@ -343,10 +355,18 @@ def main():
         coll = None
         if world > 1:
             nbytes = 4 * (V * sampler.Kp + sampler.Kp)
-            coll = {"op": "all_reduce(SUM, int32) of the nw/nwsum delta, once per sweep",
-                    "bytes_per_sweep": nbytes,
-                    "ring_bytes_per_rank_per_sweep": 2 * (world - 1) * nbytes // world,
-                    "ms_per_sweep": trainer.reduce_ms(args.steps)}
+            coll = {"op": ("all_reduce(SUM, int32) of the nw/nwsum delta, once per sweep"
+                           if parts == 1 else
+                           f"all_reduce(SUM, int32) of the nw/nwsum delta of each of {parts} "
+                           f"sweep parts, part i's overlapping part i+1's sampling"),
+                    "exchange_parts": parts,
+                    "reserve_cus": args.reserve_cus if parts > 1 else 0,
+                    "bytes_per_sweep": nbytes * parts,
+                    "ring_bytes_per_rank_per_sweep": 2 * (world - 1) * nbytes * parts // world,
+                    # parts == 1: the whole collective; > 1: the exposed tail after
+                    # the last part's sampling
+                    "ms_per_sweep": trainer.reduce_ms(args.steps),
+                    "ms_kind": "collective" if parts == 1 else "exposed (after the last part)"}
         result = {
             "metric": f"Gibbs tokens sampled/sec at K={K}",
             "value": value,

@@ -104,6 +104,24 @@ lda_status lda_delta_buffer(lda_ctx* ctx, void** dev_ptr, size_t* count);
 /* nw += delta, nwsum += delta, delta = 0, refresh the per-topic tables. */
 lda_status lda_apply(lda_ctx* ctx);
 
+/* Split sweep: the exchange overlapped with sampling.
+ * Mallet sums its workers' counts only after every worker has finished the
+ * sweep (ParallelTopicModel.sumTypeTopicCounts, [M]); here the shard's work
+ * ranges are cut into `parts` token-balanced parts (1..LDA_MAX_EXCHANGE_PARTS),
+ * each with its own delta buffer.  lda_sample_part(ctx, i) samples part i
+ * against the unchanged snapshot; after it, buffer i is final for the sweep,
+ * so its all-reduce can run (on another stream) while part i+1 samples.
+ * Parts are sampled in order 0..parts-1 and all use the same sweep counter;
+ * lda_apply folds every buffer.  Results are identical for any `parts`
+ * (integer sums; draws keyed by the global token index).  lda_sample runs
+ * every part.  reserve_cus: CUs' worth of sampler blocks left free in a split
+ * sweep for the collective's kernels (0 = none). */
+#define LDA_MAX_EXCHANGE_PARTS 4
+lda_status lda_set_exchange_parts(lda_ctx* ctx, int32_t parts, int32_t reserve_cus);
+lda_status lda_get_exchange_parts(lda_ctx* ctx, int32_t* parts);
+lda_status lda_sample_part(lda_ctx* ctx, int32_t part);
+lda_status lda_delta_buffer_part(lda_ctx* ctx, int32_t part, void** dev_ptr, size_t* count);
+
 /* The HIP stream every call of this context is ordered on (hipStream_t;
  * NULL = the context's own stream). */
 lda_status lda_set_stream(lda_ctx* ctx, void* hip_stream);

@@ -61,6 +61,10 @@ lda_status ldatm_set_random_seed(ldatm* m, int64_t seed);      /* setRandomSeed 
 lda_status ldatm_set_num_threads(ldatm* m, int32_t n);
 /* LDA_SAMPLER_* (default: DENSE for K <= 1024, SPARSE above) */
 lda_status ldatm_set_sampler(ldatm* m, int32_t sampler);
+/* With more than one GPU shard: cut every sweep into `parts` parts
+ * (1..LDA_MAX_EXCHANGE_PARTS) whose all-reduces overlap the next part's
+ * sampling (lda_set_exchange_parts).  No effect on one GPU or on results. */
+lda_status ldatm_set_exchange_parts(ldatm* m, int32_t parts);
 /* State a Java-side ParallelTopicModel already holds, for GpuParallelTopicModel
  * (integration/): the topics Mallet's own addInstances drew (z[n], n = every
  * token of the model), alpha[K] / alphaSum / beta after an earlier optimisation,

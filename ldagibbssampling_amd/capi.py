@@ -26,6 +26,7 @@ STATUS_NAMES = {
 MAX_TOPICS = 4096
 MAX_TOPICS_DENSE = 1024
 MAX_DOC_TOKENS_BIGK = 65535
+MAX_EXCHANGE_PARTS = 4
 SAMPLERS = {"dense": 0, "sparse": 1}
 
 
@@ -63,6 +64,10 @@ SIGNATURES = {
     "lda_sample": (C.c_int32, [_vp]),
     "lda_delta_buffer": (C.c_int32, [_vp, C.POINTER(_vp), C.POINTER(C.c_size_t)]),
     "lda_apply": (C.c_int32, [_vp]),
+    "lda_set_exchange_parts": (C.c_int32, [_vp, C.c_int32, C.c_int32]),
+    "lda_get_exchange_parts": (C.c_int32, [_vp, C.POINTER(C.c_int32)]),
+    "lda_sample_part": (C.c_int32, [_vp, C.c_int32]),
+    "lda_delta_buffer_part": (C.c_int32, [_vp, C.c_int32, C.POINTER(_vp), C.POINTER(C.c_size_t)]),
     "lda_set_stream": (C.c_int32, [_vp, _vp]),
     "lda_get_stream": (C.c_int32, [_vp, C.POINTER(_vp)]),
     "lda_synchronize": (C.c_int32, [_vp]),

@@ -85,6 +85,34 @@ std::vector<int64_t> make_ranges(const std::vector<int64_t>& off, int64_t target
   return r;
 }
 
+// The work ranges of a split sweep: documents cut into `parts` token-balanced
+// spans, each span grouped by make_ranges on its own (its own short tail).
+// part_range[i] is the index of part i's first range.  parts == 1 gives
+// exactly make_ranges(off, target).
+std::vector<int64_t> make_part_ranges(const std::vector<int64_t>& off, int64_t target, int parts,
+                                      std::vector<int64_t>& part_range) {
+  const int64_t D = (int64_t)off.size() - 1;
+  std::vector<int64_t> r{0};
+  part_range.assign(1, 0);
+  int64_t d_begin = 0;
+  for (int i = 0; i < parts; ++i) {
+    int64_t d_end = D;
+    if (i + 1 < parts) {
+      const int64_t tgt = off[0] + (off[D] - off[0]) * (i + 1) / parts;
+      d_end = std::lower_bound(off.begin(), off.end(), tgt) - off.begin();
+      d_end = std::min(std::max(d_end, d_begin), D);
+    }
+    if (d_end > d_begin) {
+      const std::vector<int64_t> sub(off.begin() + d_begin, off.begin() + d_end + 1);
+      const std::vector<int64_t> rr = make_ranges(sub, target);
+      for (size_t j = 1; j < rr.size(); ++j) r.push_back(d_begin + rr[j]);
+    }
+    part_range.push_back((int64_t)r.size() - 1);
+    d_begin = d_end;
+  }
+  return r;
+}
+
 template <typename T>
 hipError_t dalloc(T** p, size_t n) {
   *p = nullptr;
@@ -128,6 +156,11 @@ struct lda_ctx {
   int32_t* nw = nullptr;
   int32_t* nwsum = nullptr;
   int32_t* delta = nullptr;
+  // split sweep (lda_set_exchange_parts): part i samples the work ranges
+  // [part_range[i], part_range[i+1]) into delta_part[i] (delta_part[0] == delta)
+  int parts = 1, next_part = 0, reserve_cus = 0;
+  int32_t* delta_part[LDA_MAX_EXCHANGE_PARTS] = {};
+  std::vector<int64_t> part_range{0, 0};
   double* alpha_d = nullptr;
   float* alpha_f = nullptr;
   float* inv = nullptr;
@@ -147,6 +180,8 @@ struct lda_ctx {
                     (void*)inv, (void*)inv_m1, (void*)partial, (void*)nonzero, (void*)ent,
                     (void*)row_off, (void*)row_nnz, (void*)nw16, (void*)wide})
       if (p) (void)hipFree(p);
+    for (int i = 1; i < LDA_MAX_EXCHANGE_PARTS; ++i)
+      if (delta_part[i]) (void)hipFree(delta_part[i]);
     for (int i = 0; i < LDA_TIME_RING; ++i) {
       if (ev0[i]) (void)hipEventDestroy(ev0[i]);
       if (ev1[i]) (void)hipEventDestroy(ev1[i]);
@@ -209,7 +244,13 @@ static lda_status build_row_capacity(lda_ctx* c) {
 }
 
 static lda_status apply_impl(lda_ctx* c) {
+  if (c->next_part != 0)
+    return fail(LDA_ERR_STATE, "lda_apply inside a split sweep: sample every part first");
   HIP_TRY(hipSetDevice(c->device));
+  // a split sweep's later parts are folded into part 0's buffer (the one the
+  // apply kernels read) and zeroed
+  for (int i = 1; i < c->parts; ++i)
+    HIP_TRY(lda::launch_fold_delta(c->delta, c->delta_part[i], (int64_t)c->V * c->Kp + c->Kp, c->stream));
   if (c->sampler == LDA_SAMPLER_DENSE) {
     // one launch: apply, 16-bit rows, topic tables, queue reset (k_apply_packed)
     lda::TopicTables t{c->nwsum, c->alpha_d, c->alpha_f, c->inv, c->inv_m1,
@@ -237,7 +278,9 @@ static lda_status apply_impl(lda_ctx* c) {
 
 static lda_status recount_impl(lda_ctx* c) {
   // local (word, topic) counts of this shard become the pending delta
-  HIP_TRY(hipMemsetAsync(c->delta, 0, sizeof(int32_t) * ((size_t)c->V * c->Kp + c->Kp), c->stream));
+  for (int i = 0; i < c->parts; ++i)
+    HIP_TRY(hipMemsetAsync(c->delta_part[i], 0, sizeof(int32_t) * ((size_t)c->V * c->Kp + c->Kp), c->stream));
+  c->next_part = 0;
   HIP_TRY(hipMemsetAsync(c->nw, 0, sizeof(int32_t) * (size_t)c->V * c->Kp, c->stream));
   HIP_TRY(hipMemsetAsync(c->nwsum, 0, sizeof(int32_t) * c->Kp, c->stream));
   HIP_TRY(lda::launch_count(c->words, c->z, c->N, c->Kp, c->delta, c->delta + (int64_t)c->V * c->Kp,
@@ -344,14 +387,14 @@ lda_status lda_create(lda_ctx** out, const lda_config* cfg, const int64_t* doc_o
   // 56 us per sweep against a 256-token floor)
   if (tpr <= 0) tpr = std::max<int64_t>(16, std::min<int64_t>(65536, N / std::max<int64_t>(1, waves * 32)));
   c->tokens_per_range = tpr;
-  std::vector<int64_t> ranges = make_ranges(off, tpr);
+  std::vector<int64_t> ranges = make_part_ranges(off, tpr, 1, c->part_range);
   c->R = (int64_t)ranges.size() - 1;
 
   CT(dalloc(&c->words, N));
   CT(dalloc(&c->z, N));
   CT(dalloc(&c->doc_off, D + 1));
   CT(dalloc(&c->range_doc, ranges.size()));
-  CT(dalloc(&c->queue, 4));
+  CT(dalloc(&c->queue, LDA_MAX_EXCHANGE_PARTS));
   CT(dalloc(&c->nw, (size_t)c->V * c->Kp));
   CT(dalloc(&c->nwsum, c->Kp));
   if (c->sampler == LDA_SAMPLER_DENSE) {
@@ -359,6 +402,7 @@ lda_status lda_create(lda_ctx** out, const lda_config* cfg, const int64_t* doc_o
     CT(dalloc(&c->wide, (size_t)c->V));
   }
   CT(dalloc(&c->delta, (size_t)c->V * c->Kp + c->Kp));
+  c->delta_part[0] = c->delta;
   CT(dalloc(&c->alpha_d, c->K));
   CT(dalloc(&c->alpha_f, c->Kp));
   CT(dalloc(&c->inv, c->Kp));
@@ -440,16 +484,30 @@ lda_status lda_apply(lda_ctx* c) {
   return apply_impl(c);
 }
 
-lda_status lda_sample(lda_ctx* c) {
-  if (!c) return fail(LDA_ERR_INVALID_ARG, "null ctx");
-  if (c->pending) return fail(LDA_ERR_STATE, "lda_sample with a pending delta: call lda_apply first");
+// One launch of the sampler over part `part` of a (possibly split) sweep.
+static lda_status sample_part_impl(lda_ctx* c, int part) {
+  if (part != c->next_part)
+    return fail(LDA_ERR_STATE, "split sweep parts must be sampled in order 0, 1, ...");
+  if (part == 0 && c->pending) return fail(LDA_ERR_STATE, "lda_sample with a pending delta: call lda_apply first");
   HIP_TRY(hipSetDevice(c->device));
-  if (c->N > 0) {
-    // the dense sampler's apply (which every sample follows) zeroed the queue
-    if (c->sampler != LDA_SAMPLER_DENSE) HIP_TRY(hipMemsetAsync(c->queue, 0, sizeof(int32_t), c->stream));
-    const lda::SampleParams p = c->params(false);
+  const int64_t r0 = c->part_range[(size_t)part], r1 = c->part_range[(size_t)part + 1];
+  if (r1 > r0) {
+    // the dense sampler's apply (which every sample follows) zeroed queue[0]
+    if (c->sampler != LDA_SAMPLER_DENSE || part > 0)
+      HIP_TRY(hipMemsetAsync(c->queue + part, 0, sizeof(int32_t), c->stream));
+    lda::SampleParams p = c->params(false);
+    p.range_doc = c->range_doc + r0;
+    p.num_ranges = r1 - r0;
+    p.queue = c->queue + part;
+    p.delta = c->delta_part[part];
+    p.dsum = c->delta_part[part] + (int64_t)c->V * c->Kp;
     const int64_t wpb = c->waves_per_block;
-    const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>(c->sample_blocks, (c->R + wpb - 1) / wpb));
+    // a split sweep leaves reserve_cus CUs' worth of sampler blocks free, so
+    // the collective of the part before this one finds CUs to run on
+    int64_t cap = c->sample_blocks;
+    if (c->parts > 1 && c->reserve_cus > 0)
+      cap = std::max<int64_t>(1, (int64_t)c->sample_blocks * std::max(1, c->cus - c->reserve_cus) / c->cus);
+    const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>(cap, (r1 - r0 + wpb - 1) / wpb));
     const int slot = (int)(c->launches % lda_ctx::LDA_TIME_RING);
     HIP_TRY(hipEventRecord(c->ev0[slot], c->stream));
     if (c->sampler == LDA_SAMPLER_SPARSE)
@@ -459,8 +517,79 @@ lda_status lda_sample(lda_ctx* c) {
     HIP_TRY(hipEventRecord(c->ev1[slot], c->stream));
     c->launches++;
   }
-  c->sweep++;
-  c->pending = true;
+  c->pending = true;  // the part buffers hold this sweep's changes
+  if (++c->next_part == c->parts) {
+    c->next_part = 0;
+    c->sweep++;
+  }
+  return LDA_OK;
+}
+
+lda_status lda_sample(lda_ctx* c) {
+  if (!c) return fail(LDA_ERR_INVALID_ARG, "null ctx");
+  if (c->next_part != 0) return fail(LDA_ERR_STATE, "lda_sample inside a split sweep: finish it with lda_sample_part");
+  for (int i = 0; i < c->parts; ++i) {
+    lda_status s = sample_part_impl(c, i);
+    if (s) return s;
+  }
+  return LDA_OK;
+}
+
+lda_status lda_sample_part(lda_ctx* c, int32_t part) {
+  if (!c) return fail(LDA_ERR_INVALID_ARG, "null ctx");
+  if (part < 0 || part >= c->parts) return fail(LDA_ERR_INVALID_ARG, "part out of range [0, parts)");
+  return sample_part_impl(c, part);
+}
+
+lda_status lda_set_exchange_parts(lda_ctx* c, int32_t parts, int32_t reserve_cus) {
+  if (!c) return fail(LDA_ERR_INVALID_ARG, "null ctx");
+  if (parts < 1 || parts > LDA_MAX_EXCHANGE_PARTS)
+    return fail(LDA_ERR_INVALID_ARG, "parts must be in [1, LDA_MAX_EXCHANGE_PARTS]");
+  if (reserve_cus < 0) return fail(LDA_ERR_INVALID_ARG, "reserve_cus must be >= 0");
+  if (c->next_part != 0) return fail(LDA_ERR_STATE, "inside a split sweep");
+  HIP_TRY(hipSetDevice(c->device));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  const size_t cells = (size_t)c->V * c->Kp + c->Kp;
+  for (int i = 1; i < LDA_MAX_EXCHANGE_PARTS; ++i) {
+    if (i < parts && !c->delta_part[i]) {
+      HIP_TRY(dalloc(&c->delta_part[i], cells));
+      HIP_TRY(hipMemsetAsync(c->delta_part[i], 0, sizeof(int32_t) * cells, c->stream));
+    } else if (i >= parts && c->delta_part[i]) {
+      // a pending change in a dropped part goes to part 0 first
+      HIP_TRY(lda::launch_fold_delta(c->delta, c->delta_part[i], (int64_t)cells, c->stream));
+      HIP_TRY(hipStreamSynchronize(c->stream));
+      HIP_TRY(hipFree(c->delta_part[i]));
+      c->delta_part[i] = nullptr;
+    }
+  }
+  std::vector<int64_t> pr;
+  std::vector<int64_t> ranges = make_part_ranges(c->doc_off_h, c->tokens_per_range, parts, pr);
+  int64_t* dr = nullptr;
+  HIP_TRY(dalloc(&dr, ranges.size()));
+  hipError_t e = hipMemcpyAsync(dr, ranges.data(), sizeof(int64_t) * ranges.size(), hipMemcpyHostToDevice, c->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+  if (e != hipSuccess) (void)hipFree(dr);
+  HIP_TRY(e);
+  (void)hipFree(c->range_doc);
+  c->range_doc = dr;
+  c->R = (int64_t)ranges.size() - 1;
+  c->part_range = pr;
+  c->parts = parts;
+  c->reserve_cus = reserve_cus;
+  return LDA_OK;
+}
+
+lda_status lda_get_exchange_parts(lda_ctx* c, int32_t* parts) {
+  if (!c || !parts) return fail(LDA_ERR_INVALID_ARG, "null argument");
+  *parts = c->parts;
+  return LDA_OK;
+}
+
+lda_status lda_delta_buffer_part(lda_ctx* c, int32_t part, void** dev_ptr, size_t* count) {
+  if (!c || !dev_ptr || !count) return fail(LDA_ERR_INVALID_ARG, "null argument");
+  if (part < 0 || part >= c->parts) return fail(LDA_ERR_INVALID_ARG, "part out of range [0, parts)");
+  *dev_ptr = c->delta_part[part];
+  *count = (size_t)c->V * c->Kp + c->Kp;
   return LDA_OK;
 }
 

@@ -103,6 +103,8 @@ hipError_t launch_init_z(int32_t* z, int64_t n, int32_t K, int64_t token_base, u
 hipError_t launch_count(const int32_t* words, const int32_t* z, int64_t n, int32_t Kp,
                         int32_t* delta, int32_t* dsum, hipStream_t st);
 hipError_t launch_apply(int32_t* nw, int32_t* delta, int64_t n, hipStream_t st);
+// dst += src; src = 0 over n int32 (n a multiple of 4): a split sweep's parts
+hipError_t launch_fold_delta(int32_t* dst, int32_t* src, int64_t n, hipStream_t st);
 hipError_t launch_prepare_topics(int32_t* nwsum, int32_t* dsum, const double* alpha, double beta,
                                  double vbeta, int32_t K, int32_t Kp, float* alpha_f, float* inv,
                                  float* inv_m1, hipStream_t st);

@@ -1506,6 +1506,25 @@ __global__ __launch_bounds__(256) void k_apply(int4* __restrict__ nw, int4* __re
   }
 }
 
+// Split sweep (lda_set_exchange_parts): dst += src; src = 0 over the whole
+// [V*Kp | Kp] delta region (a multiple of 4 int32: Kp is a multiple of 64).
+// int4 groups that are zero in src are neither written nor re-zeroed.
+__global__ __launch_bounds__(256) void k_fold_delta(int4* __restrict__ dst, int4* __restrict__ src,
+                                                    int64_t n4) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += (int64_t)gridDim.x * 256) {
+    const int4 d = src[i];
+    if (d.x | d.y | d.z | d.w) {
+      int4 a = dst[i];
+      a.x += d.x;
+      a.y += d.y;
+      a.z += d.z;
+      a.w += d.w;
+      dst[i] = a;
+      src[i] = make_int4(0, 0, 0, 0);
+    }
+  }
+}
+
 // One pass per sweep for the dense sampler: nw += delta (rows with an
 // all-zero delta are not rewritten), delta = 0, the 16-bit copy and wide
 // flag of every row, and — in the first block — nwsum += dsum and the
@@ -2013,6 +2032,15 @@ hipError_t launch_apply(int32_t* nw, int32_t* delta, int64_t n, hipStream_t st) 
   const int blocks = (int)std::min<int64_t>((n4 + 255) / 256, 8192);
   hipLaunchKernelGGL(k_apply, dim3(blocks), dim3(256), 0, st, reinterpret_cast<int4*>(nw),
                      reinterpret_cast<int4*>(delta), n4);
+  return hipGetLastError();
+}
+
+hipError_t launch_fold_delta(int32_t* dst, int32_t* src, int64_t n, hipStream_t st) {
+  const int64_t n4 = n / 4;
+  if (n4 <= 0) return hipSuccess;
+  const int blocks = (int)std::min<int64_t>((n4 + 255) / 256, 8192);
+  hipLaunchKernelGGL(k_fold_delta, dim3(blocks), dim3(256), 0, st, reinterpret_cast<int4*>(dst),
+                     reinterpret_cast<int4*>(src), n4);
   return hipGetLastError();
 }
 

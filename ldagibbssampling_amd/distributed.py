@@ -5,11 +5,18 @@ threads (setNumThreads(4) at src/cmu_ron/TrainAndPredict.java:164 and
 src/cmu/TrainAndPredict.java:262): contiguous doc blocks per thread, and after
 every sweep the per-thread counts are summed into the global typeTopicCounts
 / tokensPerTopic and copied back (ParallelTopicModel.sumTypeTopicCounts).
-Here that exchange is ONE collective per sweep: an in-place SUM all-reduce of
-the int32 delta buffer [V*Kp nw delta | Kp nwsum delta] over the process group
-(RCCL over xGMI for the "nccl" backend; gloo for CPU tests).  Integer sums
-commute and every draw is keyed by the GLOBAL token index, so the result is
-bit-identical for any number of ranks (tests/test_distributed.py).
+Here that exchange is an in-place SUM all-reduce of the int32 delta buffer
+[V*Kp nw delta | Kp nwsum delta] over the process group (RCCL over xGMI for
+the "nccl" backend; gloo for CPU tests).  Integer sums commute and every draw
+is keyed by the GLOBAL token index, so the result is bit-identical for any
+number of ranks (tests/test_distributed.py).
+
+Split sweeps (engine.exchange_parts > 1, lda_set_exchange_parts): the shard's
+documents are sampled in P parts with one delta buffer each; part i's
+all-reduce is issued asynchronously as soon as part i has been sampled, so it
+runs while part i+1 samples, and only the last part's exchange is exposed.
+The snapshot does not change inside a sweep, so this is the same sweep, bit
+for bit, as the unsplit one (tests/test_distributed.py::*split*).
 """
 from __future__ import annotations
 
@@ -71,6 +78,7 @@ class ADLDATrainer:
         self.dist = dist
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
         self._delta = engine.delta_tensor() if self.world > 1 else None
+        self._part_deltas = {}
         self._initialised = False
         if self.world > 1 and not sync_before_reduce:
             self._check_stream_order()
@@ -112,7 +120,9 @@ class ADLDATrainer:
 
     def reduce_ms(self, last: int):
         """Mean duration (ms, CUDA events on torch's stream) of the last `last`
-        all-reduces (time_reduce=True; None when none were recorded)."""
+        all-reduces (time_reduce=True; None when none were recorded).  In a
+        split sweep this is the exposed part: from the last part's collective
+        being issued to every part's sum having landed."""
         evs = self._events[-last:] if last > 0 else []
         if not evs:
             return None
@@ -125,12 +135,54 @@ class ADLDATrainer:
         self.engine.apply()
         self._initialised = True
 
+    @property
+    def parts(self) -> int:
+        return int(getattr(self.engine, "exchange_parts", 1) or 1)
+
+    def _split_sweep(self, parts: int):
+        """One sweep in `parts` parts, part i's all-reduce overlapping part
+        i+1's sampling (async collectives; the engine's stream or, in the
+        default mode, a host sync orders each collective behind its part)."""
+        dist = self.dist
+        on_cuda = self._delta.device.type == "cuda"
+        works = []
+        ev = None
+        for i in range(parts):
+            self.engine.sample_part(i)
+            if self.sync_before_reduce:
+                self.engine.synchronize()
+            if i == parts - 1 and self.time_reduce and on_cuda:
+                import torch
+                ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                ev[0].record()
+            works.append(dist.all_reduce(self._part_delta(i), op=dist.ReduceOp.SUM,
+                                         group=self.group, async_op=True))
+        for w in works:
+            w.wait()           # the current stream waits for every part's sum
+        if ev is not None:
+            ev[1].record()      # exposed exchange: the last part's collective
+            self._events = (self._events + [ev])[-256:]
+        if self.sync_before_reduce and on_cuda:
+            import torch
+            torch.cuda.current_stream(self._delta.device).synchronize()
+
+    def _part_delta(self, i: int):
+        if i == 0:
+            return self._delta
+        if i not in self._part_deltas:
+            self._part_deltas[i] = self.engine.delta_tensor(i)
+        return self._part_deltas[i]
+
     def sweep(self, n: int = 1):
         if not self._initialised:
             self.init_counts()
+        parts = self.parts if self.world > 1 else 1
         for _ in range(n):
-            self.engine.sample()
-            self._reduce()
+            if parts > 1:
+                self._split_sweep(parts)
+            else:
+                self.engine.sample()
+                self._reduce()
             self.engine.apply()
 
     def log_likelihood(self) -> float:

@@ -51,37 +51,102 @@ void check(lda_status s, const char* where) {
 // One lda_ctx per GPU over a contiguous, token-balanced document range; the
 // delta buffers are summed in place with one RCCL all-reduce per sweep
 // (ncclCommInitAll over the shards' devices, grouped calls from this thread).
+//
+// Split sweeps (setExchangeParts, lda_set_exchange_parts): every shard samples
+// its documents in P parts with one delta buffer each; part i's all-reduce is
+// issued on a per-shard collective stream that waits only for part i, so it
+// runs while part i+1 samples, and the shards' streams wait for the last sum
+// before the apply.  Same sweep bit for bit (integer sums, fixed snapshot).
 class ShardGroup {
  public:
   std::vector<lda_ctx*> ctx;
   std::vector<int64_t> doc_begin;  // shard g owns documents [doc_begin[g], doc_begin[g+1])
   std::vector<ncclComm_t> comms;
+  std::vector<hipStream_t> comm_streams;  // per shard, split sweeps only
+  std::vector<hipEvent_t> events;
+  int parts = 1;
 
   ~ShardGroup() {
     for (auto c : comms) ncclCommDestroy(c);
+    for (size_t g = 0; g < comm_streams.size(); ++g) {
+      (void)hipSetDevice((int)g);
+      (void)hipEventDestroy(events[g]);
+      (void)hipStreamDestroy(comm_streams[g]);
+    }
     for (auto c : ctx) lda_destroy(c);
   }
 
-  void reduce() {
-    if (ctx.size() < 2) return;
+  hipStream_t stream(size_t g) {
+    void* s = nullptr;
+    check(lda_get_stream(ctx[g], &s), "lda_get_stream");
+    return static_cast<hipStream_t>(s);
+  }
+
+  // one grouped SUM all-reduce of part `part`'s delta buffers, each on
+  // streams[g] (the shard's own stream, or its collective stream)
+  void reduce_part(int part, const std::vector<hipStream_t>& streams) {
     std::vector<void*> ptr(ctx.size());
-    std::vector<hipStream_t> st(ctx.size());
     size_t count = 0;
-    for (size_t g = 0; g < ctx.size(); ++g) {
-      check(lda_delta_buffer(ctx[g], &ptr[g], &count), "lda_delta_buffer");
-      void* s = nullptr;
-      check(lda_get_stream(ctx[g], &s), "lda_get_stream");
-      st[g] = static_cast<hipStream_t>(s);
-    }
+    for (size_t g = 0; g < ctx.size(); ++g)
+      check(lda_delta_buffer_part(ctx[g], part, &ptr[g], &count), "lda_delta_buffer_part");
     ncclResult_t r = ncclGroupStart();
     for (size_t g = 0; g < ctx.size() && r == ncclSuccess; ++g)
-      r = ncclAllReduce(ptr[g], ptr[g], count, ncclInt32, ncclSum, comms[g], st[g]);
+      r = ncclAllReduce(ptr[g], ptr[g], count, ncclInt32, ncclSum, comms[g], streams[g]);
     const ncclResult_t r2 = ncclGroupEnd();
     if (r != ncclSuccess || r2 != ncclSuccess)
       raise(LDA_ERR_DEVICE, std::string("ncclAllReduce: ") + ncclGetErrorString(r != ncclSuccess ? r : r2));
   }
-  void sample() {
-    for (auto c : ctx) check(lda_sample(c), "lda_sample");
+
+  void reduce() {
+    if (ctx.size() < 2) return;
+    std::vector<hipStream_t> st(ctx.size());
+    for (size_t g = 0; g < ctx.size(); ++g) st[g] = stream(g);
+    reduce_part(0, st);
+  }
+
+  void set_parts(int p) {
+    parts = ctx.size() < 2 ? 1 : p;   // nothing to overlap on one GPU
+    for (auto c : ctx) check(lda_set_exchange_parts(c, parts, parts > 1 ? 8 : 0), "lda_set_exchange_parts");
+    if (parts > 1 && comm_streams.empty()) {
+      comm_streams.resize(ctx.size());
+      events.resize(ctx.size());
+      for (size_t g = 0; g < ctx.size(); ++g) {
+        if (hipSetDevice((int)g) != hipSuccess ||
+            hipStreamCreateWithFlags(&comm_streams[g], hipStreamNonBlocking) != hipSuccess ||
+            hipEventCreateWithFlags(&events[g], hipEventDisableTiming) != hipSuccess)
+          raise(LDA_ERR_DEVICE, "collective stream");
+      }
+    }
+  }
+
+  // sample + exchange + apply of one sweep
+  void sweep() {
+    if (ctx.size() < 2 || parts < 2) {
+      for (auto c : ctx) check(lda_sample(c), "lda_sample");
+      reduce();
+      apply();
+      return;
+    }
+    std::vector<hipStream_t> st(ctx.size());
+    for (size_t g = 0; g < ctx.size(); ++g) st[g] = stream(g);
+    auto hip = [](hipError_t e, const char* what) {
+      if (e != hipSuccess) raise(LDA_ERR_DEVICE, std::string(what) + ": " + hipGetErrorString(e));
+    };
+    for (int i = 0; i < parts; ++i) {
+      for (size_t g = 0; g < ctx.size(); ++g) {
+        check(lda_sample_part(ctx[g], i), "lda_sample_part");
+        hip(hipSetDevice((int)g), "hipSetDevice");
+        hip(hipEventRecord(events[g], st[g]), "hipEventRecord");           // part i sampled
+        hip(hipStreamWaitEvent(comm_streams[g], events[g], 0), "hipStreamWaitEvent");
+      }
+      reduce_part(i, comm_streams);
+    }
+    for (size_t g = 0; g < ctx.size(); ++g) {
+      hip(hipSetDevice((int)g), "hipSetDevice");
+      hip(hipEventRecord(events[g], comm_streams[g]), "hipEventRecord");   // every sum landed
+      hip(hipStreamWaitEvent(st[g], events[g], 0), "hipStreamWaitEvent");
+    }
+    apply();
   }
   void apply() {
     for (auto c : ctx) check(lda_apply(c), "lda_apply");
@@ -149,6 +214,12 @@ void ParallelTopicModel::setNumThreads(int32_t n) {
   if (n < 1) raise(LDA_ERR_INVALID_ARG, "numThreads must be >= 1");
   markDirty();
   num_threads_ = n;
+}
+
+void ParallelTopicModel::setExchangeParts(int32_t parts) {
+  if (parts < 1 || parts > LDA_MAX_EXCHANGE_PARTS) raise(LDA_ERR_INVALID_ARG, "parts out of range");
+  exchange_parts_ = parts;
+  if (shards_ && !shards_dirty_) shards_->set_parts(parts);
 }
 
 void ParallelTopicModel::setSampler(int32_t sampler) {
@@ -257,10 +328,18 @@ void ParallelTopicModel::ensureShards() {
   // the shards' local counts are the pending delta: sum them, apply
   sg->reduce();
   sg->apply();
+  sg->set_parts(exchange_parts_);
   for (auto c : sg->ctx) check(lda_set_sweep(c, sweep_), "lda_set_sweep");
   shards_ = std::move(sg);
   shards_dirty_ = false;
   z_dirty_ = true;
+  // word totals never change between addInstances calls: the bound of beta's
+  // countHistogram is taken once here, not by an O(N) pass per optimisation
+  {
+    std::vector<int32_t> totals((size_t)V_, 0);
+    for (int32_t w : words_) totals[(size_t)w]++;
+    max_word_total_ = totals.empty() ? 0 : *std::max_element(totals.begin(), totals.end());
+  }
   int32_t m = 0;
   for (int64_t d = 0; d < D; ++d) m = std::max<int32_t>(m, (int32_t)(doc_off_[d + 1] - doc_off_[d]));
   if (m != max_doc_len_) {  // statistics gathered so far stay valid unless the shape changes
@@ -333,9 +412,7 @@ void ParallelTopicModel::optimizeAlpha() {
 
 void ParallelTopicModel::optimizeBeta() {
   // countHistogram: nw cells by count, up to the largest word total
-  std::vector<int32_t> totals((size_t)V_, 0);
-  for (int32_t w : words_) totals[(size_t)w]++;
-  const int64_t max_count = totals.empty() ? 0 : *std::max_element(totals.begin(), totals.end());
+  const int64_t max_count = max_word_total_;
   std::vector<int32_t> hist((size_t)max_count + 1, 0);
   check(lda_count_histogram(shards_->ctx[0], max_count, hist.data()), "lda_count_histogram");
   // topicSizeHistogram, sparse: (tokens in topic, number of topics)
@@ -367,9 +444,7 @@ void ParallelTopicModel::estimate() {
   for (int32_t it = 1; it <= num_iterations_; ++it) {
     if (show_topics_interval_ != 0 && it % show_topics_interval_ == 0)
       log("\n" + displayTopWords(words_per_topic_, false));
-    shards_->sample();
-    shards_->reduce();
-    shards_->apply();
+    shards_->sweep();
     z_dirty_ = true;
     const bool opt = it > burnin_period_ && optimize_interval_ != 0;
     if (opt && it % save_sample_interval_ == 0)
@@ -392,6 +467,9 @@ void ParallelTopicModel::estimate() {
       }
     }
   }
+  // Mallet's estimate() returns when the sweeps are done: wait for the shards'
+  // streams (a kernel fault surfaces here, not in a later call)
+  for (auto c : shards_->ctx) check(lda_synchronize(c), "lda_synchronize");
 }
 
 std::vector<double> ParallelTopicModel::getTopicProbabilities(int64_t doc) {
@@ -740,6 +818,7 @@ TM_SETTER(ldatm_set_burnin_period, setBurninPeriod(n))
 TM_SETTER(ldatm_set_symmetric_alpha, setSymmetricAlpha(n != 0))
 TM_SETTER(ldatm_set_num_threads, setNumThreads(n))
 TM_SETTER(ldatm_set_sampler, setSampler(n))
+TM_SETTER(ldatm_set_exchange_parts, setExchangeParts(n))
 TM_SETTER(ldatm_set_verbosity, setVerbosity(n))
 TM_SETTER(ldatm_set_print_log_likelihood, setPrintLogLikelihood(n != 0))
 

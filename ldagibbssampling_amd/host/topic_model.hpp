@@ -48,6 +48,9 @@ class ParallelTopicModel {
   void setRandomSeed(int64_t seed);
   void setNumThreads(int32_t n);
   void setSampler(int32_t sampler);
+  // split sweeps across GPU shards: each shard's sweep in `parts` parts, part
+  // i's all-reduce overlapping part i+1's sampling (1 = one exchange per sweep)
+  void setExchangeParts(int32_t parts);
   void setVerbosity(int32_t v) { verbosity_ = v; }
   // state a Java-side ParallelTopicModel already holds (GpuParallelTopicModel:
   // Mallet's own addInstances topics, alpha/beta optimised in an earlier
@@ -111,11 +114,12 @@ class ParallelTopicModel {
   int32_t save_sample_interval_ = 10, show_topics_interval_ = 50, words_per_topic_ = 7;
   bool symmetric_alpha_ = false, print_log_likelihood_ = true;
   uint64_t seed_ = 0;
-  int32_t num_threads_ = 1, sampler_ = LDA_SAMPLER_DENSE, verbosity_ = 0;
+  int32_t num_threads_ = 1, sampler_ = LDA_SAMPLER_DENSE, verbosity_ = 0, exchange_parts_ = 1;
 
   std::unique_ptr<ShardGroup> shards_;
   bool shards_dirty_ = true;
   int32_t max_doc_len_ = -1;
+  int64_t max_word_total_ = 0;  // largest word frequency (countHistogram bound), set with the shards
   uint32_t sweep_ = 0;  // Philox sweep counter carried across re-sharding
   std::vector<int32_t> doc_len_counts_, topic_doc_counts_;  // alpha statistics
   std::vector<std::pair<int32_t, double>> ll_trace_;

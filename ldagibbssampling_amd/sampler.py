@@ -103,19 +103,38 @@ class GibbsSampler:
     def apply(self):
         capi.check(self._L.lda_apply(self._h), "lda_apply")
 
-    def delta_buffer(self):
+    def delta_buffer(self, part: int = 0):
         ptr, cnt = C.c_void_p(), C.c_size_t()
-        capi.check(self._L.lda_delta_buffer(self._h, C.byref(ptr), C.byref(cnt)), "lda_delta_buffer")
+        capi.check(self._L.lda_delta_buffer_part(self._h, int(part), C.byref(ptr), C.byref(cnt)),
+                   "lda_delta_buffer_part")
         return int(ptr.value), int(cnt.value)
 
-    def delta_tensor(self):
-        """Zero-copy torch int32 view of the pending delta (device memory)."""
+    def delta_tensor(self, part: int = 0):
+        """Zero-copy torch int32 view of the pending delta of split-sweep part
+        `part` (device memory; part 0 is lda_delta_buffer)."""
         import torch
 
-        ptr, cnt = self.delta_buffer()
+        ptr, cnt = self.delta_buffer(part)
         t = torch.as_tensor(_DeviceArray(ptr, cnt), device=f"cuda:{self.device}")
         assert t.data_ptr() == ptr and t.dtype == torch.int32
         return t
+
+    # ------------------------------------------------- split sweep (§5)
+    def set_exchange_parts(self, parts: int, reserve_cus: int = 0):
+        """Cut each sweep into `parts` token-balanced parts with their own delta
+        buffers, so one part's all-reduce can overlap the next part's sampling
+        (lda_set_exchange_parts)."""
+        capi.check(self._L.lda_set_exchange_parts(self._h, int(parts), int(reserve_cus)),
+                   "lda_set_exchange_parts")
+
+    @property
+    def exchange_parts(self) -> int:
+        n = C.c_int32()
+        capi.check(self._L.lda_get_exchange_parts(self._h, C.byref(n)), "lda_get_exchange_parts")
+        return n.value
+
+    def sample_part(self, part: int):
+        capi.check(self._L.lda_sample_part(self._h, int(part)), "lda_sample_part")
 
     def set_stream(self, stream_handle: int | None):
         capi.check(self._L.lda_set_stream(self._h, stream_handle), "lda_set_stream")

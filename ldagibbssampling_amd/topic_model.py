@@ -50,6 +50,7 @@ TM_SIGNATURES = {
     "ldatm_set_random_seed": (_i32, [_vp, C.c_int64]),
     "ldatm_set_num_threads": (_i32, [_vp, _i32]),
     "ldatm_set_sampler": (_i32, [_vp, _i32]),
+    "ldatm_set_exchange_parts": (_i32, [_vp, _i32]),
     "ldatm_set_topics": (_i32, [_vp, C.c_int64, _vp]),
     "ldatm_set_hyper": (_i32, [_vp, _vp, C.c_double, C.c_double]),
     "ldatm_get_sweep": (_i32, [_vp, C.POINTER(C.c_uint32)]),
@@ -276,6 +277,10 @@ class ParallelTopicModel:
 
     def setSampler(self, kind: str):
         _check(self._L.ldatm_set_sampler(self._h, capi.SAMPLERS[kind]), "setSampler")
+
+    def setExchangeParts(self, parts: int):
+        """Split sweeps across GPU shards (exchange overlapped with sampling)."""
+        _check(self._L.ldatm_set_exchange_parts(self._h, int(parts)), "setExchangeParts")
 
     # --------------------------------------------------------- training
     def estimate(self):

@@ -645,6 +645,19 @@ void orc_exact_sample(orc_exact* s, int frozen) {
   s->sweep++;
 }
 
+/* Documents [d0, d1) of the current sweep only (the sweep counter is not
+ * advanced; orc_exact_end_sweep does that): a split sweep's part, restated
+ * for the tests of the exchange-overlapped driver (lda_sample_part). */
+void orc_exact_sample_docs(orc_exact* s, int64_t d0, int64_t d1) {
+  if (d0 < 0) d0 = 0;
+  if (d1 > s->D) d1 = s->D;
+  if (d1 <= d0) return;
+  exact_sample_stream(s, s->doc_off + d0, s->words, s->z, d1 - d0, 0, s->sweep, STREAM_SAMPLE,
+                      s->token_base, s->delta);
+}
+
+void orc_exact_end_sweep(orc_exact* s) { s->sweep++; }
+
 void orc_exact_get_z(const orc_exact* s, int32_t* z) { memcpy(z, s->z, sizeof(int32_t) * s->N); }
 
 void orc_exact_get_counts(const orc_exact* s, int32_t* nw, int32_t* nwsum, int32_t* nd,

@@ -67,6 +67,8 @@ def lib():
     L.orc_exact_kpad.restype = C.c_int32
     L.orc_exact_kpad.argtypes = [C.c_void_p]
     L.orc_exact_sample.argtypes = [C.c_void_p, C.c_int]
+    L.orc_exact_sample_docs.argtypes = [C.c_void_p, C.c_int64, C.c_int64]
+    L.orc_exact_end_sweep.argtypes = [C.c_void_p]
     L.orc_exact_delta.restype = C.POINTER(C.c_int32)
     L.orc_exact_delta.argtypes = [C.c_void_p]
     L.orc_exact_apply.argtypes = [C.c_void_p]
@@ -205,6 +207,15 @@ class ExactSampler:
             raise RuntimeError("sample with a pending delta: apply first (as lda_sample)")
         lib().orc_exact_sample(self._h, 1 if frozen else 0)
         self._pending = not frozen
+
+    def sample_docs(self, d0: int, d1: int):
+        """Documents [d0, d1) of the current sweep into the delta, the sweep
+        counter unchanged (one part of a split sweep; end_sweep() advances)."""
+        lib().orc_exact_sample_docs(self._h, int(d0), int(d1))
+
+    def end_sweep(self):
+        lib().orc_exact_end_sweep(self._h)
+        self._pending = True
 
     def apply(self):
         lib().orc_exact_apply(self._h)

@@ -38,13 +38,56 @@ class OracleEngine:
         return self.s.log_likelihood_parts()
 
 
+class SplitOracleEngine(OracleEngine):
+    """cpu_exact behind the split-sweep engine interface (lda_sample_part /
+    lda_delta_buffer_part): part i's changes land in buffer i, which the
+    trainer all-reduces asynchronously while part i+1 samples."""
+
+    def __init__(self, sampler, parts):
+        super().__init__(sampler)
+        self.exchange_parts = parts
+        off = sampler.doc_off
+        n = int(off[-1] - off[0])
+        self.cuts = [0] + [int(np.searchsorted(off, off[0] + n * (i + 1) // parts, side="left"))
+                           for i in range(parts - 1)] + [sampler.D]
+        scratch = sampler.delta()
+        self.bufs = [np.zeros_like(scratch) for _ in range(parts)]
+        self.bufs[0][:] = scratch      # the shard's initial counts (pending at create)
+        scratch[:] = 0
+        self.next = 0
+
+    def sample(self):
+        for i in range(self.exchange_parts):
+            self.sample_part(i)
+
+    def sample_part(self, i):
+        assert i == self.next
+        scratch = self.s.delta()
+        self.s.sample_docs(self.cuts[i], self.cuts[i + 1])
+        self.bufs[i][:] = scratch
+        scratch[:] = 0
+        self.next = (i + 1) % self.exchange_parts
+        if self.next == 0:
+            self.s.end_sweep()
+
+    def apply(self):
+        scratch = self.s.delta()
+        for b in self.bufs:
+            scratch += b
+            b[:] = 0
+        self.s.apply()
+
+    def delta_tensor(self, part=0):
+        return torch.from_numpy(self.bufs[part])
+
+
 def _corpus():
     from ldagibbssampling_amd.corpus import synthetic_lda
     return synthetic_lda(num_docs=70, num_types=300, num_topics=K, doc_len=None, mean_len=40,
                          min_len=0, max_len=150, seed=13)
 
 
-def _worker(rank, world, port, outdir):
+def _worker(rank, world, port, outdir, parts=1):
     sys.path.insert(0, ROOT)
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -53,7 +96,8 @@ def _worker(rank, world, port, outdir):
     c = _corpus()
     sh = shard_corpus(c.doc_off, c.words, world, rank)
     o = O.ExactSampler(K, c.num_types, sh.doc_off, sh.words, 0.1, 0.01, SEED, token_base=sh.token_base)
-    tr = ADLDATrainer(OracleEngine(o))
+    tr = ADLDATrainer(OracleEngine(o) if parts == 1 else SplitOracleEngine(o, parts))
+    assert tr.parts == parts
     tr.sweep(SWEEPS)
     ll = tr.log_likelihood()
     nw, nwsum, _, _ = o.counts()
@@ -72,10 +116,13 @@ def _free_port():
     return p
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_gloo_adlda_matches_single(oracle, world):
+@pytest.mark.parametrize("world,parts", [(2, 1), (3, 1), (2, 3), (3, 2)])
+def test_gloo_adlda_matches_single(oracle, world, parts):
+    """parts > 1: split sweeps, every part's all-reduce overlapping the next
+    part's sampling (async gloo collectives) -- the same result bit for bit."""
     with tempfile.TemporaryDirectory() as d:
-        mp.start_processes(_worker, args=(world, _free_port(), d), nprocs=world, start_method="spawn")
+        mp.start_processes(_worker, args=(world, _free_port(), d, parts), nprocs=world,
+                           start_method="spawn")
         res = [np.load(os.path.join(d, f"r{r}.npz")) for r in range(world)]
     c = _corpus()
     single = oracle.ExactSampler(K, c.num_types, c.doc_off, c.words, 0.1, 0.01, SEED)

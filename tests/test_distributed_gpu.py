@@ -21,7 +21,7 @@ def _corpus():
                          min_len=0, max_len=300, seed=31)
 
 
-def _worker(rank, world, port, outdir, stream_ordered=False):
+def _worker(rank, world, port, outdir, stream_ordered=False, parts=1):
     sys.path.insert(0, ROOT)
     import torch
     import torch.distributed as dist
@@ -34,6 +34,8 @@ def _worker(rank, world, port, outdir, stream_ordered=False):
     sh = shard_corpus(c.doc_off, c.words, world, rank)
     g = GibbsSampler(K, c.num_types, sh.doc_off, sh.words, 0.1, 0.01, seed=SEED,
                      token_base=sh.token_base)
+    if parts > 1:
+        g.set_exchange_parts(parts, reserve_cus=8)    # split sweeps, async collectives
     if stream_ordered:
         # bench.py's arrangement: sampler and collective on one torch stream, no host sync
         st = torch.cuda.Stream()
@@ -59,8 +61,8 @@ def _worker(rank, world, port, outdir, stream_ordered=False):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("stream_ordered", [False, True])
-def test_two_ranks_one_gpu(oracle, stream_ordered):
+@pytest.mark.parametrize("stream_ordered,parts", [(False, 1), (True, 1), (False, 3), (True, 2)])
+def test_two_ranks_one_gpu(oracle, stream_ordered, parts):
     import socket
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
@@ -68,7 +70,7 @@ def test_two_ranks_one_gpu(oracle, stream_ordered):
     s.close()
     world = 2
     with tempfile.TemporaryDirectory() as d:
-        mp.start_processes(_worker, args=(world, port, d, stream_ordered), nprocs=world,
+        mp.start_processes(_worker, args=(world, port, d, stream_ordered, parts), nprocs=world,
                            start_method="spawn")
         res = [np.load(os.path.join(d, f"r{r}.npz")) for r in range(world)]
     c = _corpus()
