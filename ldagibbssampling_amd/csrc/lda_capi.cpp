@@ -220,8 +220,9 @@ struct lda_ctx {
   }
 };
 
-// Sparse-row capacities: min(Kp, total count of the word), fixed once the
-// global counts exist (word totals never change afterwards).
+// Sparse-row capacities: min(Kp, total count of the word) rounded up to whole
+// 64-entry rounds, fixed once the global counts exist (word totals never
+// change afterwards).
 static lda_status build_row_capacity(lda_ctx* c) {
   int32_t* caps = nullptr;
   HIP_TRY(dalloc(&caps, c->V));
@@ -233,7 +234,8 @@ static lda_status build_row_capacity(lda_ctx* c) {
   HIP_TRY(e);
   std::vector<int64_t> off(c->V + 1);
   off[0] = 0;
-  for (int w = 0; w < c->V; ++w) off[w + 1] = off[w] + h[w];
+  // whole rounds of 64 entries (k_build_sparse zero-fills the padding)
+  for (int w = 0; w < c->V; ++w) off[w + 1] = off[w] + ((h[w] + 63) & ~int64_t(63));
   HIP_TRY(dalloc(&c->row_off, c->V + 1));
   HIP_TRY(dalloc(&c->row_nnz, c->V));
   HIP_TRY(dalloc(&c->ent, (size_t)off[c->V]));

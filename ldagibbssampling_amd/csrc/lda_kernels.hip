@@ -1057,18 +1057,36 @@ __global__ __launch_bounds__(256) void k_sample_sparse(SampleParams p) {
 // lane's C topics is one pass over NG rows plus a ballot.  LDS holds a
 // per-block float2 {alpha, inv} table and per-wave 16-bit document counts
 // (documents < 65536 tokens); coefficients are recomputed where used, which
-// keeps SB_WAVES waves per CU resident.  The word part streams its rounds of
-// 64 entries (the first SB_RB of the next P tokens prefetched, the rest in
-// batches); the selected lane's rounds are re-walked one per lane, followed
-// by a serial readlane chain that reproduces the sum pass's order.
-// prefetched rounds per upcoming token / loads per streamed batch (A/B on C5:
-// 8/8 vs 2/4 is +13% near init, +15% after 30 sweeps; 127 VGPRs, 4 waves/SIMD)
+// keeps 16 waves per CU resident.
+//
+// The word part streams its rounds of 64 entries.  Rows are padded with zero
+// entries to whole rounds (k_build_sparse), so every round is one full-wave
+// load and a padding entry adds +0 (its count is 0; the own-token correction
+// saturates at 0, and a real entry of topic z_old always has a count >= 1).
+// The first SB_RB rounds of the next tokens sit in a ring of SB_NS slots.  The
+// slot of token t-1 is refilled with token t+SB_NS-1 right AFTER token t has
+// consumed its own rounds: vmcnt counts loads in issue order, so every wait in
+// token t then covers loads issued at least one token earlier (refilling at
+// the end of a token, the first use in the next token waited for the load
+// just issued).  Count changes go out per 64-token chunk (lane i: token i),
+// not per token, so no atomics sit between a refill and the next wait.
+// Each lane keeps its running B sum after each of the SB_RB register rounds,
+// so the selected lane's prefix search over them is one compare per round
+// (no re-walk); only rounds >= SB_RB of long rows are re-read, one per lane.
+// The sums and their order are those of oracle exact_draw_sparse.
 #ifndef SB_RB
-#define SB_RB 8
+#define SB_RB 10
 #endif
 #ifndef SB_BATCH
 #define SB_BATCH 8
 #endif
+#ifndef SB_NS
+#define SB_NS 3
+#endif
+#ifndef SB_GRP
+#define SB_GRP 1
+#endif
+static_assert(SB_RB % SB_GRP == 0 && SB_BATCH % SB_GRP == 0, "round groups");
 template <int C>
 constexpr int sb_waves() { return 16; }
 
@@ -1085,12 +1103,13 @@ __device__ __forceinline__ float row_scan16(float x) {
   return x;
 }
 
-template <int C, int P, bool FROZEN>
+template <int C, int NS, bool FROZEN>
 __global__ __launch_bounds__(64 * sb_waves<C>()) void k_sample_sparse_big(SampleParams p) {
   extern __shared__ __attribute__((aligned(16))) int32_t smem[];
   constexpr int KP = C * 64;
   constexpr int NG = C / 16;
   constexpr int WB = sb_waves<C>();
+  static_assert(NS >= 2 && NS <= 8, "ring slots");
   const int lane = threadIdx.x & 63;
   const int wid = threadIdx.x >> 6;
   const int row = lane >> 4, col = lane & 15;
@@ -1113,24 +1132,29 @@ __global__ __launch_bounds__(64 * sb_waves<C>()) void k_sample_sparse_big(Sample
     const float2 t = tab[k];
     return ((float)nd16_get(nd2, k) + t.x) * ((k == zc) ? invc : t.y);
   };
+  // one word-part term: coef[t] * float(c - [t == z_old]); SAT: the row holds
+  // a saturated count field, read the exact count from nw
+  auto term_of = [&](uint32_t e, int w, int zc, float invc, bool sat) -> float {
+    const int tq = (int)(e & ENT_TOPIC_MASK);
+    uint32_t cq = e >> ENT_TOPIC_BITS;
+    if (sat && cq == ENT_COUNT_SAT) cq = (uint32_t)nw[(int64_t)w * KP + tq];
+    if (!FROZEN) cq = __builtin_elementwise_sub_sat(cq, (uint32_t)(tq == zc));
+    return coef_at(tq, zc, invc) * (float)(int)cq;
+  };
   // one row pass: lane (row r, col j) evaluates topic owner*C + g*16 + j of
   // the (owner, g) its row was given; returns the in-row inclusive scan
   auto row_pass = [&](int owner, int g, int zc, float invc) -> float {
     return row_scan16(coef_at(owner * C + g * 16 + col, zc, invc) * beta);
   };
-  auto set_tg = [&](float (&TG)[NG], int owner, int g, float v) {
-#pragma unroll
-    for (int q = 0; q < NG; ++q)
-      if (q == g) TG[q] = (lane == owner) ? v : TG[q];
+  // the lane's NG group sums as one register vector: a wave-uniform group
+  // index becomes an indexed register move (an array was placed in scratch)
+  typedef float tg_t __attribute__((ext_vector_type(NG)));
+  auto set_tg = [&](tg_t& TG, int owner, int g, float v) {
+    const float cur = TG[g];
+    TG[g] = (lane == owner) ? v : cur;
   };
-  auto get_tg = [&](const float (&TG)[NG], int g) -> float {
-    float v = TG[0];
-#pragma unroll
-    for (int q = 1; q < NG; ++q)
-      if (q == g) v = TG[q];
-    return v;
-  };
-  auto lane_total = [&](const float (&TG)[NG]) -> float {
+  auto get_tg = [&](const tg_t& TG, int g) -> float { return TG[g]; };
+  auto lane_total = [&](const tg_t& TG) -> float {
     float t = TG[0];
 #pragma unroll
     for (int q = 1; q < NG; ++q) t = t + TG[q];
@@ -1165,7 +1189,19 @@ __global__ __launch_bounds__(64 * sb_waves<C>()) void k_sample_sparse_big(Sample
     int cn = cz;
     float cu = u01(draw_u32((uint64_t)(p.token_base + t0 + lane), p.c2, p.c3, p.k0, p.k1));
 
-    float TG[NG];
+    // the chunk's count changes, lane i = token i: two delta and two nwsum
+    // atomics when its topic changed (lanes past the range hold cz == cn)
+    auto flush_chunk = [&]() {
+      if (!FROZEN && cn != cz) {
+        const uint64_t rb = (uint64_t)(uint32_t)cw * (uint64_t)KP;
+        atomicAdd(p.delta + (rb + (uint32_t)cz), -1);
+        atomicAdd(p.delta + (rb + (uint32_t)cn), 1);
+        atomicAdd(p.dsum + cz, -1);
+        atomicAdd(p.dsum + cn, 1);
+      }
+    };
+
+    tg_t TG;
     // document start: every lane evaluates its own NG group trees serially
     // (the same additions as the row scan, element by element)
     auto build_doc = [&](int64_t ts, int64_t te) {
@@ -1183,9 +1219,7 @@ __global__ __launch_bounds__(64 * sb_waves<C>()) void k_sample_sparse_big(Sample
         for (int d = 1; d < 16; d <<= 1)
 #pragma unroll
           for (int j = 15; j >= d; --j) x[j] = x[j - d] + x[j];
-#pragma unroll
-        for (int q = 0; q < NG; ++q)
-          if (q == g) TG[q] = x[15];
+        TG[g] = x[15];
       }
     };
     auto clear_doc = [&]() {
@@ -1200,202 +1234,225 @@ __global__ __launch_bounds__(64 * sb_waves<C>()) void k_sample_sparse_big(Sample
     int64_t doc_end = p.doc_off[doc + 1];
     build_doc(t0, doc_end);
 
-    uint32_t ring[P][SB_RB];
-    float cinv[P];
-#pragma unroll
-    for (int s = 0; s < P; ++s) {
-      const int64_t tp = t0 + s;
-      const int n = readlane_i(cmn, s) & 0x7FFFFFFF;
-      const int64_t o = ((int64_t)readlane_i((int)(cmo >> 32), s) << 32) | (uint32_t)readlane_i((int)cmo, s);
+    // ring slot of token t: t % NS; slot (t + NS - 1) % NS is refilled during t
+    uint32_t ring[NS][SB_RB];
+    float cinv[NS];
+    // the first SB_RB rounds of token tp (< t1, at most 70 tokens past cbase)
+    auto prefetch = [&](uint32_t (&rg)[SB_RB], float& ci, int64_t tp) {
+      const int pidx = (int)(tp - cbase);
+      int np, zp;
+      int64_t op;
+      if (pidx < 64) {
+        np = readlane_i(cmn, pidx);
+        op = ((int64_t)readlane_i((int)(cmo >> 32), pidx) << 32) | (uint32_t)readlane_i((int)cmo, pidx);
+        zp = readlane_i(cz, pidx);
+      } else {
+        np = readlane_i(m1n, pidx - 64);
+        op = ((int64_t)readlane_i((int)(m1o >> 32), pidx - 64) << 32) |
+             (uint32_t)readlane_i((int)m1o, pidx - 64);
+        zp = readlane_i(z1, pidx - 64);
+      }
+      const int nrp = ((np & 0x7FFFFFFF) + 63) >> 6;
+      const uint32_t* rp = ent + op + lane;
 #pragma unroll
       for (int q = 0; q < SB_RB; ++q)
-        ring[s][q] = (tp < t1 && q * 64 + lane < n) ? ent[o + q * 64 + lane] : 0u;
-      if (!FROZEN) cinv[s] = inv_m1[(tp < t1) ? readlane_i(cz, s) : 0];
-    }
-
-    for (int64_t tb = t0; tb < t1; tb += P) {
+        if (q < nrp) rg[q] = rp[q * 64];
+      if (!FROZEN) ci = inv_m1[zp];
+    };
 #pragma unroll
-      for (int s = 0; s < P; ++s) {
+    for (int s = 0; s < NS - 1; ++s)
+      if (t0 + s < t1) prefetch(ring[s], cinv[s], t0 + s);
+
+    for (int64_t tb = t0; tb < t1; tb += NS) {
+#pragma unroll
+      for (int s = 0; s < NS; ++s) {
         const int64_t t = tb + s;
-        if (t >= t1) break;
-        int idx = (int)(t - cbase);
-        if (idx == 64) {
-          p.z[cbase + lane] = cn;
-          cbase += 64;
-          idx = 0;
-          cw = w1;
-          cz = z1;
-          cmn = m1n;
-          cmo = m1o;
-          w1 = w2;
-          z1 = z2;
-          m1n = row_nnz[w1];
-          m1o = row_off[w1];
-          cn = cz;
-          cu = u01(draw_u32((uint64_t)(p.token_base + cbase + lane), p.c2, p.c3, p.k0, p.k1));
-          if (cbase + 128 + lane < t1) {
-            w2 = p.words[cbase + 128 + lane];
-            z2 = p.z[cbase + 128 + lane];
-          }
-        }
-        if (t == doc_end) {
-          clear_doc();
-          ++doc;
-          while (p.doc_off[doc + 1] <= t) ++doc;
-          doc_end = p.doc_off[doc + 1];
-          build_doc(t, doc_end);
-        }
-
-        const int w = readlane_i(cw, idx);
-        const int zo = readlane_i(cz, idx);
-        const float u = readlane_f(cu, idx);
-        const int n_raw = readlane_i(cmn, idx);
-        const bool row_sat = n_raw < 0;           // the row holds a saturated count
-        const int n = n_raw & 0x7FFFFFFF;
-        const int64_t off = ((int64_t)readlane_i((int)(cmo >> 32), idx) << 32) | (uint32_t)readlane_i((int)cmo, idx);
-        const int lo = zo / C;
-        const int go = (zo % C) / 16;
-        // while the token is out: topic zc's coefficient uses invc (inv_m1[zo])
-        const int zc = FROZEN ? -1 : zo;
-        const float invc = FROZEN ? 0.0f : cinv[s];
-        const float g_saved = readlane_f(get_tg(TG, go), lo);
-
-        // remove the token from its document; re-evaluate its group
-        if (lane == 0) nd2[zo >> 1] -= (zo & 1) ? 0x10000u : 1u;
-        wave_lds_fence();
-        set_tg(TG, lo, go, readlane_f(row_pass(lo, go, zc, invc), 15));
-
-        // word part: rounds of 64 entries, lane l holds e = l + 64 r
-        const int nr_all = (n + 63) >> 6;
-        auto entry_b = [&](uint32_t e, bool valid, int& tq) -> float {
-          tq = (int)(e & ENT_TOPIC_MASK);
-          int cq = (int)(e >> ENT_TOPIC_BITS);
-          if (row_sat && valid && (uint32_t)cq == ENT_COUNT_SAT) cq = nw[(int64_t)w * KP + tq];
-          if (!FROZEN) cq -= (tq == zo) ? 1 : 0;
-          return valid ? coef_at(tq, zc, invc) * (float)cq : 0.0f;
-        };
-        float accB = 0.0f;
-#pragma unroll
-        for (int q = 0; q < SB_RB; ++q) {
-          if (q < nr_all) {
-            int tq;
-            accB = accB + entry_b(ring[s][q], q * 64 + lane < n, tq);
-          }
-        }
-        for (int q0 = SB_RB; q0 < nr_all; q0 += SB_BATCH) {
-          uint32_t eb[SB_BATCH];
-#pragma unroll
-          for (int b = 0; b < SB_BATCH; ++b) {
-            const int e = (q0 + b) * 64 + lane;
-            eb[b] = e < n ? ent[off + e] : 0u;
-          }
-#pragma unroll
-          for (int b = 0; b < SB_BATCH; ++b) {
-            if (q0 + b < nr_all) {
-              int tq;
-              accB = accB + entry_b(eb[b], (q0 + b) * 64 + lane < n, tq);
+        if (t < t1) {
+          int idx = (int)(t - cbase);
+          if (idx == 64) {
+            flush_chunk();
+            p.z[cbase + lane] = cn;
+            cbase += 64;
+            idx = 0;
+            cw = w1;
+            cz = z1;
+            cmn = m1n;
+            cmo = m1o;
+            w1 = w2;
+            z1 = z2;
+            m1n = row_nnz[w1];
+            m1o = row_off[w1];
+            cn = cz;
+            cu = u01(draw_u32((uint64_t)(p.token_base + cbase + lane), p.c2, p.c3, p.k0, p.k1));
+            if (cbase + 128 + lane < t1) {
+              w2 = p.words[cbase + 128 + lane];
+              z2 = p.z[cbase + 128 + lane];
             }
           }
-        }
-        const float TB = wave_incl_scan(accB);
-        const float TAs = wave_incl_scan(lane_total(TG));
-        const float sumB = readlane_f(TB, 63);
-        const float sumA = readlane_f(TAs, 63);
-        const float thr = u * (sumB + sumA);
-        int kn;
-        if (thr < sumB) {
-          const int nl = n < 64 ? n : 64;
-          const uint64_t m = __ballot((TB > thr) && (lane < nl));
-          const int lstar = m ? (int)__builtin_ctzll(m) : nl - 1;
-          const float E = lstar > 0 ? readlane_f(TB, lstar - 1) : 0.0f;
-          // lane q takes round q of lane lstar (entry lstar + 64 q)
-          const int nr = (n - lstar + 63) >> 6;
-          uint32_t e = 0u;
-#pragma unroll
-          for (int q = 0; q < SB_RB; ++q) {
-            const uint32_t rq = (uint32_t)readlane_i((int)ring[s][q], lstar);
-            if (lane == q) e = rq;
+          if (t == doc_end) {
+            clear_doc();
+            ++doc;
+            while (p.doc_off[doc + 1] <= t) ++doc;
+            doc_end = p.doc_off[doc + 1];
+            build_doc(t, doc_end);
           }
-          if (lane >= SB_RB && lane < nr) e = ent[off + lstar + 64 * lane];
-          int tq;
-          const float term = entry_b(e, lane < nr, tq);
-          // the sum pass's serial order: acc = ((t0 + t1) + t2) + ...
+
+          const int w = readlane_i(cw, idx);
+          const int zo = readlane_i(cz, idx);
+          const float u = readlane_f(cu, idx);
+          const int n_raw = readlane_i(cmn, idx);
+          const bool row_sat = n_raw < 0;           // the row holds a saturated count
+          const int n = n_raw & 0x7FFFFFFF;
+          const int64_t off = ((int64_t)readlane_i((int)(cmo >> 32), idx) << 32) | (uint32_t)readlane_i((int)cmo, idx);
+          const int lo = zo / C;
+          const int go = (zo % C) / 16;
+          // while the token is out: topic zc's coefficient uses invc (inv_m1[zo])
+          const int zc = FROZEN ? -1 : zo;
+          const float invc = FROZEN ? 0.0f : cinv[s];
+          const float g_saved = readlane_f(get_tg(TG, go), lo);
+
+          // remove the token from its document; re-evaluate its group
+          if (lane == 0) nd2[zo >> 1] -= (zo & 1) ? 0x10000u : 1u;
+          wave_lds_fence();
+          set_tg(TG, lo, go, readlane_f(row_pass(lo, go, zc, invc), 15));
+
+          // word part, register rounds: lane l holds entry l + 64 q; accq[q]
+          // = the lane's running sum after round q
+          const int nr_all = (n + 63) >> 6;
+          float accq[SB_RB];
           float acc = 0.0f;
-          int sel = nr - 1;
-          for (int q = 0; q < nr; ++q) {
-            acc = acc + readlane_f(term, q);
-            if (!(E + acc <= thr)) {
-              sel = q;
-              break;
+          // rounds in groups of SB_GRP under one uniform branch, so the
+          // group's LDS reads are in flight together (a round past the row's
+          // last one is evaluated and not added)
+          auto rounds = [&](bool sat) {
+#pragma unroll
+            for (int q = 0; q < SB_RB; q += SB_GRP) {
+              if (q < nr_all) {
+                float tt[SB_GRP];
+#pragma unroll
+                for (int g = 0; g < SB_GRP; ++g) tt[g] = term_of(ring[s][q + g], w, zc, invc, sat);
+#pragma unroll
+                for (int g = 0; g < SB_GRP; ++g) {
+                  const float na = acc + tt[g];
+                  acc = (g == 0 || q + g < nr_all) ? na : acc;
+                  accq[q + g] = acc;
+                }
+              } else {
+#pragma unroll
+                for (int g = 0; g < SB_GRP; ++g) accq[q + g] = acc;
+              }
+            }
+          };
+          if (!row_sat) rounds(false);
+          else rounds(true);
+          // every use of this token's ring slot is above: refill the slot of
+          // token t-1 now (the loads cannot move above this point)
+          asm volatile("" : "+v"(acc)::"memory");
+          {
+            const int sp = (s + NS - 1) % NS;
+            const int64_t tp = t + NS - 1;
+            if (tp < t1) prefetch(ring[sp], cinv[sp], tp);
+          }
+          // the rounds past SB_RB (long rows), streamed in batches
+          for (int q0 = SB_RB; q0 < nr_all; q0 += SB_BATCH) {
+            uint32_t eb[SB_BATCH];
+            const uint32_t* rp = ent + off + lane + q0 * 64;
+#pragma unroll
+            for (int b = 0; b < SB_BATCH; ++b) eb[b] = (q0 + b < nr_all) ? rp[b * 64] : 0u;
+#pragma unroll
+            for (int b = 0; b < SB_BATCH; b += SB_GRP) {
+              if (q0 + b < nr_all) {
+                float tt[SB_GRP];
+#pragma unroll
+                for (int g = 0; g < SB_GRP; ++g) tt[g] = term_of(eb[b + g], w, zc, invc, row_sat);
+#pragma unroll
+                for (int g = 0; g < SB_GRP; ++g) {
+                  const float na = acc + tt[g];
+                  acc = (g == 0 || q0 + b + g < nr_all) ? na : acc;
+                }
+              }
             }
           }
-          kn = readlane_i(tq, sel);
-        } else {
-          const float thr2 = thr - sumB;
-          const uint64_t m = __ballot((TAs > thr2) && (lane <= last_lane));
-          const int lstar = m ? (int)__builtin_ctzll(m) : last_lane;
-          const float E = lstar > 0 ? readlane_f(TAs, lstar - 1) : 0.0f;
-          // row r takes group r of lane lstar; group prefix P_{r-1} added on top
-          const float x = row_pass(lstar, row % NG, zc, invc);
-          float G[NG];
+          const float TB = wave_incl_scan(acc);
+          const float TAs = wave_incl_scan(lane_total(TG));
+          const float sumB = readlane_f(TB, 63);
+          const float sumA = readlane_f(TAs, 63);
+          const float thr = u * (sumB + sumA);
+          int kn;
+          if (thr < sumB) {
+            const int nl = n < 64 ? n : 64;
+            const uint64_t m = __ballot((TB > thr) && (lane < nl));
+            const int lstar = m ? (int)__builtin_ctzll(m) : nl - 1;
+            const float E = lstar > 0 ? readlane_f(TB, lstar - 1) : 0.0f;
+            const int nr = (n - lstar + 63) >> 6;  // rounds of lane lstar
+            // #{q : E + accq[q] <= thr} over lane lstar's register rounds; the
+            // sums are monotone and constant past its last round, so a count
+            // >= nr means "none exceeds" (oracle: the last round)
+            int cnt = 0;
 #pragma unroll
-          for (int q = 0; q < NG; ++q) G[q] = readlane_f(x, 16 * q + 15);
-          float base = 0.0f, Pq = G[0];
-#pragma unroll
-          for (int q = 1; q < NG; ++q) {
-            if (row == q) base = Pq;
-            Pq = Pq + G[q];
-          }
-          const float val = row == 0 ? x : base + x;
-          const int cnt = __builtin_popcountll(__ballot((E + val <= thr2) && lane < C));
-          const int last_j = (lstar < last_lane) ? C - 1 : (p.K - 1) % C;
-          kn = lstar * C + (cnt < C ? cnt : last_j);
-        }
-
-        // add the token back under its new topic
-        if (lane == 0) nd2[kn >> 1] += (kn & 1) ? 0x10000u : 1u;
-        wave_lds_fence();
-        if (kn == zo) {
-          set_tg(TG, lo, go, g_saved);        // the document is as before the removal
-        } else {
-          const int ln = kn / C, gn = (kn % C) / 16;
-          const float x = row_pass(row == 0 ? lo : ln, row == 0 ? go : gn, -1, 0.0f);
-          const float gl = readlane_f(x, 15), gk = readlane_f(x, 31);
-          set_tg(TG, lo, go, gl);
-          set_tg(TG, ln, gn, gk);
-        }
-        cn = (lane == idx) ? kn : cn;
-        if (!FROZEN && kn != zo) {
-          if (lane < 2) {
-            const int k = lane == 0 ? zo : kn;
-            const int v = lane == 0 ? -1 : 1;
-            atomicAdd(&p.delta[(int64_t)w * KP + k], v);
-            atomicAdd(&p.dsum[k], v);
-          }
-        }
-
-        // keep the pipeline full: token t+P
-        const int64_t tp = t + P;
-        if (tp < t1) {
-          const int pidx = (int)(tp - cbase);
-          int np, zp;
-          int64_t op;
-          if (pidx < 64) {
-            np = readlane_i(cmn, pidx) & 0x7FFFFFFF;
-            op = ((int64_t)readlane_i((int)(cmo >> 32), pidx) << 32) | (uint32_t)readlane_i((int)cmo, pidx);
-            zp = readlane_i(cz, pidx);
+            for (int q = 0; q < SB_RB; ++q) cnt = add_lane_bit(cnt, __ballot(E + accq[q] <= thr), lstar);
+            int sel;
+            if (cnt < nr && cnt < SB_RB) {
+              sel = cnt;
+              kn = (int)((uint32_t)readlane_i((int)ring[s][sel], lstar) & ENT_TOPIC_MASK);
+            } else if (nr <= SB_RB) {
+              sel = nr - 1;
+              kn = (int)((uint32_t)readlane_i((int)ring[s][sel], lstar) & ENT_TOPIC_MASK);
+            } else {
+              // rounds SB_RB.. of lane lstar, one per lane, continuing its sum
+              const int nx = nr - SB_RB;
+              const uint32_t e = lane < nx ? ent[off + lstar + 64 * (SB_RB + lane)] : 0u;
+              const float term = term_of(e, w, zc, invc, row_sat);
+              float a = readlane_f(accq[SB_RB - 1], lstar);
+              sel = nx - 1;
+              for (int q = 0; q < nx; ++q) {
+                a = a + readlane_f(term, q);
+                if (!(E + a <= thr)) {
+                  sel = q;
+                  break;
+                }
+              }
+              kn = (int)((uint32_t)readlane_i((int)e, sel) & ENT_TOPIC_MASK);
+            }
           } else {
-            np = readlane_i(m1n, pidx - 64) & 0x7FFFFFFF;
-            op = ((int64_t)readlane_i((int)(m1o >> 32), pidx - 64) << 32) |
-                 (uint32_t)readlane_i((int)m1o, pidx - 64);
-            zp = readlane_i(z1, pidx - 64);
-          }
+            const float thr2 = thr - sumB;
+            const uint64_t m = __ballot((TAs > thr2) && (lane <= last_lane));
+            const int lstar = m ? (int)__builtin_ctzll(m) : last_lane;
+            const float E = lstar > 0 ? readlane_f(TAs, lstar - 1) : 0.0f;
+            // row r takes group r of lane lstar; group prefix P_{r-1} added on top
+            const float x = row_pass(lstar, row % NG, zc, invc);
+            float G[NG];
 #pragma unroll
-          for (int q = 0; q < SB_RB; ++q) ring[s][q] = (q * 64 + lane < np) ? ent[op + q * 64 + lane] : 0u;
-          if (!FROZEN) cinv[s] = inv_m1[zp];
+            for (int q = 0; q < NG; ++q) G[q] = readlane_f(x, 16 * q + 15);
+            float base = 0.0f, Pq = G[0];
+#pragma unroll
+            for (int q = 1; q < NG; ++q) {
+              if (row == q) base = Pq;
+              Pq = Pq + G[q];
+            }
+            const float val = row == 0 ? x : base + x;
+            const int cnt = __builtin_popcountll(__ballot((E + val <= thr2) && lane < C));
+            const int last_j = (lstar < last_lane) ? C - 1 : (p.K - 1) % C;
+            kn = lstar * C + (cnt < C ? cnt : last_j);
+          }
+
+          // add the token back under its new topic
+          if (lane == 0) nd2[kn >> 1] += (kn & 1) ? 0x10000u : 1u;
+          wave_lds_fence();
+          if (kn == zo) {
+            set_tg(TG, lo, go, g_saved);        // the document is as before the removal
+          } else {
+            const int ln = kn / C, gn = (kn % C) / 16;
+            const float x = row_pass(row == 0 ? lo : ln, row == 0 ? go : gn, -1, 0.0f);
+            const float gl = readlane_f(x, 15), gk = readlane_f(x, 31);
+            set_tg(TG, lo, go, gl);
+            set_tg(TG, ln, gn, gk);
+          }
+          cn = (lane == idx) ? kn : cn;
         }
       }
     }
+    flush_chunk();
     if (cbase + lane < t1) p.z[cbase + lane] = cn;
     clear_doc();
   }
@@ -1425,7 +1482,8 @@ __global__ __launch_bounds__(256) void k_row_caps(const int32_t* __restrict__ nw
   }
 }
 
-// Compact every nw row into its sparse entries, topic ascending (one wave per row).
+// Compact every nw row into its sparse entries, topic ascending, zero-padded
+// to a whole number of 64-entry rounds (one wave per row).
 template <int C>
 __global__ __launch_bounds__(256) void k_build_sparse(const int32_t* __restrict__ nw, int64_t V,
                                                       const int64_t* __restrict__ row_off,
@@ -1455,6 +1513,12 @@ __global__ __launch_bounds__(256) void k_build_sparse(const int32_t* __restrict_
         ++pos;
       }
     }
+    // zero entries up to the next whole round of 64 (the capacity is padded
+    // to whole rounds): the large-K sampler loads full rounds, and a zero
+    // entry adds +0 to its sums
+    const int nnz = __shfl(incl, 63);
+    const int pad_end = (nnz + 63) & ~63;
+    if (nnz + lane < pad_end) ent[o + nnz + lane] = 0u;
     // sign bit: the row holds a saturated count (the sampler then checks
     // entries for the escape; otherwise it skips that per-entry branch)
     if (lane == 63) row_nnz[w] = row_sat ? (int32_t)((uint32_t)incl | 0x80000000u) : incl;
@@ -1897,7 +1961,7 @@ static size_t sparse_big_lds() {
   // {alpha, inv} table + per-wave 16-bit nd pairs; > 64 KiB at C = 64
   constexpr size_t lds = (2 * 64 * C + sb_waves<C>() * 32 * C) * sizeof(int32_t);
   static bool attr = [] {
-    return hipFuncSetAttribute(reinterpret_cast<const void*>(&k_sample_sparse_big<C, SPARSE_P, FROZEN>),
+    return hipFuncSetAttribute(reinterpret_cast<const void*>(&k_sample_sparse_big<C, SB_NS, FROZEN>),
                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) == hipSuccess;
   }();
   (void)attr;
@@ -1906,7 +1970,7 @@ static size_t sparse_big_lds() {
 template <int C, bool FROZEN>
 static hipError_t launch_sparse_big_t(const SampleParams& p, int blocks, hipStream_t st) {
   const size_t lds = sparse_big_lds<C, FROZEN>();
-  hipLaunchKernelGGL((k_sample_sparse_big<C, SPARSE_P, FROZEN>), dim3(blocks), dim3(64 * sb_waves<C>()),
+  hipLaunchKernelGGL((k_sample_sparse_big<C, SB_NS, FROZEN>), dim3(blocks), dim3(64 * sb_waves<C>()),
                      lds, st, p);
   return hipGetLastError();
 }
@@ -1914,7 +1978,7 @@ template <int C, bool FROZEN>
 static int occupancy_sparse_big_t() {
   int nb = 0;
   const size_t lds = sparse_big_lds<C, FROZEN>();
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_sample_sparse_big<C, SPARSE_P, FROZEN>,
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_sample_sparse_big<C, SB_NS, FROZEN>,
                                                    64 * sb_waves<C>(), lds) != hipSuccess)
     return 1;
   return nb > 0 ? nb : 1;

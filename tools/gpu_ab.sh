@@ -5,7 +5,8 @@ cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out
 CFG=${CFG:-c4}
 for b in ${BURNINS:-0}; do
-for v in default variants/*; do
+for v in default variants/*/liblda_mi355x.so; do
+  v=${v%/liblda_mi355x.so}
   if [ "$v" = default ]; then unset LDA_MI355X_LIB; else export LDA_MI355X_LIB=$PWD/$v/liblda_mi355x.so; fi
   n=$(basename $v)
   timeout -k 10 600 python bench.py --config $CFG ${SAMPLER:+--sampler $SAMPLER} --burnin $b --no-cpu-baseline --steps 10 --warmup 3 > gpurun_out/ab_${n}_b$b.log 2>&1 || { echo "$n FAILED"; tail -5 gpurun_out/ab_${n}_b$b.log; exit 1; }
