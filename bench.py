@@ -67,17 +67,27 @@ def _newest(pattern):
 def pmc_record(tokens_per_launch: int, kernel_prefix: str, K: int):
     """The newest committed rocprofv3 summary (profiles/rNN/traffic_*.json,
     tools/make_traffic.py over separate FETCH_SIZE / WRITE_SIZE / SQ passes of
-    this same command) measured on exactly the library loaded now (sha256),
-    for this workload and kernel; (None, None) otherwise."""
+    this same command) measured on the kernel code loaded now (the library's
+    sha256, or the sha256 of the kernel sources it is built from), for this
+    workload and kernel; (None, None) otherwise."""
     import hashlib
     from ldagibbssampling_amd import capi
     lib = os.environ.get("LDA_MI355X_LIB") or capi.LIB_PATH
     with open(lib, "rb") as f:
         lib_sha = hashlib.sha256(f.read()).hexdigest()
+    # the kernel sources the in-tree library is built from (a variant library
+    # loaded through LDA_MI355X_LIB matches by its own sha only)
+    src = hashlib.sha256()
+    for name in ("lda_kernels.hip", "lda_kernels.h"):
+        with open(os.path.join(ROOT, "ldagibbssampling_amd", "csrc", name), "rb") as f:
+            src.update(f.read())
+    src_sha = None if os.environ.get("LDA_MI355X_LIB") else src.hexdigest()
     for path in _newest("traffic_*.json"):
         with open(path) as f:
             t = json.load(f)
-        if (t.get("tokens_per_launch") == tokens_per_launch and t.get("lib_sha256") == lib_sha
+        same_code = t.get("lib_sha256") == lib_sha or (
+            src_sha is not None and t.get("kernel_src_sha256") == src_sha)
+        if (t.get("tokens_per_launch") == tokens_per_launch and same_code
                 and t.get("kernel", "").startswith(kernel_prefix)
                 and t.get("num_topics", K) == K):
             return t, os.path.relpath(path, ROOT)

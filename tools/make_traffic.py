@@ -7,9 +7,10 @@ roofline.traffic) from the rocprofv3 summaries of one profile run.
 summary_dir holds summary_kt.json (--kernel-trace --stats), summary_fetch.json
 (--pmc FETCH_SIZE) and summary_write.json (--pmc WRITE_SIZE), each its own
 rocprofv3 pass over the same bench command (tools/profile.sh).  Bytes follow
-MI355X_MICROARCH.md §HBM for gfx950: FETCH_SIZE/WRITE_SIZE are KiB and
-FETCH_SIZE counts half of a 16 B/lane coalesced read stream (the sampler's row
-gathers), so hbm = (2*FETCH_SIZE + WRITE_SIZE) * 1024.
+MI355X_MICROARCH.md §HBM for gfx950: FETCH_SIZE/WRITE_SIZE are KiB, and
+FETCH_SIZE's bytes per byte read depend on the access width, so each sampler
+kernel's FETCH is divided by the factor measured on known bytes of its own
+pattern (tools/fetch_calib.hip -> profiles/rNN/fetch_calib.json).
 When the SQ passes (summary_sq.json / summary_lds.json / summary_grbm.json)
 are there too, the per-token instruction mix and the effective clock are
 recorded as well: bench.py's issue-bound roofline reads them.
@@ -33,10 +34,51 @@ def _ctr(d, name, kernel, counter):
     return c["avg_per_dispatch"] if c else None
 
 
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def kernel_src_sha256():
+    """sha256 of the kernel sources (lda_kernels.hip + lda_kernels.h): the
+    counters belong to the machine code built from exactly these."""
+    import hashlib
+    h = hashlib.sha256()
+    for f in ("lda_kernels.hip", "lda_kernels.h"):
+        with open(os.path.join(ROOT, "ldagibbssampling_amd", "csrc", f), "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()
+
+
+def access_pattern(kernel):
+    """The calibrated load pattern (tools/fetch_calib.hip) of a sampler kernel:
+    its word rows are 16 B per lane at C >= 8, 4 B per lane at C = 2, and 4 B
+    per lane in 256 B rounds for the large-K sparse sampler."""
+    if kernel.startswith("k_sample_sparse_big"):
+        return "k_round4"
+    if kernel.startswith("k_sample<8") or kernel.startswith("k_sample<16"):
+        return "k_row16"
+    if kernel.startswith("k_sample<2"):
+        return "k_row4x2"
+    return None
+
+
+def fetch_factor(pattern):
+    """FETCH_SIZE bytes per byte read for this pattern, from the newest
+    profiles/rNN/fetch_calib.json; the guide's 1/2 for 16 B/lane streams when
+    no calibration covers it."""
+    import glob
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "fetch_calib.json")))[::-1]:
+        c = json.load(open(path))
+        if pattern and pattern in c and c[pattern].get("fetch_over_read"):
+            return c[pattern]["fetch_over_read"], os.path.relpath(path, ROOT) + ":" + pattern
+    return 0.5, "MI355X_MICROARCH.md §HBM (16 B/lane stream)"
+
+
 def main(d, kernel, tokens, workload, out, K=None):
     kt = json.load(open(os.path.join(d, "summary_kt.json")))
     fe = json.load(open(os.path.join(d, "summary_fetch.json")))["counters"][kernel]["FETCH_SIZE"]
     wr = json.load(open(os.path.join(d, "summary_write.json")))["counters"][kernel]["WRITE_SIZE"]
+    pat = access_pattern(kernel)
+    ff, fsrc = fetch_factor(pat)
     t = {
         "workload": workload,
         "kernel": kernel,
@@ -44,11 +86,13 @@ def main(d, kernel, tokens, workload, out, K=None):
         "avg_ns_kernel_trace": kt["kernels"][kernel]["avg_ns"],
         "FETCH_SIZE_KiB": fe["avg_per_dispatch"],
         "WRITE_SIZE_KiB": wr["avg_per_dispatch"],
-        "hbm_bytes_per_launch": (2 * fe["avg_per_dispatch"] + wr["avg_per_dispatch"]) * 1024,
+        "hbm_bytes_per_launch": (fe["avg_per_dispatch"] / ff + wr["avg_per_dispatch"]) * 1024,
         "hbm_bytes_per_launch_uncorrected": (fe["avg_per_dispatch"] + wr["avg_per_dispatch"]) * 1024,
-        "correction": "MI355X_MICROARCH.md §HBM: FETCH_SIZE (KiB) reads 1/2 of a 16 B/lane "
-                      "coalesced stream on gfx950 -> bytes = (2*FETCH_SIZE + WRITE_SIZE)*1024; "
-                      "FETCH_SIZE also counts Infinity-Cache hits",
+        "access_pattern": pat,
+        "fetch_size_per_byte_read": ff,
+        "correction": f"bytes = (FETCH_SIZE / {ff:.4f} + WRITE_SIZE) * 1024, the FETCH factor "
+                      f"calibrated on known bytes of this access pattern ({fsrc}); FETCH_SIZE also "
+                      "counts Infinity-Cache hits",
         "source": f"tools/profile.sh passes summarised in {d}",
     }
     tcc = os.path.join(d, "summary_tcc.json")
@@ -79,6 +123,7 @@ def main(d, kernel, tokens, workload, out, K=None):
         os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "ldagibbssampling_amd", "lib",
         "liblda_mi355x.so")
     t["lib_sha256"] = lib_sha256(lib)
+    t["kernel_src_sha256"] = kernel_src_sha256()
     with open(out, "w") as f:
         json.dump(t, f, indent=1)
     print(json.dumps(t, indent=1))
