@@ -17,6 +17,7 @@
 #include <cstdio>
 #include <cstring>
 #include <string>
+#include <cstdlib>
 #include <vector>
 
 #include "../../include/lda_mi355x.h"
@@ -142,6 +143,7 @@ struct lda_ctx {
   int64_t* row_off = nullptr;
   int32_t* row_nnz = nullptr;
   bool rows_ready = false;
+  bool half = false;    // dense K <= 128: the half-wave variant (LDA_DENSE_HALF=1)
   // 16-bit rows of the snapshot (LDA_SAMPLER_DENSE)
   uint16_t* nw16 = nullptr;
   uint8_t* wide = nullptr;
@@ -377,10 +379,14 @@ lda_status lda_create(lda_ctx** out, const lda_config* cfg, const int64_t* doc_o
     c->sample_blocks = lda::sample_sparse_blocks_per_cu(c->C, false) * c->cus;
     c->sample_blocks_frozen = lda::sample_sparse_blocks_per_cu(c->C, true) * c->cus;
   } else {
-    c->sample_blocks = lda::sample_blocks_per_cu(c->C, false) * c->cus;
-    c->sample_blocks_frozen = lda::sample_blocks_per_cu(c->C, true) * c->cus;
+    // the half-wave dense variant (two documents per wave, oracle
+    // exact_draw_half): opt-in, it measures slower than k_sample<C>
+    const char* hv = std::getenv("LDA_DENSE_HALF");
+    c->half = c->C <= 2 && hv && hv[0] == '1';
+    c->sample_blocks = lda::sample_blocks_per_cu(c->C, false, c->K, c->half) * c->cus;
+    c->sample_blocks_frozen = lda::sample_blocks_per_cu(c->C, true, c->K, c->half) * c->cus;
   }
-  c->waves_per_block = lda::sample_waves_per_block(c->C, c->sampler == LDA_SAMPLER_SPARSE);
+  c->waves_per_block = lda::sample_waves_per_block(c->C, c->sampler == LDA_SAMPLER_SPARSE, c->half);
   const int64_t waves = (int64_t)c->sample_blocks * c->waves_per_block;
   int64_t tpr = cfg->tokens_per_range;
   // ~32 ranges per wave: fine enough that the launch tail stays short (C4: +5%
@@ -515,7 +521,7 @@ static lda_status sample_part_impl(lda_ctx* c, int part) {
     if (c->sampler == LDA_SAMPLER_SPARSE)
       HIP_TRY(lda::launch_sample_sparse(c->C, false, p, blocks, c->stream));
     else
-      HIP_TRY(lda::launch_sample(c->C, false, p, blocks, c->stream));
+      HIP_TRY(lda::launch_sample(c->C, false, p, blocks, c->stream, c->half));
     HIP_TRY(hipEventRecord(c->ev1[slot], c->stream));
     c->launches++;
   }
@@ -925,7 +931,7 @@ lda_status lda_infer(lda_ctx* c, int64_t Dh, const int64_t* doc_off, const int32
     chk(hipMemsetAsync(q, 0, sizeof(int32_t), c->stream));
     if (e == hipSuccess)
       chk(c->sampler == LDA_SAMPLER_SPARSE ? lda::launch_sample_sparse(c->C, true, p, blocks, c->stream)
-                                           : lda::launch_sample(c->C, true, p, blocks, c->stream));
+                                           : lda::launch_sample(c->C, true, p, blocks, c->stream, c->half));
     if (it > burn_in && (it - burn_in) % thin == 0) {
       ++nsamples;
       if (e == hipSuccess) chk(lda::launch_doc_topics(dz, doff, Dh, c->K, c->Kp, acc, 1, c->stream));

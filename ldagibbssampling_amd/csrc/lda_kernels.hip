@@ -181,6 +181,10 @@ __device__ __forceinline__ float readlane_f(float v, int l) {
   return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), l));
 }
 __device__ __forceinline__ int uniform_i(int v) { return __builtin_amdgcn_readfirstlane(v); }
+__device__ __forceinline__ int64_t uniform_l(int64_t v) {
+  return (int64_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(v >> 32)) << 32) |
+                   (uint32_t)__builtin_amdgcn_readfirstlane((int)v));
+}
 
 // Lanes of one wavefront hand LDS values to each other (histogram atomics,
 // lane-0 updates read by every lane).  Without a fence that is a data race in
@@ -686,6 +690,386 @@ void k_sample(SampleParams p) {
     wave_lds_fence();
   }
 
+  if (!FROZEN) {
+    __syncthreads();
+    for (int i = threadIdx.x; i < KP; i += 256) {
+      const int v = bsum[i];
+      if (v != 0) atomicAdd(&p.dsum[i], v);
+    }
+  }
+}
+
+// ------------------------------------------- the half-wave dense sampler
+// An opt-in variant of the dense draw for K <= 128 (lda_capi.cpp:
+// LDA_DENSE_HALF=1; oracle exact_draw_half): two documents per wavefront.
+// Measured on C2 (K = 128) it is slower than k_sample<2>: 8.29 vs 9.60e9
+// tokens/s, VALU per token 69.7 vs 50.6 while SALU fell 45.5 -> 31.0
+// (profiles/r02/half_wave/).
+// K <= 128: two documents per wavefront.  Each 32-lane half runs its own
+// stream of work ranges (its own chunk registers, document counts and row
+// prefetches) and draws one token per step, so the per-token chain (LDS
+// round trip, scan, ballot, lane select, count) is paid once for two tokens.
+// Half-lane l (l = lane & 31) owns topics [l*CH, l*CH+CH), CH = 1, 2, 4 for
+// K <= 32, 64, 128; the draw is exact_draw_half of the oracle:
+//   S_j  = fma(a_j, b_j, S_{j-1})            (serial inside the half-lane)
+//   T    = 32-lane inclusive scan: row_shr 1,2,4,8 inside 16-lane rows, then
+//          row_bcast:15 into the half's second row
+//   thr  = u * T_31;  l* = first half-lane <= last with T > thr (else last)
+//   j*   = #{j : T_{l*-1} + S_j <= thr} clamped to the last valid topic
+// The per-half scalars (token index, chunk base, document end, next topic
+// to add back) are wave-uniform pairs; values the vector draw needs per
+// lane (u, thr, E, the new topic) are selected by half.  A half whose queue
+// ran dry idles (its draws write nothing) until the other half finishes.
+constexpr uint64_t kHalf0 = 0x00000000FFFFFFFFull;
+
+template <int CH>
+__device__ __forceinline__ void load_row16_half(uint32_t (&r)[(CH + 1) / 2], const uint16_t* __restrict__ p) {
+  if constexpr (CH == 4) {
+    const uint2 v = *reinterpret_cast<const uint2*>(p);
+    r[0] = v.x;
+    r[1] = v.y;
+  } else if constexpr (CH == 2) {
+    r[0] = *reinterpret_cast<const uint32_t*>(p);
+  } else {
+    r[0] = p[0];
+  }
+}
+
+// 32-lane inclusive scan inside each half (exact_draw_half's order)
+__device__ __forceinline__ float half_incl_scan(float x) {
+  x = dpp_mov<0x111, 0xf, true>(x) + x;
+  x = dpp_mov<0x112, 0xf, true>(x) + x;
+  x = dpp_mov<0x114, 0xf, true>(x) + x;
+  x = dpp_mov<0x118, 0xf, true>(x) + x;
+  asm("s_nop 1\n\tv_add_f32_dpp %0, %0, %0 row_bcast:15 row_mask:0xa bank_mask:0xf" : "+v"(x));
+  return x;
+}
+
+template <int CH, int P, bool FROZEN>
+__global__ __launch_bounds__(256) void k_sample_half(SampleParams p) {
+  extern __shared__ __attribute__((aligned(16))) int32_t smem[];
+  constexpr int KH = 32 * CH;                        // topics a half covers
+  constexpr int KP = KH < 64 ? 64 : KH;              // row stride of nw / nw16
+  constexpr int HD = (CH + 1) / 2;                   // dwords of a 16-bit row per lane
+  const int lane = threadIdx.x & 63;
+  const int wid = threadIdx.x >> 6;
+  const int hl = lane & 31;
+  const bool hi = lane >= 32;
+  float* t_alpha = reinterpret_cast<float*>(smem);   // [KP] per block
+  int32_t* bsum = smem + KP;                         // [KP] per-block nwsum delta
+  float* t_invm1 = reinterpret_cast<float*>(smem + 2 * KP);  // [KP]
+  // per wave and half: live doc counts nd[KH] and a = float(nd) + alpha [KH]
+  int32_t* ndw = smem + 3 * KP + wid * 4 * KH;
+  int32_t* nd_l = ndw + (hi ? 2 * KH : 0);           // this lane's half
+  float* av_l = reinterpret_cast<float*>(nd_l + KH);
+
+  for (int i = threadIdx.x; i < KP; i += 256) {
+    t_alpha[i] = p.alpha[i];
+    bsum[i] = 0;
+    t_invm1[i] = FROZEN ? 0.0f : p.inv_m1[i];
+  }
+  for (int i = threadIdx.x; i < 16 * KH; i += 256) smem[3 * KP + i] = 0;
+  __syncthreads();
+
+  float inv_r[CH];
+#pragma unroll
+  for (int j = 0; j < CH; ++j) inv_r[j] = p.inv[hl * CH + j];
+  const float beta = p.beta;
+  const int last_lane = (p.K - 1) / CH;
+  const int last_j_tail = (p.K - 1) % CH;
+  const uint64_t last_mask = __ballot(hl <= last_lane);
+  const uint16_t* __restrict__ nw16 = p.nw16;
+  const uint8_t* __restrict__ wide_of = p.wide;
+  const int32_t* __restrict__ nw = p.nw;
+  constexpr int kWordMask = 0x7FFFFFFF;
+
+  // per-half uniform state (two structs, not arrays: an array indexed by
+  // half was kept in vector registers and every check became a VALU compare)
+  struct Half {
+    int64_t t0, doc;
+    int nt, t, cbase, doc_end, ev, kp, inc;
+    int active, loaded;
+  };
+  Half H0 = {0, 0, 0, 0, 0, 0, 0, 0, 0, 1, 0};
+  Half H1 = H0;
+  // chunk registers: lane hl of half h <-> token HS(h).cbase + hl of its range
+  // (words carry the int32-row flag in bit 31), the next two chunks, and the
+  // word of token HS(h).cbase + hl + P for the prefetch
+  int cw = 0, cz = 0, cn = 0, w1 = 0, z1 = 0, w2 = 0, z2 = 0, pw = 0;
+  float cu = 0.0f;
+  uint32_t rows[P][HD];
+#pragma unroll
+  for (int s = 0; s < P; ++s)
+#pragma unroll
+    for (int q = 0; q < HD; ++q) rows[s][q] = 0u;
+
+#define HS(h) ((h) == 0 ? H0 : H1)
+  // lane i of the half <- x of half-lane i + S (across the next chunk)
+  auto half_shift = [&](int a, int b) -> int {
+    const int src = (lane & 32) | ((hl + P) & 31);
+    const int va = __shfl(a, src), vb = __shfl(b, src);
+    return hl + P < 32 ? va : vb;
+  };
+  // the half's finished chunk: new z out, count changes into the delta
+  auto flush_chunk = [&](int h) {
+    if ((lane >> 5) == h) {
+      const int n = HS(h).nt - HS(h).cbase;
+      if (hl < n) p.z[HS(h).t0 + HS(h).cbase + hl] = cn;
+      if (!FROZEN && cn != cz) {
+        const uint32_t row = (uint32_t)(cw & kWordMask) * (uint32_t)KP;
+        atomicAdd(p.delta + (row + (uint32_t)cz), -1);
+        atomicAdd(p.delta + (row + (uint32_t)cn), 1);
+        atomicAdd(&bsum[cz], -1);
+        atomicAdd(&bsum[cn], 1);
+      }
+    }
+  };
+  auto build_doc = [&](int h, int from) {
+    const int32_t* zr = p.z + HS(h).t0;
+    if ((lane >> 5) == h) {
+      for (int i = from + hl; i < HS(h).doc_end; i += 32) atomicAdd(&nd_l[zr[i]], 1);
+    }
+    wave_lds_fence();
+    if ((lane >> 5) == h) {
+#pragma unroll
+      for (int j = 0; j < CH; ++j) av_l[hl * CH + j] = (float)nd_l[hl * CH + j] + t_alpha[hl * CH + j];
+    }
+    wave_lds_fence();
+  };
+  auto clear_doc = [&](int h) {
+    if ((lane >> 5) == h) {
+#pragma unroll
+      for (int j = 0; j < CH; ++j) nd_l[hl * CH + j] = 0;
+    }
+    wave_lds_fence();
+  };
+  // rows of tokens HS(h).t .. HS(h).t+P-1 of half h into slots s0, s0+1, ...
+  auto prime = [&](int h, int s0) {
+#pragma unroll
+    for (int j = 0; j < P; ++j) {
+      const int wp = readlane_i(cw, 32 * h + j) & kWordMask;   // chunk 0 holds >= P tokens' ids
+      if ((lane >> 5) == h) load_row16_half<CH>(rows[(s0 + j) % P], nw16 + (int64_t)wp * KP + hl * CH);
+    }
+  };
+  // the next work range of half h (or idle when the queue is empty)
+  auto next_range = [&](int h, int s0) {
+    while (true) {
+      int r = 0;
+      if (lane == 32 * h) r = atomicAdd(p.queue, 1);
+      r = readlane_i(r, 32 * h);
+      if (r >= p.num_ranges) {
+        HS(h).active = 0;
+        HS(h).loaded = 0;
+        HS(h).ev = 0x7FFFFFFF;
+        HS(h).inc = 0;
+        HS(h).t = 0;                 // an idle half draws token 0 of a zero chunk
+        HS(h).cbase = 0;
+        HS(h).nt = 0;
+        if ((lane >> 5) == h) {
+          cw = 0;
+          cz = 0;
+          cn = 0;
+        }
+        return;
+      }
+      const int64_t d0 = p.range_doc[r], d1 = p.range_doc[r + 1];
+      const int64_t s = p.doc_off[d0];
+      const int n = (int)(p.doc_off[d1] - s);
+      if (n <= 0) continue;
+      HS(h).t0 = uniform_l(s);
+      HS(h).nt = uniform_i(n);
+      HS(h).t = 0;
+      HS(h).cbase = 0;
+      HS(h).loaded = 1;
+      const int32_t* wrd = p.words + s;
+      const int32_t* zr = p.z + s;
+      if ((lane >> 5) == h) {
+        cw = hl < n ? wrd[hl] : 0;
+        cz = hl < n ? zr[hl] : 0;
+        w1 = 32 + hl < n ? wrd[32 + hl] : 0;
+        z1 = 32 + hl < n ? zr[32 + hl] : 0;
+        w2 = 64 + hl < n ? wrd[64 + hl] : 0;
+        z2 = 64 + hl < n ? zr[64 + hl] : 0;
+        cw |= (int)wide_of[cw] << 31;
+        w1 |= (int)wide_of[w1] << 31;
+        cn = cz;
+        cu = u01(draw_u32((uint64_t)(p.token_base + s + hl), p.c2, p.c3, p.k0, p.k1));
+      }
+      const int sh = half_shift(cw, w1);
+      if ((lane >> 5) == h) pw = sh;
+      int64_t dd = d0;
+      while (p.doc_off[dd + 1] <= s) ++dd;
+      HS(h).doc = uniform_l(dd);
+      HS(h).doc_end = uniform_i((int)(p.doc_off[dd + 1] - s));
+      build_doc(h, 0);
+      HS(h).inc = 0;
+      HS(h).ev = uniform_i(min(32, HS(h).doc_end));
+      prime(h, s0);
+      return;
+    }
+  };
+  auto event = [&](int h, int s0) {
+    if (HS(h).t == HS(h).nt) {
+      // the range is done (or none was loaded yet)
+      if (HS(h).loaded) {
+        flush_chunk(h);
+        clear_doc(h);
+      }
+      next_range(h, s0);
+      return;
+    }
+    if (HS(h).t - HS(h).cbase == 32) {
+      flush_chunk(h);
+      HS(h).cbase = uniform_i(HS(h).cbase + 32);
+      const int n = HS(h).nt;
+      const int32_t* wrd = p.words + HS(h).t0;
+      const int32_t* zr = p.z + HS(h).t0;
+      if ((lane >> 5) == h) {
+        cw = w1;
+        cz = z1;
+        w1 = w2;
+        z1 = z2;
+        w1 |= (int)wide_of[w1] << 31;
+        cn = cz;
+        cu = u01(draw_u32((uint64_t)(p.token_base + HS(h).t0 + HS(h).cbase + hl), p.c2, p.c3, p.k0, p.k1));
+        if (HS(h).cbase + 64 + hl < n) {
+          w2 = wrd[HS(h).cbase + 64 + hl];
+          z2 = zr[HS(h).cbase + 64 + hl];
+        }
+      }
+      const int sh = half_shift(cw, w1);
+      if ((lane >> 5) == h) pw = sh;
+    }
+    if (HS(h).t == HS(h).doc_end) {
+      HS(h).inc = 0;                 // the pending add-back belonged to the last document
+      clear_doc(h);
+      int64_t dd = HS(h).doc + 1;
+      while (p.doc_off[dd + 1] - HS(h).t0 <= HS(h).t) ++dd;
+      HS(h).doc = uniform_l(dd);
+      HS(h).doc_end = uniform_i((int)(p.doc_off[dd + 1] - HS(h).t0));
+      build_doc(h, HS(h).t);
+    }
+    HS(h).ev = uniform_i(min(HS(h).cbase + 32, HS(h).doc_end));
+  };
+
+  while (true) {
+#pragma unroll
+    for (int s = 0; s < P; ++s) {
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+        if (HS(h).t == HS(h).ev) event(h, s);
+      if (!H0.active && !H1.active) goto done;
+
+      // ---- one token of each half
+      const int idx0 = H0.t - H0.cbase, idx1 = H1.t - H1.cbase;
+      const int wf0 = readlane_i(cw, idx0), wf1 = readlane_i(cw, 32 + idx1);
+      const int zo0 = readlane_i(cz, idx0), zo1 = readlane_i(cz, 32 + idx1);
+      const float u0 = readlane_f(cu, idx0), u1 = readlane_f(cu, 32 + idx1);
+      const int zo_l = hi ? zo1 : zo0;
+
+      // lanes 0 / 32: add the previous token of the half back under kp
+      // (deferred from its draw), then remove this one
+      if (hl == 0 && (hi ? H1.active : H0.active)) {
+        const int k = hi ? H1.kp : H0.kp;
+        const int ndk = nd_l[k] + (hi ? H1.inc : H0.inc);
+        nd_l[k] = ndk;
+        av_l[k] = (float)ndk + t_alpha[k];
+        const int ndz = nd_l[zo_l] - 1;
+        nd_l[zo_l] = ndz;
+        av_l[zo_l] = (float)ndz + t_alpha[zo_l];
+      }
+      wave_lds_fence();
+      float a[CH];
+      load_lds_f<CH>(a, av_l + hl * CH);
+      const float cinv = FROZEN ? 0.0f : t_invm1[zo_l];
+
+      // counts of the row (16-bit, or the int32 row for a word with a count
+      // > 65535: rare, uniform per half, drained in its branch)
+      int32_t cfull[CH];
+      const bool wide0 = wf0 < 0, wide1 = wf1 < 0;
+      if (wide0 || wide1) {
+        const bool mine = hi ? wide1 : wide0;
+        const int wl = (hi ? wf1 : wf0) & kWordMask;
+#pragma unroll
+        for (int j = 0; j < CH; ++j) {
+          const int c16 = (j & 1) ? (int)(rows[s][j >> 1] >> 16) : (int)(rows[s][j >> 1] & 0xFFFFu);
+          cfull[j] = mine ? nw[(int64_t)wl * KP + hl * CH + j] : (CH == 1 ? (int)rows[s][0] : c16);
+        }
+        __builtin_amdgcn_s_waitcnt(kVmcnt0);
+      } else {
+        if constexpr (CH == 1) {
+          cfull[0] = (int32_t)rows[s][0];
+        } else {
+#pragma unroll
+          for (int j = 0; j < CH; ++j)
+            cfull[j] = (j & 1) ? (int32_t)(rows[s][j >> 1] >> 16) : (int32_t)(rows[s][j >> 1] & 0xFFFFu);
+        }
+      }
+      // own-token correction: topic zo of each half, one vector compare per
+      // element against the lane's half's z_old (the scalar unit is the
+      // scarce one here)
+      bool own[CH];
+#pragma unroll
+      for (int j = 0; j < CH; ++j) own[j] = !FROZEN && (hl * CH + j == zo_l);
+      int32_t c_old = cfull[0];
+#pragma unroll
+      for (int j = 1; j < CH; ++j) c_old = own[j] ? cfull[j] : c_old;
+      const float bc = FROZEN ? 0.0f : ((float)(c_old - 1) + beta) * cinv;
+      float S[CH];
+      float acc = 0.0f;
+#pragma unroll
+      for (int j = 0; j < CH; ++j) {
+        const float bw = ((float)cfull[j] + beta) * inv_r[j];
+        const float b = own[j] ? bc : bw;
+        acc = __builtin_fmaf(a[j], b, acc);
+        S[j] = acc;
+      }
+
+      // the half scans and the two draws
+      const float T = half_incl_scan(acc);
+      const float thr0 = u0 * readlane_f(T, 31), thr1 = u1 * readlane_f(T, 63);
+      const float thr = hi ? thr1 : thr0;
+      const uint64_t m = __ballot(T > thr) & last_mask;
+      const int ls0 = first_lane_or(m & kHalf0, last_lane);
+      const int ls1 = first_lane_or(m >> 32, last_lane);
+      const float Tsh = dpp_mov<0x138, 0xf, true>(T);      // wave_shr:1
+      const float E0 = ls0 > 0 ? readlane_f(Tsh, ls0) : 0.0f;
+      const float E1 = ls1 > 0 ? readlane_f(Tsh, 32 + ls1) : 0.0f;
+      const float E = hi ? E1 : E0;
+      // each lane counts its own prefix; lane l* of each half is read
+      int cl = 0;
+#pragma unroll
+      for (int j = 0; j < CH; ++j) cl += (E + S[j] <= thr) ? 1 : 0;
+      const int cnt0 = readlane_i(cl, ls0), cnt1 = readlane_i(cl, 32 + ls1);
+      const int lim0 = ls0 < last_lane ? CH - 1 : last_j_tail;
+      const int lim1 = ls1 < last_lane ? CH - 1 : last_j_tail;
+      const int kn0 = ls0 * CH + (cnt0 < lim0 ? cnt0 : lim0);
+      const int kn1 = ls1 * CH + (cnt1 < lim1 ? cnt1 : lim1);
+
+      // the token goes back under kn with the half's next token; lane idx of
+      // each active half takes its new topic
+      const uint64_t upd = (H0.active ? (1ull << (uint32_t)idx0) : 0ull) |
+                           (H1.active ? (1ull << (uint32_t)(32 + idx1)) : 0ull);
+      cn = __builtin_amdgcn_inverse_ballot_w64(upd) ? (hi ? kn1 : kn0) : cn;
+      H0.kp = uniform_i(kn0);
+      H1.kp = uniform_i(kn1);
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        HS(h).inc = HS(h).active ? 1 : 0;
+        HS(h).t = uniform_i(HS(h).t + (HS(h).active ? 1 : 0));
+      }
+
+      // keep the pipeline full: the rows of each half's token t + P - 1 + 1
+      {
+        const int pi0 = (H0.t - 1 - H0.cbase) & 31, pi1 = (H1.t - 1 - H1.cbase) & 31;
+        const int wp0 = readlane_i(pw, pi0) & kWordMask, wp1 = readlane_i(pw, 32 + pi1) & kWordMask;
+        const int wp = hi ? wp1 : wp0;
+        load_row16_half<CH>(rows[s], nw16 + (int64_t)wp * KP + hl * CH);
+      }
+    }
+  }
+done:
+#undef HS
   if (!FROZEN) {
     __syncthreads();
     for (int i = threadIdx.x; i < KP; i += 256) {
@@ -1923,22 +2307,58 @@ static int occupancy_t() {
     default: break;                                               \
   }
 
+// the half-wave kernel (K <= 128): topics per half-lane
+int half_topics_per_lane(int K) { return K <= 32 ? 1 : (K <= 64 ? 2 : 4); }
+template <int CH>
+static constexpr size_t sample_half_lds() {
+  constexpr int KH = 32 * CH, KP = KH < 64 ? 64 : KH;
+  return (3 * KP + 16 * KH) * sizeof(int32_t);
+}
+template <int CH, bool FROZEN>
+static hipError_t launch_half_t(const SampleParams& p, int blocks, hipStream_t st) {
+  hipLaunchKernelGGL((k_sample_half<CH, SAMPLE_PH, FROZEN>), dim3(blocks), dim3(256), sample_half_lds<CH>(), st, p);
+  return hipGetLastError();
+}
+template <int CH, bool FROZEN>
+static int occupancy_half_t() {
+  int nb = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_sample_half<CH, SAMPLE_PH, FROZEN>, 256,
+                                                   sample_half_lds<CH>()) != hipSuccess)
+    return 1;
+  return nb > 0 ? nb : 1;
+}
 template <bool FROZEN>
-static hipError_t launch_sample_c(int C, const SampleParams& p, int blocks, hipStream_t st) {
+static hipError_t launch_sample_c(int C, const SampleParams& p, int blocks, hipStream_t st, bool half) {
+  if (half && C <= 2) {
+    switch (half_topics_per_lane(p.K)) {
+      case 1: return launch_half_t<1, FROZEN>(p, blocks, st);
+      case 2: return launch_half_t<2, FROZEN>(p, blocks, st);
+      default: return launch_half_t<4, FROZEN>(p, blocks, st);
+    }
+  }
   LDA_DISPATCH_C(C, launch_sample_t, p, blocks, st)
   return hipErrorInvalidValue;
 }
 template <bool FROZEN>
-static int occupancy_c(int C) {
+static int occupancy_c(int C, int K, bool half) {
+  if (half && C <= 2) {
+    switch (half_topics_per_lane(K)) {
+      case 1: return occupancy_half_t<1, FROZEN>();
+      case 2: return occupancy_half_t<2, FROZEN>();
+      default: return occupancy_half_t<4, FROZEN>();
+    }
+  }
   LDA_DISPATCH_C(C, occupancy_t)
   return 1;
 }
 
-hipError_t launch_sample(int C, bool frozen, const SampleParams& p, int blocks, hipStream_t st) {
-  return frozen ? launch_sample_c<true>(C, p, blocks, st) : launch_sample_c<false>(C, p, blocks, st);
+hipError_t launch_sample(int C, bool frozen, const SampleParams& p, int blocks, hipStream_t st,
+                         bool half) {
+  return frozen ? launch_sample_c<true>(C, p, blocks, st, half)
+                : launch_sample_c<false>(C, p, blocks, st, half);
 }
-int sample_blocks_per_cu(int C, bool frozen) {
-  return frozen ? occupancy_c<true>(C) : occupancy_c<false>(C);
+int sample_blocks_per_cu(int C, bool frozen, int K, bool half) {
+  return frozen ? occupancy_c<true>(C, K, half) : occupancy_c<false>(C, K, half);
 }
 
 template <int C, int P, int R0, bool FROZEN>
@@ -2014,9 +2434,10 @@ int sample_sparse_blocks_per_cu(int C, bool frozen) {
   return frozen ? occupancy_sparse_c<true>(C) : occupancy_sparse_c<false>(C);
 }
 
-int sample_waves_per_block(int C, bool sparse) {
+int sample_waves_per_block(int C, bool sparse, bool half) {
   if (sparse && C == 32) return sb_waves<32>();
   if (sparse && C == 64) return sb_waves<64>();
+  if (!sparse && half && C <= 2) return 8;   // two range workers per wave
   return 4;
 }
 

@@ -238,6 +238,7 @@ struct orc_exact {
   int64_t token_base;
   uint32_t sweep;
   int kind; /* 0 = dense draw, 1 = sparse (SparseLDA-split) draw */
+  int half; /* dense, K <= 128: the half-wave variant's draw (exact_draw_half) */
 };
 
 static void exact_prepare_topics(orc_exact* s) {
@@ -316,6 +317,7 @@ int32_t orc_exact_kpad(const orc_exact* s) { return s->Kp; }
 int32_t* orc_exact_delta(orc_exact* s) { return s->delta; }
 void orc_exact_set_sweep(orc_exact* s, uint32_t sweep) { s->sweep = sweep; }
 void orc_exact_set_kind(orc_exact* s, int kind) { s->kind = kind; }
+void orc_exact_set_half(orc_exact* s, int half) { s->half = half; }
 uint32_t orc_exact_get_sweep(const orc_exact* s) { return s->sweep; }
 
 void orc_exact_apply(orc_exact* s) {
@@ -415,6 +417,55 @@ static int exact_draw(const orc_exact* s, const int32_t* nwrow, const int32_t* n
     jsel = (lstar < last_lane) ? C - 1 : (K - 1) % C;
   }
   return lstar * C + jsel;
+}
+
+/* The half-wave dense draw (K <= 128; lda_kernels.hip: k_sample_half): two
+ * documents per wavefront, so one token's topics spread over the 32 lanes of
+ * a half, CH = 1, 2, 4 topics per lane for K <= 32, 64, 128.  The per-lane
+ * serial fma prefix is exact_draw's; the scan is the half's 32-lane one
+ * (row_shr 1,2,4,8 inside 16-lane rows, then row_bcast:15 into its second
+ * row), thr = u * T_31, and the lane / element selection follow exact_draw. */
+static int half_topics_per_lane(int K) { return K <= 32 ? 1 : (K <= 64 ? 2 : 4); }
+
+static int exact_draw_half(const orc_exact* s, const int32_t* nwrow, const int32_t* nd, int zo,
+                           float u, float* S) {
+  const int K = s->K, CH = half_topics_per_lane(K);
+  float t[32], y[32];
+  for (int l = 0; l < 32; ++l) {
+    float acc = 0.0f;
+    for (int j = 0; j < CH; ++j) {
+      const int k = l * CH + j;
+      int32_t c = nwrow[k];
+      float iv = s->inv[k];
+      if (k == zo) {
+        c -= 1;
+        iv = s->inv_m1[k];
+      }
+      const float b = ((float)c + s->beta_f) * iv;
+      const float a = (float)nd[k] + s->alpha_f[k];
+      acc = fmaf(a, b, acc);
+      S[k] = acc;
+    }
+    t[l] = acc;
+  }
+  for (int d = 1; d <= 8; d <<= 1) {
+    for (int l = 0; l < 32; ++l) y[l] = ((l & 15) >= d) ? t[l - d] : 0.0f;
+    for (int l = 0; l < 32; ++l) t[l] = y[l] + t[l];
+  }
+  for (int l = 16; l < 32; ++l) t[l] = t[l] + t[15];
+  const float thr = u * t[31];
+  const int last_lane = (K - 1) / CH;
+  int lstar = last_lane;
+  for (int l = 0; l <= last_lane; ++l)
+    if (t[l] > thr) {
+      lstar = l;
+      break;
+    }
+  const float E = lstar > 0 ? t[lstar - 1] : 0.0f;
+  int cnt = 0;
+  for (int j = 0; j < CH; ++j) cnt += (E + S[lstar * CH + j] <= thr) ? 1 : 0;
+  const int lim = lstar < last_lane ? CH - 1 : (K - 1) % CH;
+  return lstar * CH + (cnt < lim ? cnt : lim);
 }
 
 /* The sparse draw (kind 1, ldagibbssampling_amd/csrc/lda_kernels.hip:
@@ -552,7 +603,9 @@ static void exact_sample_docs(const orc_exact* s, const int64_t* doc_off, const 
       nd[zo]--;
       int kn = s->kind == 1
                    ? exact_draw_sparse(s, s->nw + (size_t)w * s->Kp, nd, frozen ? -1 : zo, u, S, et, ec)
-                   : exact_draw(s, s->nw + (size_t)w * s->Kp, nd, frozen ? -1 : zo, u, S);
+                   : (s->half && s->Kp <= 128)
+                         ? exact_draw_half(s, s->nw + (size_t)w * s->Kp, nd, frozen ? -1 : zo, u, S)
+                         : exact_draw(s, s->nw + (size_t)w * s->Kp, nd, frozen ? -1 : zo, u, S);
       nd[kn]++;
       z[i] = kn;
     }

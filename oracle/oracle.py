@@ -76,6 +76,7 @@ def lib():
     L.orc_exact_set_sweep.argtypes = [C.c_void_p, C.c_uint32]
     L.orc_exact_load_snapshot.argtypes = [C.c_void_p, _i32p, _i32p]
     L.orc_exact_set_kind.argtypes = [C.c_void_p, C.c_int]
+    L.orc_exact_set_half.argtypes = [C.c_void_p, C.c_int]
     L.orc_exact_get_sweep.restype = C.c_uint32
     L.orc_exact_get_sweep.argtypes = [C.c_void_p]
     L.orc_exact_get_z.argtypes = [C.c_void_p, _i32p]
@@ -173,7 +174,9 @@ class ExactSampler:
     """cpu_exact: the bit-exact definition of the GPU sampler (one shard)."""
 
     def __init__(self, K, V, doc_off, words, alpha, beta, seed, z_init=None, token_base=0,
-                 kind="dense"):
+                 kind="dense", half=False):
+        """half: the draw of the opt-in half-wave dense kernel (K <= 128,
+        LDA_DENSE_HALF=1 on the GPU side)."""
         self.K, self.V = int(K), int(V)
         self.doc_off = np.ascontiguousarray(doc_off, dtype=np.int64)
         self.words = np.ascontiguousarray(words, dtype=np.int32)
@@ -189,6 +192,7 @@ class ExactSampler:
         self.Kp = int(lib().orc_exact_kpad(self._h))
         self._pending = True      # create leaves the shard's counts as the pending delta
         lib().orc_exact_set_kind(self._h, {"dense": 0, "dense32": 0, "sparse": 1}[kind])
+        lib().orc_exact_set_half(self._h, 1 if half else 0)
 
     def __del__(self):
         h = getattr(self, "_h", None)

@@ -191,3 +191,34 @@ def test_large_k_selects_sparse_sampler(oracle):
     o, alpha, alpha_sum, beta, ll = _oracle_schedule(oracle, c, c.num_types, K, z0, alpha0, 50.0,
                                                      0.01, seed, 5, 12, 0, 200, 10, kind="sparse")
     _check(out, o, alpha, alpha_sum, beta, ll, K, c.num_types, 12)
+
+
+def test_checkpoint_resume_equals_uninterrupted(oracle):
+    """Checkpoint/resume (src/cmu_ron/TrainAndPredict.java:179-200): Mallet's
+    ObjectOutputStream saves the fields estimate() wrote back (topicSequence,
+    alpha, alphaSum, beta, betaSum) and the sweep-counter field of the
+    drop-in; a model read back and trained on continues the chain exactly:
+    estimate(15) -> save -> load -> estimate(25) == estimate(40).  (With
+    optimisation off: Mallet restarts its iteration counter, and so its
+    optimisation schedule, in every estimate() call.)"""
+    c = synthetic_lda(num_docs=150, num_types=600, num_topics=10, doc_len=None, mean_len=40,
+                      min_len=1, max_len=120, seed=21)
+    K, V, seed = 24, c.num_types, 17
+    z0 = np.random.default_rng(4).integers(0, K, c.num_tokens).astype(np.int32)
+    alpha0 = np.full(K, 6.0 / K)
+    hyper0 = np.array([6.0, 0.02, 0.02 * V])
+    whole = _run(K, V, c, z0, alpha0, hyper0, 0, [40, 200, 0, 10, 0, 2, 0], seed)
+    part = _run(K, V, c, z0, alpha0, hyper0, 0, [15, 200, 0, 10, 0, 2, 0], seed)
+    with tempfile.TemporaryDirectory() as d:   # the saved fields, written and read back
+        path = os.path.join(d, "model.npz")
+        np.savez(path, z=part["z"], alpha=part["alpha"], hyper=part["hyper"],
+                 sweep=np.int64(part["sweep"]))
+        st = np.load(path)
+        resumed = _run(K, V, c, st["z"], st["alpha"], st["hyper"], int(st["sweep"]),
+                       [25, 200, 0, 10, 0, 2, 0], seed)
+    np.testing.assert_array_equal(resumed["z"], whole["z"])
+    np.testing.assert_array_equal(resumed["rows"], whole["rows"])
+    np.testing.assert_array_equal(resumed["tpt"], whole["tpt"])
+    assert resumed["sweep"] == whole["sweep"] == 40
+    o, *_ = _oracle_schedule(oracle, c, V, K, z0, alpha0, 6.0, 0.02, seed, 0, 40, 0, 200, 10)
+    np.testing.assert_array_equal(whole["z"], o.z())

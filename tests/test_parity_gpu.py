@@ -400,3 +400,39 @@ def test_inference_skips_types_without_training_tokens(oracle, kind):
     tm = m.infer(off[:2], docs[0], n_iter=20, burn_in=4, thin=4, seed=5)
     np.testing.assert_allclose(tm[0], alpha / alpha.sum(), rtol=0, atol=1e-15)
     np.testing.assert_array_equal(tg[1], t_clean[0])
+
+
+@pytest.mark.parametrize("K", [3, 20, 48, 100, 128])
+def test_dense_half_wave_variant(oracle, K, monkeypatch):
+    """The opt-in half-wave dense kernel (two documents per wave, K <= 128;
+    LDA_DENSE_HALF=1) against its own oracle draw (exact_draw_half): ragged
+    documents (empty, one token, 1500 tokens) over short work ranges, so the
+    two halves switch ranges, chunks and documents at different steps and one
+    half idles at the end; counts > 65535 (the int32-row path) at K = 3;
+    inference (the frozen kernel)."""
+    from ldagibbssampling_amd.sampler import GibbsSampler
+    from ldagibbssampling_amd.corpus import Corpus
+    monkeypatch.setenv("LDA_DENSE_HALF", "1")
+    if K == 3:
+        rng = np.random.default_rng(2)
+        D, L = 8, 40000
+        words = np.where(rng.random(D * L) < 0.9, 0, rng.integers(1, 300, D * L)).astype(np.int32)
+        corpus = Corpus(np.arange(D + 1, dtype=np.int64) * L, words, 300)
+    else:
+        corpus = _ragged_corpus(D=150, V=700, seed=K)
+    alpha = np.full(K, 0.1)
+    g = GibbsSampler(K, corpus.num_types, corpus.doc_off, corpus.words, alpha, 0.01, seed=77 + K,
+                     tokens_per_range=100)
+    o = oracle.ExactSampler(K, corpus.num_types, corpus.doc_off, corpus.words, alpha, 0.01, 77 + K,
+                            half=True)
+    for n in (1, 2):
+        g.sweep(n)
+        o.sweep(n)
+        _assert_same_state(g, o, with_nd=K != 3)
+    if K == 3:
+        assert g.counts()[0].max() > 65535
+        return
+    held = _ragged_corpus(D=30, V=700, seed=K + 1, empty_every=7)
+    tg = g.infer(held.doc_off, held.words, n_iter=20, burn_in=5, thin=5, seed=3)
+    to = o.infer(held.doc_off, held.words, n_iter=20, burn_in=5, thin=5, seed=3)
+    np.testing.assert_allclose(tg, to, rtol=0, atol=1e-12)
