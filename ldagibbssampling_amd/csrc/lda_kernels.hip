@@ -1470,6 +1470,10 @@ __global__ __launch_bounds__(256) void k_sample_sparse(SampleParams p) {
 #ifndef SB_GRP
 #define SB_GRP 1
 #endif
+// batches whose per-lane end sums are kept for the draw's re-read
+#ifndef SB_NB
+#define SB_NB 2
+#endif
 static_assert(SB_RB % SB_GRP == 0 && SB_BATCH % SB_GRP == 0, "round groups");
 template <int C>
 constexpr int sb_waves() { return 16; }
@@ -1737,8 +1741,14 @@ __global__ __launch_bounds__(64 * sb_waves<C>()) void k_sample_sparse_big(Sample
             const int64_t tp = t + NS - 1;
             if (tp < t1) prefetch(ring[sp], cinv[sp], tp);
           }
-          // the rounds past SB_RB (long rows), streamed in batches
-          for (int q0 = SB_RB; q0 < nr_all; q0 += SB_BATCH) {
+          // the rounds past SB_RB (long rows), streamed in batches; the
+          // lane's running sum after each of the first SB_NB batches is kept
+          // so the draw re-reads one batch of the selected lane, not all
+          float accb[SB_NB];
+#pragma unroll
+          for (int i = 0; i < SB_NB; ++i) accb[i] = 0.0f;
+          int mb = 0;
+          for (int q0 = SB_RB; q0 < nr_all; q0 += SB_BATCH, ++mb) {
             uint32_t eb[SB_BATCH];
             const uint32_t* rp = ent + off + lane + q0 * 64;
 #pragma unroll
@@ -1756,6 +1766,8 @@ __global__ __launch_bounds__(64 * sb_waves<C>()) void k_sample_sparse_big(Sample
                 }
               }
             }
+#pragma unroll
+            for (int i = 0; i < SB_NB; ++i) accb[i] = (mb == i) ? acc : accb[i];
           }
           const float TB = wave_incl_scan(acc);
           const float TAs = wave_incl_scan(lane_total(TG));
@@ -1783,20 +1795,38 @@ __global__ __launch_bounds__(64 * sb_waves<C>()) void k_sample_sparse_big(Sample
               sel = nr - 1;
               kn = (int)((uint32_t)readlane_i((int)ring[s][sel], lstar) & ENT_TOPIC_MASK);
             } else {
-              // rounds SB_RB.. of lane lstar, one per lane, continuing its sum
-              const int nx = nr - SB_RB;
-              const uint32_t e = lane < nx ? ent[off + lstar + 64 * (SB_RB + lane)] : 0u;
-              const float term = term_of(e, w, zc, invc, row_sat);
-              float a = readlane_f(accq[SB_RB - 1], lstar);
-              sel = nx - 1;
-              for (int q = 0; q < nx; ++q) {
-                a = a + readlane_f(term, q);
-                if (!(E + a <= thr)) {
-                  sel = q;
-                  break;
+              // lane lstar's batches: the first whose end sum exceeds (its
+              // sums are monotone), among the SB_NB kept ones
+              const int nbl = (nr - SB_RB + SB_BATCH - 1) / SB_BATCH;
+              int cb = 0;
+#pragma unroll
+              for (int i = 0; i < SB_NB; ++i)
+                if (i < nbl && cb == i && E + readlane_f(accb[i], lstar) <= thr) cb = i + 1;
+              if (cb == nbl) {
+                sel = -1;                 // none exceeds: the lane's last round
+                const uint32_t e = (uint32_t)ent[off + lstar + 64 * (nr - 1)];
+                kn = (int)(e & ENT_TOPIC_MASK);
+              } else {
+                // rounds r0.. of lane lstar (one batch, or all the rest past the
+                // kept batches), one per lane, continuing its serial sum
+                const int r0 = SB_RB + SB_BATCH * cb;
+                const int nx = (cb < SB_NB ? min(nr, r0 + SB_BATCH) : nr) - r0;
+                const uint32_t e = lane < nx ? ent[off + lstar + 64 * (r0 + lane)] : 0u;
+                const float term = term_of(e, w, zc, invc, row_sat);
+                float a = readlane_f(accq[SB_RB - 1], lstar);
+#pragma unroll
+                for (int i = 0; i < SB_NB; ++i)
+                  if (cb == i + 1) a = readlane_f(accb[i], lstar);
+                sel = nx - 1;
+                for (int q = 0; q < nx; ++q) {
+                  a = a + readlane_f(term, q);
+                  if (!(E + a <= thr)) {
+                    sel = q;
+                    break;
+                  }
                 }
+                kn = (int)((uint32_t)readlane_i((int)e, sel) & ENT_TOPIC_MASK);
               }
-              kn = (int)((uint32_t)readlane_i((int)e, sel) & ENT_TOPIC_MASK);
             }
           } else {
             const float thr2 = thr - sumB;

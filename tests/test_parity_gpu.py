@@ -436,3 +436,28 @@ def test_dense_half_wave_variant(oracle, K, monkeypatch):
     tg = g.infer(held.doc_off, held.words, n_iter=20, burn_in=5, thin=5, seed=3)
     to = o.infer(held.doc_off, held.words, n_iter=20, burn_in=5, thin=5, seed=3)
     np.testing.assert_allclose(tg, to, rtol=0, atol=1e-12)
+
+
+def test_large_k_sparse_very_long_rows(oracle):
+    """Word rows far longer than the register rounds (K = 4096): rows of up
+    to ~3500 entries, so a draw can land in the register rounds, in either of
+    the batches whose running sums are kept, or past them (the re-read of
+    the rest of the selected lane), and the sparse rows are padded to whole
+    64-entry rounds."""
+    from ldagibbssampling_amd.corpus import Corpus
+    rng = np.random.default_rng(12)
+    D, L, V = 600, 300, 2000
+    p = np.empty(V)
+    p[:40] = np.geomspace(0.05, 0.002, 40)       # a few very frequent words
+    p[40:] = (1.0 - p[:40].sum()) / (V - 40)
+    words = rng.choice(V, size=D * L, p=p / p.sum()).astype(np.int32)
+    c = Corpus(np.arange(D + 1, dtype=np.int64) * L, words, V)
+    K = 4096
+    g, o = _pair(oracle, c, K, np.full(K, 0.05), 0.01, seed=31, kind="sparse")
+    g.sweep(2)
+    o.sweep(2)
+    _assert_same_state(g, o, with_nd=False)
+    nnz = (g.counts()[0] > 0).sum(1)
+    rounds = (nnz + 63) // 64
+    assert rounds.max() > 10 + 8 * 3                 # past every kept batch
+    assert ((rounds > 10) & (rounds <= 18)).any() and ((rounds > 18) & (rounds <= 26)).any()
