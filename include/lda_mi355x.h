@@ -226,6 +226,14 @@ lda_status lda_last_sample_ms(lda_ctx* ctx, float* ms);
  * lda_sample calls: bench.py reads the launches of its timed region. */
 lda_status lda_sample_times(lda_ctx* ctx, int32_t max, float* ms, int32_t* n);
 
+/* Diagnostics: the sampler's own uniform draws on the current device.
+ * out[i] = word 0 of Philox4x32-10 with counter {gtok[i] lo, gtok[i] hi, c2,
+ * c3} and key {seed lo, seed hi} -- the x0 every kernel draws (c2 = sweep,
+ * c3 = stream: 0 sample, 1 init, 2 inference).  Used to pin the device RNG
+ * against rocRAND's philox4x32_10 (tests/native/philox_vs_rocrand.hip). */
+lda_status lda_philox_draws(uint64_t seed, uint32_t c2, uint32_t c3, const int64_t* gtok, int64_t n,
+                            uint32_t* out);
+
 const char* lda_last_error(void);
 const char* lda_version(void);
 

@@ -21,6 +21,13 @@ def build_jni_harness() -> str:
     return os.path.join(ROOT, "tests", "jni", "bin", "estimate_harness")
 
 
+def build_native_tests() -> str:
+    """GPU test programs over the sampler ABI (tests/native/: the device RNG
+    against rocRAND's philox4x32_10)."""
+    subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "tests", "native")], check=True)
+    return os.path.join(ROOT, "tests", "native", "bin", "philox_vs_rocrand")
+
+
 def build_oracle() -> str:
     subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle")], check=True)
     return os.path.join(ROOT, "oracle", "lib", "liblda_oracle.so")

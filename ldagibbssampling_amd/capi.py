@@ -97,6 +97,7 @@ SIGNATURES = {
     "lda_last_sample_ms": (C.c_int32, [_vp, C.POINTER(C.c_float)]),
     "lda_row_stats": (C.c_int32, [_vp, C.POINTER(C.c_double)]),
     "lda_sample_times": (C.c_int32, [_vp, C.c_int32, _vp, C.POINTER(C.c_int32)]),
+    "lda_philox_draws": (C.c_int32, [C.c_uint64, C.c_uint32, C.c_uint32, _vp, C.c_int64, _vp]),
     "lda_last_error": (C.c_char_p, []),
     "lda_version": (C.c_char_p, []),
 }

@@ -635,6 +635,23 @@ lda_status lda_last_sample_ms(lda_ctx* c, float* ms) {
   return LDA_OK;
 }
 
+lda_status lda_philox_draws(uint64_t seed, uint32_t c2, uint32_t c3, const int64_t* gtok, int64_t n,
+                            uint32_t* out) {
+  if (n < 0 || (n > 0 && (!gtok || !out))) return fail(LDA_ERR_INVALID_ARG, "bad argument");
+  if (n == 0) return LDA_OK;
+  int64_t* dg = nullptr;
+  uint32_t* dout = nullptr;
+  hipError_t e = hipMalloc(&dg, sizeof(int64_t) * n);
+  if (e == hipSuccess) e = hipMalloc(&dout, sizeof(uint32_t) * n);
+  if (e == hipSuccess) e = hipMemcpy(dg, gtok, sizeof(int64_t) * n, hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = lda::launch_philox_draws(dg, n, c2, c3, seed, dout, nullptr);
+  if (e == hipSuccess) e = hipMemcpy(out, dout, sizeof(uint32_t) * n, hipMemcpyDeviceToHost);
+  (void)hipFree(dg);
+  (void)hipFree(dout);
+  HIP_TRY(e);
+  return LDA_OK;
+}
+
 lda_status lda_sample_times(lda_ctx* c, int32_t max, float* ms, int32_t* n) {
   if (!c || !n || max < 0 || (max > 0 && !ms)) return fail(LDA_ERR_INVALID_ARG, "bad argument");
   const int64_t avail = std::min<int64_t>(c->launches, lda_ctx::LDA_TIME_RING);

@@ -106,6 +106,8 @@ struct TopicTables {
 // nwsum/tables (k_apply + k_build_packed + k_prepare_topics in one launch)
 hipError_t launch_apply_packed(int32_t* nw, int32_t* delta, int64_t V, int32_t Kp, uint16_t* nw16,
                                uint8_t* wide, const TopicTables& t, hipStream_t st);
+hipError_t launch_philox_draws(const int64_t* gtok, int64_t n, uint32_t c2, uint32_t c3, uint64_t seed,
+                               uint32_t* out, hipStream_t st);
 hipError_t launch_init_z(int32_t* z, int64_t n, int32_t K, int64_t token_base, uint32_t k0,
                          uint32_t k1, hipStream_t st);
 hipError_t launch_count(const int32_t* words, const int32_t* z, int64_t n, int32_t Kp,

@@ -1939,6 +1939,14 @@ __global__ __launch_bounds__(256) void k_build_sparse(const int32_t* __restrict_
   }
 }
 
+// the draws of given global token indices (lda_philox_draws diagnostics)
+__global__ __launch_bounds__(256) void k_philox_draws(const int64_t* __restrict__ gtok, int64_t n,
+                                                      uint32_t c2, uint32_t c3, uint32_t k0,
+                                                      uint32_t k1, uint32_t* __restrict__ out) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256)
+    out[i] = draw_u32((uint64_t)gtok[i], c2, c3, k0, k1);
+}
+
 // ----------------------------------------------------------- count kernels
 __global__ __launch_bounds__(256) void k_init_z(int32_t* __restrict__ z, int64_t n, int32_t K,
                                                 int64_t token_base, uint32_t k0, uint32_t k1) {
@@ -2469,6 +2477,15 @@ int sample_waves_per_block(int C, bool sparse, bool half) {
   if (sparse && C == 64) return sb_waves<64>();
   if (!sparse && half && C <= 2) return 8;   // two range workers per wave
   return 4;
+}
+
+hipError_t launch_philox_draws(const int64_t* gtok, int64_t n, uint32_t c2, uint32_t c3, uint64_t seed,
+                               uint32_t* out, hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  const int blocks = (int)std::min<int64_t>((n + 255) / 256, 4096);
+  hipLaunchKernelGGL(k_philox_draws, dim3(blocks), dim3(256), 0, st, gtok, n, c2, c3, (uint32_t)seed,
+                     (uint32_t)(seed >> 32), out);
+  return hipGetLastError();
 }
 
 hipError_t launch_row_caps(const int32_t* nw, int64_t V, int32_t Kp, int32_t* caps, hipStream_t st) {
