@@ -30,5 +30,9 @@ for cfg in c4 c1 c2 c3 c5; do
   python3 -c "import json;d=json.loads(open('$O/bench_$cfg.jsonl').read());r=d['roofline'];i=r.get('issue') or {};print('$cfg', round(d['value']/1e9,4),'Gtok/s frac',round(r['frac'],3),'traffic_frac',r.get('traffic_frac'),'issue',i.get('binding'),i.get('frac'))"
 done
 timeout -k 10 120 python bench.py --config c5 --burnin 30 --no-cpu-baseline > $O/bench_c5_b30.log 2>&1 && tail -1 $O/bench_c5_b30.log > $O/bench_c5_b30.jsonl
+timeout -k 10 120 python bench.py --config c4 --burnin 30 --no-cpu-baseline > $O/bench_c4_b30.log 2>&1 && tail -1 $O/bench_c4_b30.log > $O/bench_c4_b30.jsonl
+# the whole C4 corpus (2e9 tokens, int64 offsets) in one context on one GPU
+timeout -k 10 300 python bench.py --config c4full --no-cpu-baseline --steps 5 --warmup 2 > $O/bench_c4full.log 2>&1 && tail -1 $O/bench_c4full.log > $O/bench_c4full.jsonl
+python3 -c "import json;d=json.loads(open('$O/bench_c4full.jsonl').read());print('c4full', round(d['value']/1e9,4),'Gtok/s', d['ms_per_step'],'ms/step')"
 timeout -k 10 600 python tools/opt_cost.py > $O/opt_cost.json 2> $O/opt_cost.log || { echo OPT_COST FAILED; tail -5 $O/opt_cost.log; exit 1; }
 cat $O/opt_cost.json
