@@ -242,6 +242,10 @@ def main():
     ap.add_argument("--reserve-cus", type=int, default=8,
                     help="split sweeps: CUs' worth of sampler blocks left free for RCCL")
     args = ap.parse_args()
+    if os.environ.get("LDA_BENCH_STACKS"):
+        # diagnostics: every rank dumps its Python stacks every N s to stderr
+        import faulthandler
+        faulthandler.dump_traceback_later(int(os.environ["LDA_BENCH_STACKS"]), repeat=True)
 
     import torch
     import torch.distributed as dist
