@@ -144,6 +144,15 @@ struct lda_ctx {
   int32_t* row_nnz = nullptr;
   bool rows_ready = false;
   bool half = false;    // dense K <= 128: the half-wave variant (LDA_DENSE_HALF=1)
+  // lda_infer: word totals of the snapshot (TopicInferencer's empty-row test),
+  // valid while apply_gen == totals_gen, and grow-only scratch buffers, so a
+  // one-document call (the reference's predict loop) costs no allocation and
+  // no pass over nw
+  uint64_t apply_gen = 0, totals_gen = ~0ull;
+  std::vector<int32_t> word_totals;
+  int32_t *inf_words = nullptr, *inf_z = nullptr, *inf_acc = nullptr, *inf_q = nullptr;
+  int64_t *inf_doff = nullptr, *inf_range = nullptr;
+  size_t inf_cap[6] = {};
   // 16-bit rows of the snapshot (LDA_SAMPLER_DENSE)
   uint16_t* nw16 = nullptr;
   uint8_t* wide = nullptr;
@@ -180,7 +189,8 @@ struct lda_ctx {
     for (void* p : {(void*)words, (void*)z, (void*)doc_off, (void*)range_doc, (void*)queue,
                     (void*)nw, (void*)nwsum, (void*)delta, (void*)alpha_d, (void*)alpha_f,
                     (void*)inv, (void*)inv_m1, (void*)partial, (void*)nonzero, (void*)ent,
-                    (void*)row_off, (void*)row_nnz, (void*)nw16, (void*)wide})
+                    (void*)row_off, (void*)row_nnz, (void*)nw16, (void*)wide, (void*)inf_words,
+                    (void*)inf_z, (void*)inf_acc, (void*)inf_q, (void*)inf_doff, (void*)inf_range})
       if (p) (void)hipFree(p);
     for (int i = 1; i < LDA_MAX_EXCHANGE_PARTS; ++i)
       if (delta_part[i]) (void)hipFree(delta_part[i]);
@@ -250,6 +260,7 @@ static lda_status build_row_capacity(lda_ctx* c) {
 static lda_status apply_impl(lda_ctx* c) {
   if (c->next_part != 0)
     return fail(LDA_ERR_STATE, "lda_apply inside a split sweep: sample every part first");
+  c->apply_gen++;
   HIP_TRY(hipSetDevice(c->device));
   // a split sweep's later parts are folded into part 0's buffer (the one the
   // apply kernels read) and zeroed
@@ -882,25 +893,28 @@ lda_status lda_infer(lda_ctx* c, int64_t Dh, const int64_t* doc_off, const int32
     if (words_in[i] < 0 || words_in[i] >= c->V) return fail(LDA_ERR_INVALID_ARG, "word id out of range (OOV must be removed)");
   HIP_TRY(hipSetDevice(c->device));
   // TopicInferencer skips tokens whose type has no training tokens (an empty
-  // typeTopicCounts row): drop them here (row totals of the global snapshot)
-  std::vector<int64_t> off(Dh + 1);
-  std::vector<int32_t> kept;
-  {
+  // typeTopicCounts row): drop them here (row totals of the global snapshot,
+  // computed once per snapshot)
+  if (c->totals_gen != c->apply_gen) {
     int32_t* caps = nullptr;
     HIP_TRY(dalloc(&caps, c->V));
-    std::vector<int32_t> h(c->V);
+    c->word_totals.assign((size_t)c->V, 0);
     hipError_t e = lda::launch_row_caps(c->nw, c->V, c->Kp, caps, c->stream);
-    if (e == hipSuccess) e = hipMemcpyAsync(h.data(), caps, sizeof(int32_t) * c->V, hipMemcpyDeviceToHost, c->stream);
+    if (e == hipSuccess)
+      e = hipMemcpyAsync(c->word_totals.data(), caps, sizeof(int32_t) * c->V, hipMemcpyDeviceToHost, c->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
     (void)hipFree(caps);
     HIP_TRY(e);
-    kept.reserve((size_t)N_in);
-    off[0] = 0;
-    for (int64_t d = 0; d < Dh; ++d) {
-      for (int64_t i = doc_off[d] - doc_off[0]; i < doc_off[d + 1] - doc_off[0]; ++i)
-        if (h[words_in[i]] > 0) kept.push_back(words_in[i]);
-      off[d + 1] = (int64_t)kept.size();
-    }
+    c->totals_gen = c->apply_gen;
+  }
+  std::vector<int64_t> off(Dh + 1);
+  std::vector<int32_t> kept;
+  kept.reserve((size_t)N_in);
+  off[0] = 0;
+  for (int64_t d = 0; d < Dh; ++d) {
+    for (int64_t i = doc_off[d] - doc_off[0]; i < doc_off[d + 1] - doc_off[0]; ++i)
+      if (c->word_totals[(size_t)words_in[i]] > 0) kept.push_back(words_in[i]);
+    off[d + 1] = (int64_t)kept.size();
   }
   const int32_t* words = kept.data();
   const int64_t N = off[Dh];
@@ -908,24 +922,34 @@ lda_status lda_infer(lda_ctx* c, int64_t Dh, const int64_t* doc_off, const int32
     for (int64_t d = 0; d < Dh; ++d)
       if (off[d + 1] - off[d] > LDA_MAX_DOC_TOKENS_BIGK)
         return fail(LDA_ERR_UNSUPPORTED, "document longer than 65535 tokens with num_topics > 1024");
-  int32_t *dw = nullptr, *dz = nullptr, *acc = nullptr, *q = nullptr;
-  int64_t *doff = nullptr, *drange = nullptr;
   std::vector<int64_t> ranges = make_ranges(off, std::max<int64_t>(16, std::min<int64_t>(c->tokens_per_range, N / std::max<int64_t>(1, (int64_t)c->sample_blocks_frozen * c->waves_per_block * 8))));
   const int64_t R = (int64_t)ranges.size() - 1;
   hipError_t e = hipSuccess;
   auto chk = [&](hipError_t x) {
     if (e == hipSuccess) e = x;
   };
-  chk(dalloc(&dw, N));
-  chk(dalloc(&dz, N));
-  chk(dalloc(&acc, (size_t)std::max<int64_t>(Dh, 1) * c->K));
-  chk(dalloc(&q, 4));
-  chk(dalloc(&doff, Dh + 1));
-  chk(dalloc(&drange, ranges.size()));
+  // grow-only scratch (kept by the context between calls)
+  auto need = [&](auto*& ptr, size_t n, int slot) {
+    if (e != hipSuccess || n <= c->inf_cap[slot]) return;
+    if (ptr) (void)hipFree(ptr);
+    ptr = nullptr;
+    c->inf_cap[slot] = 0;
+    chk(dalloc(&ptr, n));
+    if (e == hipSuccess) c->inf_cap[slot] = n;
+  };
+  need(c->inf_words, (size_t)std::max<int64_t>(N, 1), 0);
+  need(c->inf_z, (size_t)std::max<int64_t>(N, 1), 1);
+  need(c->inf_acc, (size_t)std::max<int64_t>(Dh, 1) * c->K, 2);
+  need(c->inf_q, (size_t)std::max<int32_t>(n_iter, 1), 3);   // one work-queue counter per iteration
+  need(c->inf_doff, (size_t)Dh + 1, 4);
+  need(c->inf_range, ranges.size(), 5);
+  int32_t *dw = c->inf_words, *dz = c->inf_z, *acc = c->inf_acc, *q = c->inf_q;
+  int64_t *doff = c->inf_doff, *drange = c->inf_range;
   if (e == hipSuccess && N > 0) chk(hipMemcpyAsync(dw, words, sizeof(int32_t) * N, hipMemcpyHostToDevice, c->stream));
   if (e == hipSuccess) chk(hipMemcpyAsync(doff, off.data(), sizeof(int64_t) * (Dh + 1), hipMemcpyHostToDevice, c->stream));
   if (e == hipSuccess) chk(hipMemcpyAsync(drange, ranges.data(), sizeof(int64_t) * ranges.size(), hipMemcpyHostToDevice, c->stream));
   if (e == hipSuccess) chk(hipMemsetAsync(acc, 0, sizeof(int32_t) * (size_t)std::max<int64_t>(Dh, 1) * c->K, c->stream));
+  if (e == hipSuccess) chk(hipMemsetAsync(q, 0, sizeof(int32_t) * (size_t)std::max<int32_t>(n_iter, 1), c->stream));
   if (e == hipSuccess) chk(lda::launch_infer_init(dw, dz, N, c->nw, c->K, c->Kp, c->stream));
   int32_t nsamples = 0;
   lda::SampleParams p = c->params(true);
@@ -934,7 +958,6 @@ lda_status lda_infer(lda_ctx* c, int64_t Dh, const int64_t* doc_off, const int32
   p.doc_off = doff;
   p.range_doc = drange;
   p.num_ranges = R;
-  p.queue = q;
   p.delta = nullptr;
   p.dsum = nullptr;
   p.token_base = 0;
@@ -945,10 +968,9 @@ lda_status lda_infer(lda_ctx* c, int64_t Dh, const int64_t* doc_off, const int32
   const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>(c->sample_blocks_frozen, (R + wpb - 1) / wpb));
   for (int32_t it = 1; it <= n_iter && e == hipSuccess && N > 0; ++it) {
     p.c2 = (uint32_t)(it - 1);
-    chk(hipMemsetAsync(q, 0, sizeof(int32_t), c->stream));
-    if (e == hipSuccess)
-      chk(c->sampler == LDA_SAMPLER_SPARSE ? lda::launch_sample_sparse(c->C, true, p, blocks, c->stream)
-                                           : lda::launch_sample(c->C, true, p, blocks, c->stream, c->half));
+    p.queue = q + (it - 1);
+    chk(c->sampler == LDA_SAMPLER_SPARSE ? lda::launch_sample_sparse(c->C, true, p, blocks, c->stream)
+                                         : lda::launch_sample(c->C, true, p, blocks, c->stream, c->half));
     if (it > burn_in && (it - burn_in) % thin == 0) {
       ++nsamples;
       if (e == hipSuccess) chk(lda::launch_doc_topics(dz, doff, Dh, c->K, c->Kp, acc, 1, c->stream));
@@ -962,8 +984,6 @@ lda_status lda_infer(lda_ctx* c, int64_t Dh, const int64_t* doc_off, const int32
   if (e == hipSuccess && Dh > 0)
     chk(hipMemcpyAsync(acc_h.data(), acc, sizeof(int32_t) * (size_t)Dh * c->K, hipMemcpyDeviceToHost, c->stream));
   if (e == hipSuccess) chk(hipStreamSynchronize(c->stream));
-  for (void* ptr : {(void*)dw, (void*)dz, (void*)acc, (void*)q, (void*)doff, (void*)drange})
-    if (ptr) (void)hipFree(ptr);
   HIP_TRY(e);
   for (int64_t d = 0; d < Dh; ++d) {
     double sum = 0.0;
