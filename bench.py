@@ -350,6 +350,11 @@ def main():
         bpt = bytes_per_token(K)
         kname = (("k_sample_sparse_big" if K > 1024 else "k_sample_sparse")
                  if args.sampler == "sparse" else "k_sample")
+        if args.sampler != "sparse" and sampler.Kp <= 128:
+            # K <= 128 picks its dense kernel as lda_create does (LDA_DENSE_HALF:
+            # unset/2 quarter-wave, 1 half-wave, 0 full-wave k_sample<C>)
+            hv = os.environ.get("LDA_DENSE_HALF", "2")[:1]
+            kname = {"0": "k_sample", "1": "k_sample_half"}.get(hv, "k_sample_quarter")
         if nnz0 is not None:
             # the sparse samplers read 4 B per nonzero entry of the token's word
             # row (token-weighted mean over the timed region's snapshots) + 16 B

@@ -34,6 +34,9 @@ constexpr uint32_t STREAM_INFER = 2u;
 #ifndef SAMPLE_PH
 #define SAMPLE_PH 4
 #endif
+#ifndef SAMPLE_PQ
+#define SAMPLE_PQ 4
+#endif
 // sparse sampler: tokens in flight, 64-entry rounds prefetched per token
 #ifndef SPARSE_P
 #define SPARSE_P 4
@@ -76,12 +79,13 @@ constexpr uint32_t ENT_TOPIC_BITS = 12;
 constexpr uint32_t ENT_TOPIC_MASK = (1u << ENT_TOPIC_BITS) - 1;
 constexpr uint32_t ENT_COUNT_SAT = (1u << (32 - ENT_TOPIC_BITS)) - 1;
 
-// half: the half-wave variant k_sample_half (C <= 2 only; lda_capi.cpp:
-// LDA_DENSE_HALF), otherwise k_sample<C>
+// half: 1 = the half-wave variant k_sample_half, 2 = the quarter-wave
+// k_sample_quarter (C <= 2 only; lda_capi.cpp: LDA_DENSE_HALF), 0 = k_sample<C>
 hipError_t launch_sample(int C, bool frozen, const SampleParams& p, int blocks, hipStream_t st,
-                         bool half = false);
-int sample_blocks_per_cu(int C, bool frozen, int K, bool half = false);
+                         int half = 0);
+int sample_blocks_per_cu(int C, bool frozen, int K, int half = 0);
 int half_topics_per_lane(int K);
+int quarter_topics_per_lane(int K);
 hipError_t launch_sample_sparse(int C, bool frozen, const SampleParams& p, int blocks,
                                 hipStream_t st);
 int sample_sparse_blocks_per_cu(int C, bool frozen);
@@ -129,7 +133,7 @@ hipError_t launch_ll_words(const int32_t* nw, int64_t V, int32_t K, int32_t Kp, 
 // range workers per block of the sampler kernel used for (C, sampler): 4
 // waves, 16 for the large-K sparse kernel (C >= 32), 8 for the half-wave
 // dense kernel (4 waves x 2 halves)
-int sample_waves_per_block(int C, bool sparse, bool half = false);
+int sample_waves_per_block(int C, bool sparse, int half = 0);
 hipError_t launch_row_stats(const int32_t* nw, int64_t V, int32_t K, int32_t Kp,
                             unsigned long long* out, hipStream_t st);
 hipError_t launch_doc_hist(const int32_t* z, const int64_t* doc_off, int64_t D, int32_t K, int32_t Kp,

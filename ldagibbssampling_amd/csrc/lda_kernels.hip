@@ -1079,6 +1079,334 @@ done:
   }
 }
 
+// ------------------------------------------ the quarter-wave dense sampler
+// K <= 128: four documents per wavefront, one per 16-lane DPP row.  Each row
+// (quarter) runs its own stream of work ranges; every per-document quantity
+// is a per-lane vector that is uniform inside the row (token index, chunk
+// base, document end, next topic to add back), so one step draws one token of
+// each quarter with row-local DPP (scan, broadcast) and ds_bpermute instead of
+// the full-wave kernel's scalar unit.  Row-lane l owns topics [l*CH, l*CH+CH),
+// CH = 1, 2, 4, 8 for K <= 16, 32, 64, 128 (oracle exact_draw_quarter):
+//   S_j = fma(a_j, b_j, S_{j-1});  T = inclusive row scan (row_shr 1,2,4,8)
+//   thr = u * T_15;  l* = first row-lane <= last with T > thr (else last)
+//   j*  = #{j : T_{l*-1} + S_j <= thr} clamped to the last valid topic
+template <int CH>
+__device__ __forceinline__ void load_row16_q(uint32_t (&r)[(CH + 1) / 2], const uint16_t* __restrict__ p) {
+  if constexpr (CH == 8) {
+    const uint4 v = *reinterpret_cast<const uint4*>(p);
+    r[0] = v.x;
+    r[1] = v.y;
+    r[2] = v.z;
+    r[3] = v.w;
+  } else if constexpr (CH == 4) {
+    const uint2 v = *reinterpret_cast<const uint2*>(p);
+    r[0] = v.x;
+    r[1] = v.y;
+  } else if constexpr (CH == 2) {
+    r[0] = *reinterpret_cast<const uint32_t*>(p);
+  } else {
+    r[0] = p[0];
+  }
+}
+__device__ __forceinline__ int row_bcast15_i(int v) { return __builtin_amdgcn_update_dpp(0, v, 0x15F, 0xF, 0xF, false); }
+__device__ __forceinline__ float row_bcast15_f(float v) {
+  return __builtin_bit_cast(float, row_bcast15_i(__builtin_bit_cast(int, v)));
+}
+__device__ __forceinline__ float row_scan16_q(float x) {
+  x = dpp_mov<0x111, 0xf, true>(x) + x;
+  x = dpp_mov<0x112, 0xf, true>(x) + x;
+  x = dpp_mov<0x114, 0xf, true>(x) + x;
+  x = dpp_mov<0x118, 0xf, true>(x) + x;
+  return x;
+}
+__device__ __forceinline__ int row_scan16_i(int x) {
+  x += __builtin_amdgcn_update_dpp(0, x, 0x111, 0xf, 0xf, true);
+  x += __builtin_amdgcn_update_dpp(0, x, 0x112, 0xf, 0xf, true);
+  x += __builtin_amdgcn_update_dpp(0, x, 0x114, 0xf, 0xf, true);
+  x += __builtin_amdgcn_update_dpp(0, x, 0x118, 0xf, 0xf, true);
+  return x;
+}
+// lane (row base + i) of v, i per lane (ds_bpermute)
+__device__ __forceinline__ int row_get_i(int v, int rowbase, int i) {
+  return __builtin_amdgcn_ds_bpermute((rowbase + i) << 2, v);
+}
+__device__ __forceinline__ float row_get_f(float v, int rowbase, int i) {
+  return __builtin_bit_cast(float, row_get_i(__builtin_bit_cast(int, v), rowbase, i));
+}
+
+template <int CH, int P, bool FROZEN>
+__global__ __launch_bounds__(256) void k_sample_quarter(SampleParams p) {
+  extern __shared__ __attribute__((aligned(16))) int32_t smem[];
+  constexpr int KQ = 16 * CH;                        // topics a quarter covers
+  constexpr int KP = KQ < 64 ? 64 : KQ;              // row stride of nw / nw16
+  constexpr int HD = (CH + 1) / 2;                   // dwords of a 16-bit row per lane
+  const int lane = threadIdx.x & 63;
+  const int wid = threadIdx.x >> 6;
+  const int ql = lane & 15;
+  const int rb = lane & 48;                          // the row's first lane
+  float* t_alpha = reinterpret_cast<float*>(smem);   // [KP] per block
+  int32_t* bsum = smem + KP;                         // [KP] per-block nwsum delta
+  float* t_invm1 = reinterpret_cast<float*>(smem + 2 * KP);
+  // per wave and quarter: live doc counts nd[KQ] and a = float(nd) + alpha [KQ]
+  int32_t* nd_l = smem + 3 * KP + wid * 8 * KQ + (lane >> 4) * 2 * KQ;
+  float* av_l = reinterpret_cast<float*>(nd_l + KQ);
+
+  for (int i = threadIdx.x; i < KP; i += 256) {
+    t_alpha[i] = p.alpha[i];
+    bsum[i] = 0;
+    t_invm1[i] = FROZEN ? 0.0f : p.inv_m1[i];
+  }
+  for (int i = threadIdx.x; i < 32 * KQ; i += 256) smem[3 * KP + i] = 0;
+  __syncthreads();
+
+  float inv_r[CH];
+#pragma unroll
+  for (int j = 0; j < CH; ++j) inv_r[j] = p.inv[ql * CH + j];
+  const float beta = p.beta;
+  const int last_lane = (p.K - 1) / CH;
+  const int last_j_tail = (p.K - 1) % CH;
+  const uint16_t* __restrict__ nw16 = p.nw16;
+  const uint8_t* __restrict__ wide_of = p.wide;
+  const int32_t* __restrict__ nw = p.nw;
+  constexpr int kWordMask = 0x7FFFFFFF;
+
+  // per-quarter state, uniform inside each row
+  int64_t t0 = 0, doc = 0;
+  int nt = 0, t = 0, cbase = 0, doc_end = 0, ev = 0, kp = 0, inc = 0;
+  int active = 1, loaded = 0;
+  // chunk registers: row-lane i <-> token cbase + i of the quarter's range
+  int cw = 0, cz = 0, cn = 0, w1 = 0, z1 = 0, w2 = 0, z2 = 0, pw = 0;
+  float cu = 0.0f;
+  uint32_t rows[P][HD];
+#pragma unroll
+  for (int s = 0; s < P; ++s)
+#pragma unroll
+    for (int q = 0; q < HD; ++q) rows[s][q] = 0u;
+
+  auto shift_words = [&]() {        // word of token cbase + i + P (across chunks)
+    const int src = ql + P;
+    const int va = row_get_i(cw, rb, src & 15), vb = row_get_i(w1, rb, src & 15);
+    pw = src < 16 ? va : vb;
+  };
+
+  while (true) {
+#pragma unroll
+    for (int s = 0; s < P; ++s) {
+      // ---- events of the quarters that reached one (lanes of those rows)
+      if (__ballot(active && t == ev) != 0) {
+        if (active && t == ev) {
+          if (t == nt) {
+            // the range is done (or none loaded yet): publish, clear, next range
+            if (loaded) {
+              if (ql < nt - cbase) p.z[t0 + cbase + ql] = cn;
+              if (!FROZEN && cn != cz) {
+                const uint32_t row = (uint32_t)(cw & kWordMask) * (uint32_t)KP;
+                atomicAdd(p.delta + (row + (uint32_t)cz), -1);
+                atomicAdd(p.delta + (row + (uint32_t)cn), 1);
+                atomicAdd(&bsum[cz], -1);
+                atomicAdd(&bsum[cn], 1);
+              }
+#pragma unroll
+              for (int j = 0; j < CH; ++j) nd_l[ql * CH + j] = 0;
+            }
+            loaded = 0;
+            while (true) {
+              int r = 0;
+              if (ql == 0) r = atomicAdd(p.queue, 1);
+              r = row_get_i(r, rb, 0);
+              if (r >= p.num_ranges) {
+                active = 0;
+                ev = -1;
+                t = 0;
+                cbase = 0;
+                nt = 0;
+                inc = 0;
+                kp = 0;
+                cw = 0;
+                cz = 0;
+                cn = 0;
+                pw = 0;
+                break;
+              }
+              const int64_t d0 = p.range_doc[r], d1 = p.range_doc[r + 1];
+              const int64_t s0 = p.doc_off[d0];
+              const int n = (int)(p.doc_off[d1] - s0);
+              if (n <= 0) continue;
+              t0 = s0;
+              nt = n;
+              t = 0;
+              cbase = 0;
+              loaded = 1;
+              const int32_t* wrd = p.words + s0;
+              const int32_t* zr = p.z + s0;
+              cw = ql < n ? wrd[ql] : 0;
+              cz = ql < n ? zr[ql] : 0;
+              w1 = 16 + ql < n ? wrd[16 + ql] : 0;
+              z1 = 16 + ql < n ? zr[16 + ql] : 0;
+              w2 = 32 + ql < n ? wrd[32 + ql] : 0;
+              z2 = 32 + ql < n ? zr[32 + ql] : 0;
+              cw |= (int)wide_of[cw] << 31;
+              w1 |= (int)wide_of[w1] << 31;
+              cn = cz;
+              cu = u01(draw_u32((uint64_t)(p.token_base + s0 + ql), p.c2, p.c3, p.k0, p.k1));
+              int64_t dd = d0;
+              while (p.doc_off[dd + 1] <= s0) ++dd;
+              doc = dd;
+              doc_end = (int)(p.doc_off[dd + 1] - s0);
+              break;
+            }
+            if (active) {
+              shift_words();
+              const int32_t* zr = p.z + t0;
+              for (int i = ql; i < doc_end; i += 16) atomicAdd(&nd_l[zr[i]], 1);
+              wave_lds_fence();
+#pragma unroll
+              for (int j = 0; j < CH; ++j) av_l[ql * CH + j] = (float)nd_l[ql * CH + j] + t_alpha[ql * CH + j];
+              inc = 0;
+              ev = min(16, doc_end);
+              // rows of the range's first P tokens into slots s, s+1, ...
+#pragma unroll
+              for (int j = 0; j < P; ++j) {
+                const int wp = row_get_i(cw, rb, j) & kWordMask;
+                load_row16_q<CH>(rows[(s + j) % P], nw16 + (int64_t)wp * KP + ql * CH);
+              }
+            }
+          } else {
+            if (t - cbase == 16) {
+              // chunk switch: publish the finished chunk, shift
+              p.z[t0 + cbase + ql] = cn;
+              if (!FROZEN && cn != cz) {
+                const uint32_t row = (uint32_t)(cw & kWordMask) * (uint32_t)KP;
+                atomicAdd(p.delta + (row + (uint32_t)cz), -1);
+                atomicAdd(p.delta + (row + (uint32_t)cn), 1);
+                atomicAdd(&bsum[cz], -1);
+                atomicAdd(&bsum[cn], 1);
+              }
+              cbase += 16;
+              cw = w1;
+              cz = z1;
+              w1 = w2;
+              z1 = z2;
+              w1 |= (int)wide_of[w1] << 31;
+              cn = cz;
+              cu = u01(draw_u32((uint64_t)(p.token_base + t0 + cbase + ql), p.c2, p.c3, p.k0, p.k1));
+              if (cbase + 32 + ql < nt) {
+                w2 = p.words[t0 + cbase + 32 + ql];
+                z2 = p.z[t0 + cbase + 32 + ql];
+              }
+              shift_words();
+            }
+            if (t == doc_end) {
+              inc = 0;               // the pending add-back belonged to the last document
+#pragma unroll
+              for (int j = 0; j < CH; ++j) nd_l[ql * CH + j] = 0;
+              wave_lds_fence();
+              int64_t dd = doc + 1;
+              while (p.doc_off[dd + 1] - t0 <= t) ++dd;
+              doc = dd;
+              doc_end = (int)(p.doc_off[dd + 1] - t0);
+              const int32_t* zr = p.z + t0;
+              for (int i = t + ql; i < doc_end; i += 16) atomicAdd(&nd_l[zr[i]], 1);
+              wave_lds_fence();
+#pragma unroll
+              for (int j = 0; j < CH; ++j) av_l[ql * CH + j] = (float)nd_l[ql * CH + j] + t_alpha[ql * CH + j];
+            }
+            ev = min(cbase + 16, doc_end);
+          }
+        }
+        wave_lds_fence();
+      }
+      if (__ballot(active) == 0) goto done;
+
+      // ---- one token of every quarter
+      const int idx = t - cbase;
+      const int wf = row_get_i(cw, rb, idx);
+      const int zo = row_get_i(cz, rb, idx);
+      const float u = row_get_f(cu, rb, idx);
+      if (ql == 0 && active) {
+        const int ndk = nd_l[kp] + inc;
+        nd_l[kp] = ndk;
+        av_l[kp] = (float)ndk + t_alpha[kp];
+        const int ndz = nd_l[zo] - 1;
+        nd_l[zo] = ndz;
+        av_l[zo] = (float)ndz + t_alpha[zo];
+      }
+      wave_lds_fence();
+      float a[CH];
+      load_lds_f<CH>(a, av_l + ql * CH);
+      const float cinv = FROZEN ? 0.0f : t_invm1[zo];
+
+      int32_t cfull[CH];
+      if (__ballot(wf < 0) != 0) {
+        // a word with a count > 65535 in some quarter: its int32 row (rare)
+        const bool wide = wf < 0;
+#pragma unroll
+        for (int j = 0; j < CH; ++j) {
+          const int c16 = CH == 1 ? (int)rows[s][0] : ((j & 1) ? (int)(rows[s][j >> 1] >> 16) : (int)(rows[s][j >> 1] & 0xFFFFu));
+          cfull[j] = wide ? nw[(int64_t)(wf & kWordMask) * KP + ql * CH + j] : c16;
+        }
+        __builtin_amdgcn_s_waitcnt(kVmcnt0);
+      } else {
+        if constexpr (CH == 1) {
+          cfull[0] = (int32_t)rows[s][0];
+        } else {
+#pragma unroll
+          for (int j = 0; j < CH; ++j)
+            cfull[j] = (j & 1) ? (int32_t)(rows[s][j >> 1] >> 16) : (int32_t)(rows[s][j >> 1] & 0xFFFFu);
+        }
+      }
+      bool own[CH];
+#pragma unroll
+      for (int j = 0; j < CH; ++j) own[j] = !FROZEN && (ql * CH + j == zo);
+      int32_t c_old = cfull[0];
+#pragma unroll
+      for (int j = 1; j < CH; ++j) c_old = own[j] ? cfull[j] : c_old;
+      const float bc = FROZEN ? 0.0f : ((float)(c_old - 1) + beta) * cinv;
+      float S[CH];
+      float acc = 0.0f;
+#pragma unroll
+      for (int j = 0; j < CH; ++j) {
+        const float bw = ((float)cfull[j] + beta) * inv_r[j];
+        const float b = own[j] ? bc : bw;
+        acc = __builtin_fmaf(a[j], b, acc);
+        S[j] = acc;
+      }
+      const float T = row_scan16_q(acc);
+      const float thr = u * row_bcast15_f(T);
+      // l* = #{row-lanes with T <= thr} (T is monotone), clamped to the last
+      const int cle = row_bcast15_i(row_scan16_i(T <= thr ? 1 : 0));
+      const int ls = min(cle, last_lane);
+      const float Eraw = row_get_f(T, rb, ls > 0 ? ls - 1 : 0);
+      const float E = ls > 0 ? Eraw : 0.0f;
+      int cl = 0;
+#pragma unroll
+      for (int j = 0; j < CH; ++j) cl += (E + S[j] <= thr) ? 1 : 0;
+      const int cnt = row_get_i(cl, rb, ls);
+      const int lim = ls < last_lane ? CH - 1 : last_j_tail;
+      const int kn = ls * CH + (cnt < lim ? cnt : lim);
+
+      cn = (active && ql == idx) ? kn : cn;
+      kp = kn;
+      inc = active;
+      t += active;
+
+      // keep the pipeline full: the row of each quarter's token t + P - 1 + 1
+      {
+        const int wp = row_get_i(pw, rb, (t - 1 - cbase) & 15) & kWordMask;
+        load_row16_q<CH>(rows[s], nw16 + (int64_t)wp * KP + ql * CH);
+      }
+    }
+  }
+done:
+  if (!FROZEN) {
+    __syncthreads();
+    for (int i = threadIdx.x; i < KP; i += 256) {
+      const int v = bsum[i];
+      if (v != 0) atomicAdd(&p.dsum[i], v);
+    }
+  }
+}
+
 // 16-bit copy of nw (+ per-word "wide" flag when a count exceeds 65535).
 template <int C>
 __global__ __launch_bounds__(256) void k_build_packed(const int32_t* __restrict__ nw, int64_t V,
@@ -2365,9 +2693,37 @@ static int occupancy_half_t() {
     return 1;
   return nb > 0 ? nb : 1;
 }
+int quarter_topics_per_lane(int K) { return K <= 16 ? 1 : (K <= 32 ? 2 : (K <= 64 ? 4 : 8)); }
+template <int CH>
+static constexpr size_t sample_quarter_lds() {
+  constexpr int KQ = 16 * CH, KP = KQ < 64 ? 64 : KQ;
+  return (3 * KP + 32 * KQ) * sizeof(int32_t);
+}
+template <int CH, bool FROZEN>
+static hipError_t launch_quarter_t(const SampleParams& p, int blocks, hipStream_t st) {
+  hipLaunchKernelGGL((k_sample_quarter<CH, SAMPLE_PQ, FROZEN>), dim3(blocks), dim3(256),
+                     sample_quarter_lds<CH>(), st, p);
+  return hipGetLastError();
+}
+template <int CH, bool FROZEN>
+static int occupancy_quarter_t() {
+  int nb = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_sample_quarter<CH, SAMPLE_PQ, FROZEN>, 256,
+                                                   sample_quarter_lds<CH>()) != hipSuccess)
+    return 1;
+  return nb > 0 ? nb : 1;
+}
 template <bool FROZEN>
-static hipError_t launch_sample_c(int C, const SampleParams& p, int blocks, hipStream_t st, bool half) {
-  if (half && C <= 2) {
+static hipError_t launch_sample_c(int C, const SampleParams& p, int blocks, hipStream_t st, int half) {
+  if (half == 2 && C <= 2) {
+    switch (quarter_topics_per_lane(p.K)) {
+      case 1: return launch_quarter_t<1, FROZEN>(p, blocks, st);
+      case 2: return launch_quarter_t<2, FROZEN>(p, blocks, st);
+      case 4: return launch_quarter_t<4, FROZEN>(p, blocks, st);
+      default: return launch_quarter_t<8, FROZEN>(p, blocks, st);
+    }
+  }
+  if (half == 1 && C <= 2) {
     switch (half_topics_per_lane(p.K)) {
       case 1: return launch_half_t<1, FROZEN>(p, blocks, st);
       case 2: return launch_half_t<2, FROZEN>(p, blocks, st);
@@ -2378,8 +2734,16 @@ static hipError_t launch_sample_c(int C, const SampleParams& p, int blocks, hipS
   return hipErrorInvalidValue;
 }
 template <bool FROZEN>
-static int occupancy_c(int C, int K, bool half) {
-  if (half && C <= 2) {
+static int occupancy_c(int C, int K, int half) {
+  if (half == 2 && C <= 2) {
+    switch (quarter_topics_per_lane(K)) {
+      case 1: return occupancy_quarter_t<1, FROZEN>();
+      case 2: return occupancy_quarter_t<2, FROZEN>();
+      case 4: return occupancy_quarter_t<4, FROZEN>();
+      default: return occupancy_quarter_t<8, FROZEN>();
+    }
+  }
+  if (half == 1 && C <= 2) {
     switch (half_topics_per_lane(K)) {
       case 1: return occupancy_half_t<1, FROZEN>();
       case 2: return occupancy_half_t<2, FROZEN>();
@@ -2391,11 +2755,11 @@ static int occupancy_c(int C, int K, bool half) {
 }
 
 hipError_t launch_sample(int C, bool frozen, const SampleParams& p, int blocks, hipStream_t st,
-                         bool half) {
+                         int half) {
   return frozen ? launch_sample_c<true>(C, p, blocks, st, half)
                 : launch_sample_c<false>(C, p, blocks, st, half);
 }
-int sample_blocks_per_cu(int C, bool frozen, int K, bool half) {
+int sample_blocks_per_cu(int C, bool frozen, int K, int half) {
   return frozen ? occupancy_c<true>(C, K, half) : occupancy_c<false>(C, K, half);
 }
 
@@ -2472,10 +2836,11 @@ int sample_sparse_blocks_per_cu(int C, bool frozen) {
   return frozen ? occupancy_sparse_c<true>(C) : occupancy_sparse_c<false>(C);
 }
 
-int sample_waves_per_block(int C, bool sparse, bool half) {
+int sample_waves_per_block(int C, bool sparse, int half) {
   if (sparse && C == 32) return sb_waves<32>();
   if (sparse && C == 64) return sb_waves<64>();
-  if (!sparse && half && C <= 2) return 8;   // two range workers per wave
+  if (!sparse && half == 1 && C <= 2) return 8;    // two range workers per wave
+  if (!sparse && half == 2 && C <= 2) return 16;   // four range workers per wave
   return 4;
 }
 

@@ -174,9 +174,11 @@ class ExactSampler:
     """cpu_exact: the bit-exact definition of the GPU sampler (one shard)."""
 
     def __init__(self, K, V, doc_off, words, alpha, beta, seed, z_init=None, token_base=0,
-                 kind="dense", half=False):
-        """half: the draw of the opt-in half-wave dense kernel (K <= 128,
-        LDA_DENSE_HALF=1 on the GPU side)."""
+                 kind="dense", half=None):
+        """half: which dense kernel's draw to follow for K <= 128 (the GPU's
+        LDA_DENSE_HALF): 0 = full-wave k_sample<C>, 1 = half-wave, 2 =
+        quarter-wave (the library's default); None = as the library would
+        choose under the current environment."""
         self.K, self.V = int(K), int(V)
         self.doc_off = np.ascontiguousarray(doc_off, dtype=np.int64)
         self.words = np.ascontiguousarray(words, dtype=np.int32)
@@ -192,7 +194,10 @@ class ExactSampler:
         self.Kp = int(lib().orc_exact_kpad(self._h))
         self._pending = True      # create leaves the shard's counts as the pending delta
         lib().orc_exact_set_kind(self._h, {"dense": 0, "dense32": 0, "sparse": 1}[kind])
-        lib().orc_exact_set_half(self._h, 1 if half else 0)
+        if half is None:
+            half = os.environ.get("LDA_DENSE_HALF", "2")[:1]
+            half = int(half) if half in ("0", "1", "2") else 2
+        lib().orc_exact_set_half(self._h, int(half))
 
     def __del__(self):
         h = getattr(self, "_h", None)

@@ -50,6 +50,11 @@ CASES = {
                                            max_len=500, seed=9), 4096, 0.01, 0.05, 19, (1, 4),
                      "sparse"),
 }
+# dense K <= 128 runs the quarter-wave kernel by default (LDA_DENSE_HALF
+# unset = 2, exact_draw_quarter); the cases above pin the full-wave
+# k_sample<C> draw (half = 0, LDA_DENSE_HALF=0), these the default one
+for _n in ("k4_tiny", "k20_changelists", "k128_ragged"):
+    CASES[_n + "_quarter"] = CASES[_n] + ("dense", 2)
 
 
 def sha(a):
@@ -59,11 +64,13 @@ def sha(a):
 def exact_case(name):
     build, K, alpha, beta, seed, checkpoints = CASES[name][:6]
     kind = CASES[name][6] if len(CASES[name]) > 6 else "dense"
+    half = CASES[name][7] if len(CASES[name]) > 7 else 0
     c = build()
-    o = O.ExactSampler(K, c.num_types, c.doc_off, c.words, alpha, beta, seed, kind=kind)
+    o = O.ExactSampler(K, c.num_types, c.doc_off, c.words, alpha, beta, seed, kind=kind, half=half)
     o.apply()
     out = {"doc_off": c.doc_off, "words": c.words, "K": K, "V": c.num_types, "alpha": alpha,
-           "beta": beta, "seed": seed, "checkpoints": np.array(checkpoints), "kind": kind}
+           "beta": beta, "seed": seed, "checkpoints": np.array(checkpoints), "kind": kind,
+           "half": half}
     out["z_0"] = o.z().astype(np.int16 if K < 32768 else np.int32)
     done = 0
     meta = {}

@@ -402,17 +402,19 @@ def test_inference_skips_types_without_training_tokens(oracle, kind):
     np.testing.assert_array_equal(tg[1], t_clean[0])
 
 
-@pytest.mark.parametrize("K", [3, 20, 48, 100, 128])
-def test_dense_half_wave_variant(oracle, K, monkeypatch):
-    """The opt-in half-wave dense kernel (two documents per wave, K <= 128;
-    LDA_DENSE_HALF=1) against its own oracle draw (exact_draw_half): ragged
+@pytest.mark.parametrize("variant", [1, 2])
+@pytest.mark.parametrize("K", [3, 12, 20, 48, 100, 128])
+def test_dense_half_wave_variant(oracle, K, variant, monkeypatch):
+    """The opt-in dense variants for K <= 128 -- two documents per wave
+    (LDA_DENSE_HALF=1, exact_draw_half) and four (=2, exact_draw_quarter) --
+    against their own oracle draws: ragged
     documents (empty, one token, 1500 tokens) over short work ranges, so the
     two halves switch ranges, chunks and documents at different steps and one
     half idles at the end; counts > 65535 (the int32-row path) at K = 3;
     inference (the frozen kernel)."""
     from ldagibbssampling_amd.sampler import GibbsSampler
     from ldagibbssampling_amd.corpus import Corpus
-    monkeypatch.setenv("LDA_DENSE_HALF", "1")
+    monkeypatch.setenv("LDA_DENSE_HALF", str(variant))     # 1 half-wave, 2 quarter-wave
     if K == 3:
         rng = np.random.default_rng(2)
         D, L = 8, 40000
@@ -424,7 +426,7 @@ def test_dense_half_wave_variant(oracle, K, monkeypatch):
     g = GibbsSampler(K, corpus.num_types, corpus.doc_off, corpus.words, alpha, 0.01, seed=77 + K,
                      tokens_per_range=100)
     o = oracle.ExactSampler(K, corpus.num_types, corpus.doc_off, corpus.words, alpha, 0.01, 77 + K,
-                            half=True)
+                            half=variant)
     for n in (1, 2):
         g.sweep(n)
         o.sweep(n)

@@ -54,9 +54,10 @@ def access_pattern(kernel):
     per lane in 256 B rounds for the large-K sparse sampler."""
     if kernel.startswith("k_sample_sparse_big"):
         return "k_round4"
-    if kernel.startswith("k_sample<8") or kernel.startswith("k_sample<16"):
+    if (kernel.startswith("k_sample<8") or kernel.startswith("k_sample<16")
+            or kernel.startswith("k_sample_quarter<8")):     # quarter, K <= 128: uint4 per lane
         return "k_row16"
-    if kernel.startswith("k_sample<2"):
+    if kernel.startswith("k_sample<2") or kernel.startswith("k_sample_quarter<2"):
         return "k_row4x2"
     return None
 
