@@ -1135,7 +1135,15 @@ __device__ __forceinline__ float row_get_f(float v, int rowbase, int i) {
 }
 
 template <int CH, int P, bool FROZEN>
-__global__ __launch_bounds__(256) void k_sample_quarter(SampleParams p) {
+// 5 waves per SIMD for the training kernel (96 VGPRs + 24 B/lane of spill
+// at CH = 8): +7% on C2 after burn-in, equal near
+// init, over the unconstrained 108 VGPRs / 4 waves; 6 waves spill 76 B and
+// lose 25% (profiles/r02/quarter/ab).  The frozen kernel fits 5 unforced.
+#ifndef QUARTER_WPE
+#define QUARTER_WPE 5
+#endif
+#define QUARTER_ATTR __attribute__((amdgpu_waves_per_eu(FROZEN ? 4 : QUARTER_WPE)))
+__global__ __launch_bounds__(256) QUARTER_ATTR void k_sample_quarter(SampleParams p) {
   extern __shared__ __attribute__((aligned(16))) int32_t smem[];
   constexpr int KQ = 16 * CH;                        // topics a quarter covers
   constexpr int KP = KQ < 64 ? 64 : KQ;              // row stride of nw / nw16
