@@ -1108,6 +1108,10 @@ __device__ __forceinline__ void load_row16_q(uint32_t (&r)[(CH + 1) / 2], const 
     r[0] = p[0];
   }
 }
+template <int CH>
+__device__ __forceinline__ uint32_t qrow_first16(const uint32_t (&r)[(CH + 1) / 2]) {
+  return r[0] & 0xFFFFu;
+}
 __device__ __forceinline__ int row_bcast15_i(int v) { return __builtin_amdgcn_update_dpp(0, v, 0x15F, 0xF, 0xF, false); }
 __device__ __forceinline__ float row_bcast15_f(float v) {
   return __builtin_bit_cast(float, row_bcast15_i(__builtin_bit_cast(int, v)));
@@ -1174,9 +1178,7 @@ __global__ __launch_bounds__(256) QUARTER_ATTR void k_sample_quarter(SampleParam
   const int last_lane = (p.K - 1) / CH;
   const int last_j_tail = (p.K - 1) % CH;
   const uint16_t* __restrict__ nw16 = p.nw16;
-  const uint8_t* __restrict__ wide_of = p.wide;
   const int32_t* __restrict__ nw = p.nw;
-  constexpr int kWordMask = 0x7FFFFFFF;
 
   // per-quarter state, uniform inside each row
   int64_t t0 = 0, doc = 0;
@@ -1208,7 +1210,7 @@ __global__ __launch_bounds__(256) QUARTER_ATTR void k_sample_quarter(SampleParam
             if (loaded) {
               if (ql < nt - cbase) p.z[t0 + cbase + ql] = cn;
               if (!FROZEN && cn != cz) {
-                const uint32_t row = (uint32_t)(cw & kWordMask) * (uint32_t)KP;
+                const uint32_t row = (uint32_t)cw * (uint32_t)KP;
                 atomicAdd(p.delta + (row + (uint32_t)cz), -1);
                 atomicAdd(p.delta + (row + (uint32_t)cn), 1);
                 atomicAdd(&bsum[cz], -1);
@@ -1253,8 +1255,6 @@ __global__ __launch_bounds__(256) QUARTER_ATTR void k_sample_quarter(SampleParam
               z1 = 16 + ql < n ? zr[16 + ql] : 0;
               w2 = 32 + ql < n ? wrd[32 + ql] : 0;
               z2 = 32 + ql < n ? zr[32 + ql] : 0;
-              cw |= (int)wide_of[cw] << 31;
-              w1 |= (int)wide_of[w1] << 31;
               cn = cz;
               cu = u01(draw_u32((uint64_t)(p.token_base + s0 + ql), p.c2, p.c3, p.k0, p.k1));
               int64_t dd = d0;
@@ -1275,7 +1275,7 @@ __global__ __launch_bounds__(256) QUARTER_ATTR void k_sample_quarter(SampleParam
               // rows of the range's first P tokens into slots s, s+1, ...
 #pragma unroll
               for (int j = 0; j < P; ++j) {
-                const int wp = row_get_i(cw, rb, j) & kWordMask;
+                const int wp = row_get_i(cw, rb, j);
                 load_row16_q<CH>(rows[(s + j) % P], nw16 + (int64_t)wp * KP + ql * CH);
               }
             }
@@ -1284,7 +1284,7 @@ __global__ __launch_bounds__(256) QUARTER_ATTR void k_sample_quarter(SampleParam
               // chunk switch: publish the finished chunk, shift
               p.z[t0 + cbase + ql] = cn;
               if (!FROZEN && cn != cz) {
-                const uint32_t row = (uint32_t)(cw & kWordMask) * (uint32_t)KP;
+                const uint32_t row = (uint32_t)cw * (uint32_t)KP;
                 atomicAdd(p.delta + (row + (uint32_t)cz), -1);
                 atomicAdd(p.delta + (row + (uint32_t)cn), 1);
                 atomicAdd(&bsum[cz], -1);
@@ -1295,7 +1295,6 @@ __global__ __launch_bounds__(256) QUARTER_ATTR void k_sample_quarter(SampleParam
               cz = z1;
               w1 = w2;
               z1 = z2;
-              w1 |= (int)wide_of[w1] << 31;
               cn = cz;
               cu = u01(draw_u32((uint64_t)(p.token_base + t0 + cbase + ql), p.c2, p.c3, p.k0, p.k1));
               if (cbase + 32 + ql < nt) {
@@ -1345,13 +1344,15 @@ __global__ __launch_bounds__(256) QUARTER_ATTR void k_sample_quarter(SampleParam
       const float cinv = FROZEN ? 0.0f : t_invm1[zo];
 
       int32_t cfull[CH];
-      if (__ballot(wf < 0) != 0) {
-        // a word with a count > 65535 in some quarter: its int32 row (rare)
-        const bool wide = wf < 0;
+      // the int32 row where this lane's first 16-bit count is 0xFFFF: a wide
+      // word's row is all 0xFFFF (k_apply_packed); a true count of 65535
+      // takes the int32 row too, which holds the same value
+      const bool wide = (qrow_first16<CH>(rows[s])) == 0xFFFFu;
+      if (__ballot(wide) != 0) {
 #pragma unroll
         for (int j = 0; j < CH; ++j) {
           const int c16 = CH == 1 ? (int)rows[s][0] : ((j & 1) ? (int)(rows[s][j >> 1] >> 16) : (int)(rows[s][j >> 1] & 0xFFFFu));
-          cfull[j] = wide ? nw[(int64_t)(wf & kWordMask) * KP + ql * CH + j] : c16;
+          cfull[j] = wide ? nw[(int64_t)wf * KP + ql * CH + j] : c16;
         }
         __builtin_amdgcn_s_waitcnt(kVmcnt0);
       } else {
@@ -1381,11 +1382,14 @@ __global__ __launch_bounds__(256) QUARTER_ATTR void k_sample_quarter(SampleParam
       }
       const float T = row_scan16_q(acc);
       const float thr = u * row_bcast15_f(T);
-      // l* = #{row-lanes with T <= thr} (T is monotone), clamped to the last
-      const int cle = row_bcast15_i(row_scan16_i(T <= thr ? 1 : 0));
+      // l* = #{row-lanes with T <= thr} (T is monotone), clamped to the last:
+      // the row's 16 bits of one ballot, counted per lane
+      const uint64_t le = __ballot(T <= thr);
+      const int cle = __builtin_popcount((uint32_t)(le >> rb) & 0xFFFFu);
       const int ls = min(cle, last_lane);
-      const float Eraw = row_get_f(T, rb, ls > 0 ? ls - 1 : 0);
-      const float E = ls > 0 ? Eraw : 0.0f;
+      // every lane's count against its left neighbour's T (0 on row-lane 0):
+      // lane l*'s is the draw's (E = T_{l*-1}), fetched once
+      const float E = dpp_mov<0x111, 0xf, true>(T);
       int cl = 0;
 #pragma unroll
       for (int j = 0; j < CH; ++j) cl += (E + S[j] <= thr) ? 1 : 0;
@@ -1400,7 +1404,7 @@ __global__ __launch_bounds__(256) QUARTER_ATTR void k_sample_quarter(SampleParam
 
       // keep the pipeline full: the row of each quarter's token t + P - 1 + 1
       {
-        const int wp = row_get_i(pw, rb, (t - 1 - cbase) & 15) & kWordMask;
+        const int wp = row_get_i(pw, rb, (t - 1 - cbase) & 15);
         load_row16_q<CH>(rows[s], nw16 + (int64_t)wp * KP + ql * CH);
       }
     }
@@ -1428,10 +1432,12 @@ __global__ __launch_bounds__(256) void k_build_packed(const int32_t* __restrict_
     bool big = false;
 #pragma unroll
     for (int j = 0; j < C; ++j) big |= (uint32_t)c[j] > 0xFFFFu;
+    // a wide word's whole 16-bit row is 0xFFFF: the quarter kernel reads its
+    // "take the int32 row" flag from the row itself (k_sample_quarter)
+    const uint64_t any = __ballot(big);
 #pragma unroll
     for (int j = 0; j < C; ++j)
-      nw16[w * KP + lane * C + j] = (uint16_t)((uint32_t)c[j] > 0xFFFFu ? 0xFFFFu : (uint32_t)c[j]);
-    const uint64_t any = __ballot(big);
+      nw16[w * KP + lane * C + j] = any ? (uint16_t)0xFFFFu : (uint16_t)c[j];
     if (lane == 0) wide[w] = any ? 1 : 0;
   }
 }
@@ -2395,10 +2401,12 @@ __global__ __launch_bounds__(256) void k_apply_packed(int32_t* __restrict__ nw, 
     bool big = false;
 #pragma unroll
     for (int j = 0; j < C; ++j) big |= (uint32_t)c[j] > 0xFFFFu;
+    // a wide word's whole 16-bit row is 0xFFFF: the quarter kernel reads its
+    // "take the int32 row" flag from the row itself (k_sample_quarter)
+    const uint64_t any = __ballot(big);
 #pragma unroll
     for (int j = 0; j < C; ++j)
-      nw16[w * KP + lane * C + j] = (uint16_t)((uint32_t)c[j] > 0xFFFFu ? 0xFFFFu : (uint32_t)c[j]);
-    const uint64_t any = __ballot(big);
+      nw16[w * KP + lane * C + j] = any ? (uint16_t)0xFFFFu : (uint16_t)c[j];
     if (lane == 0) wide[w] = any ? 1 : 0;
   }
 }
