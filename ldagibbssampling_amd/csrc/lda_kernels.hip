@@ -1330,13 +1330,12 @@ __global__ __launch_bounds__(256) QUARTER_ATTR void k_sample_quarter(SampleParam
       const int wf = row_get_i(cw, rb, idx);
       const int zo = row_get_i(cz, rb, idx);
       const float u = row_get_f(cu, rb, idx);
+      // the document factors a_k as running fp32 values (oracle
+      // exact_draw_quarter): +1 for the previous token's new topic, -1 for this
+      // token's old one, as LDS float atomics (in order, nothing to wait for)
       if (ql == 0 && active) {
-        const int ndk = nd_l[kp] + inc;
-        nd_l[kp] = ndk;
-        av_l[kp] = (float)ndk + t_alpha[kp];
-        const int ndz = nd_l[zo] - 1;
-        nd_l[zo] = ndz;
-        av_l[zo] = (float)ndz + t_alpha[zo];
+        atomicAdd(&av_l[kp], (float)inc);
+        atomicAdd(&av_l[zo], -1.0f);
       }
       wave_lds_fence();
       float a[CH];

@@ -477,10 +477,13 @@ static int exact_draw_half(const orc_exact* s, const int32_t* nwrow, const int32
  * 128.  The per-lane serial fma prefix is exact_draw's; T = the row's
  * inclusive scan (row_shr 1,2,4,8); thr = u * T_15; l* = min(#{l : T_l <=
  * thr}, last lane) (the first lane with T > thr: T is monotone); E, the count
- * and the clamp as exact_draw. */
+ * and the clamp as exact_draw.  The document factor a_k is the kernel's running
+ * fp32 value af[k] (exact_sample_docs): float(nd_k) + alpha_k when the
+ * document starts, then -1.0f when a token leaves topic k and +1.0f when one
+ * joins it, in token order (LDS float atomics on the GPU). */
 static int quarter_topics_per_lane(int K) { return K <= 16 ? 1 : (K <= 32 ? 2 : (K <= 64 ? 4 : 8)); }
 
-static int exact_draw_quarter(const orc_exact* s, const int32_t* nwrow, const int32_t* nd, int zo,
+static int exact_draw_quarter(const orc_exact* s, const int32_t* nwrow, const float* af, int zo,
                               float u, float* S) {
   const int K = s->K, CH = quarter_topics_per_lane(K);
   float t[16], y[16];
@@ -495,8 +498,7 @@ static int exact_draw_quarter(const orc_exact* s, const int32_t* nwrow, const in
         iv = s->inv_m1[k];
       }
       const float b = ((float)c + s->beta_f) * iv;
-      const float a = (float)nd[k] + s->alpha_f[k];
-      acc = fmaf(a, b, acc);
+      acc = fmaf(af[k], b, acc);
       S[k] = acc;
     }
     t[l] = acc;
@@ -642,25 +644,32 @@ static void exact_sample_docs(const orc_exact* s, const int64_t* doc_off, const 
   float* S = (float*)malloc(sizeof(float) * s->Kp);
   int32_t* et = (int32_t*)malloc(sizeof(int32_t) * s->Kp);
   int32_t* ec = (int32_t*)malloc(sizeof(int32_t) * s->Kp);
+  float* af = (float*)malloc(sizeof(float) * s->Kp);
+  const int quarter = s->kind == 0 && s->half == 2 && s->Kp <= 128;
   for (int64_t d = d0; d < d1; ++d) {
     memset(nd, 0, sizeof(int32_t) * s->Kp);
     for (int64_t i = doc_off[d]; i < doc_off[d + 1]; ++i) nd[z[i]]++;
+    /* the quarter-wave kernel's running document factors (exact_draw_quarter) */
+    for (int k = 0; k < s->Kp; ++k) af[k] = (float)nd[k] + s->alpha_f[k];
     for (int64_t i = doc_off[d]; i < doc_off[d + 1]; ++i) {
       int w = words[i];
       int zo = z[i];
       float u = orc_u01(orc_draw(s->seed, (uint64_t)(token_base + i), c2, c3));
       nd[zo]--;
+      af[zo] -= 1.0f;
       int kn = s->kind == 1
                    ? exact_draw_sparse(s, s->nw + (size_t)w * s->Kp, nd, frozen ? -1 : zo, u, S, et, ec)
-                   : (s->half == 2 && s->Kp <= 128)
-                         ? exact_draw_quarter(s, s->nw + (size_t)w * s->Kp, nd, frozen ? -1 : zo, u, S)
+                   : quarter
+                         ? exact_draw_quarter(s, s->nw + (size_t)w * s->Kp, af, frozen ? -1 : zo, u, S)
                    : (s->half == 1 && s->Kp <= 128)
                          ? exact_draw_half(s, s->nw + (size_t)w * s->Kp, nd, frozen ? -1 : zo, u, S)
                          : exact_draw(s, s->nw + (size_t)w * s->Kp, nd, frozen ? -1 : zo, u, S);
       nd[kn]++;
+      af[kn] += 1.0f;
       z[i] = kn;
     }
   }
+  free(af);
   free(nd);
   free(S);
   free(et);
