@@ -5,7 +5,7 @@
 # Everything under gpurun_out/final/; traffic files also into profiles/r02/.
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
-O=gpurun_out/final; mkdir -p $O profiles/r02
+O=gpurun_out/final2; mkdir -p $O profiles/r02
 export TMPDIR=/tmp
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread --durations=15 > $O/pytest_gpu.log 2>&1 || { echo "PYTEST FAILED"; tail -60 $O/pytest_gpu.log; exit 1; }
 echo "pytest: $(grep -E 'passed|failed' $O/pytest_gpu.log | tail -1)"
@@ -20,7 +20,7 @@ prof() {  # cfg kernel tokens K
   python3 -c "import json;t=json.load(open('$O/traffic_$cfg.json'));print('$cfg', round(t['bytes_per_token'],1),'B/tok', {k:round(v,1) for k,v in t.get('per_token',{}).items()}, 'clk', round(t.get('effective_clock_ghz',0),3))"
 }
 prof c4 "k_sample<8, 3, false>" 250000000 512 && \
-prof c2 "k_sample<2, 4, false>" 20000000 128 && \
+prof c2 "k_sample_quarter<8, 4, false>" 20000000 128 && \
 prof c3 "k_sample<16, 2, false>" 20000000 1024 && \
 prof c5 "k_sample_sparse_big<64, 3, false>" 250000000 4096 || exit 1
 for cfg in c4 c1 c2 c3 c5; do
