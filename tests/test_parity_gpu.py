@@ -405,8 +405,9 @@ def test_inference_skips_types_without_training_tokens(oracle, kind):
 @pytest.mark.parametrize("variant", [1, 2])
 @pytest.mark.parametrize("K", [3, 12, 20, 48, 100, 128])
 def test_dense_half_wave_variant(oracle, K, variant, monkeypatch):
-    """The opt-in dense variants for K <= 128 -- two documents per wave
-    (LDA_DENSE_HALF=1, exact_draw_half) and four (=2, exact_draw_quarter) --
+    """The dense variants for K <= 128 -- two documents per wave (opt-in,
+    LDA_DENSE_HALF=1, exact_draw_half) and four (=2, exact_draw_quarter, the
+    default) --
     against their own oracle draws: ragged
     documents (empty, one token, 1500 tokens) over short work ranges, so the
     two halves switch ranges, chunks and documents at different steps and one
