@@ -301,7 +301,9 @@ def main():
     torch.cuda.set_stream(stream)
     sampler.set_stream(stream.cuda_stream)
     # AD-LDA: sample; all-reduce (SUM) of every rank's int32 nw/nwsum delta; apply.
-    # With N > 1 the sweep is split so that the exchange overlaps sampling.
+    # --exchange-parts P > 1 splits the sweep so that part i's all-reduce
+    # overlaps part i+1's sampling; the default is one blocking collective per
+    # sweep (C4: 205 MB against a 35 ms sweep).
     if args.exchange_parts is None:
         args.exchange_parts = 1
     if args.exchange_parts > 1:
