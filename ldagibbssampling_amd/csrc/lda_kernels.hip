@@ -1147,12 +1147,6 @@ template <int CH, int P, bool FROZEN>
 #define QUARTER_WPE 5
 #endif
 #define QUARTER_ATTR __attribute__((amdgpu_waves_per_eu(FROZEN ? 4 : QUARTER_WPE)))
-// QUARTER_AREG = 1: each row-lane keeps the a values of its CH topics in
-// registers (same fp32 adds in the same order as the LDS atomics, so the
-// oracle's exact_draw_quarter is unchanged); 0: the LDS vector (A/B)
-#ifndef QUARTER_AREG
-#define QUARTER_AREG 0
-#endif
 __global__ __launch_bounds__(256) QUARTER_ATTR void k_sample_quarter(SampleParams p) {
   extern __shared__ __attribute__((aligned(16))) int32_t smem[];
   constexpr int KQ = 16 * CH;                        // topics a quarter covers
@@ -1198,17 +1192,6 @@ __global__ __launch_bounds__(256) QUARTER_ATTR void k_sample_quarter(SampleParam
   for (int s = 0; s < P; ++s)
 #pragma unroll
     for (int q = 0; q < HD; ++q) rows[s][q] = 0u;
-  float areg[CH];
-#pragma unroll
-  for (int j = 0; j < CH; ++j) areg[j] = 0.0f;
-  auto set_a = [&]() {              // a = float(nd) + alpha for the row's new document
-#pragma unroll
-    for (int j = 0; j < CH; ++j) {
-      const float v = (float)nd_l[ql * CH + j] + t_alpha[ql * CH + j];
-      if constexpr (QUARTER_AREG) areg[j] = v;
-      else av_l[ql * CH + j] = v;
-    }
-  };
 
   auto shift_words = [&]() {        // word of token cbase + i + P (across chunks)
     const int src = ql + P;
@@ -1285,7 +1268,8 @@ __global__ __launch_bounds__(256) QUARTER_ATTR void k_sample_quarter(SampleParam
               const int32_t* zr = p.z + t0;
               for (int i = ql; i < doc_end; i += 16) atomicAdd(&nd_l[zr[i]], 1);
               wave_lds_fence();
-              set_a();
+#pragma unroll
+              for (int j = 0; j < CH; ++j) av_l[ql * CH + j] = (float)nd_l[ql * CH + j] + t_alpha[ql * CH + j];
               inc = 0;
               ev = min(16, doc_end);
               // rows of the range's first P tokens into slots s, s+1, ...
@@ -1331,7 +1315,8 @@ __global__ __launch_bounds__(256) QUARTER_ATTR void k_sample_quarter(SampleParam
               const int32_t* zr = p.z + t0;
               for (int i = t + ql; i < doc_end; i += 16) atomicAdd(&nd_l[zr[i]], 1);
               wave_lds_fence();
-              set_a();
+#pragma unroll
+              for (int j = 0; j < CH; ++j) av_l[ql * CH + j] = (float)nd_l[ql * CH + j] + t_alpha[ql * CH + j];
             }
             ev = min(cbase + 16, doc_end);
           }
@@ -1348,26 +1333,13 @@ __global__ __launch_bounds__(256) QUARTER_ATTR void k_sample_quarter(SampleParam
       // the document factors a_k as running fp32 values (oracle
       // exact_draw_quarter): +1 for the previous token's new topic, -1 for this
       // token's old one, as LDS float atomics (in order, nothing to wait for)
-      float a[CH];
-      if constexpr (QUARTER_AREG) {
-        // the lane owning kp / zo adds (float)inc / -1 to it (+0.0f elsewhere)
-        const int lk = active ? kp - ql * CH : -1, lo = active ? zo - ql * CH : -1;
-        const float finc = (float)inc;
-#pragma unroll
-        for (int j = 0; j < CH; ++j) areg[j] += (lk == j) ? finc : 0.0f;
-#pragma unroll
-        for (int j = 0; j < CH; ++j) {
-          areg[j] += (lo == j) ? -1.0f : 0.0f;
-          a[j] = areg[j];
-        }
-      } else {
-        if (ql == 0 && active) {
-          atomicAdd(&av_l[kp], (float)inc);
-          atomicAdd(&av_l[zo], -1.0f);
-        }
-        wave_lds_fence();
-        load_lds_f<CH>(a, av_l + ql * CH);
+      if (ql == 0 && active) {
+        atomicAdd(&av_l[kp], (float)inc);
+        atomicAdd(&av_l[zo], -1.0f);
       }
+      wave_lds_fence();
+      float a[CH];
+      load_lds_f<CH>(a, av_l + ql * CH);
       const float cinv = FROZEN ? 0.0f : t_invm1[zo];
 
       int32_t cfull[CH];
