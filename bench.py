@@ -338,6 +338,9 @@ def main():
     assert len(ks) == min(args.steps * parts, 256)
     # a split sweep is `parts` launches: the sampler's time per sweep is their sum
     kern_ms = float(np.mean(ks)) * parts
+    # the dense samplers' recount kernel after each launch (0 in the delta mode)
+    rc = sampler.recount_times(args.steps * parts)
+    recount_ms = float(np.mean(rc)) * parts if sampler.recount else None
     copy_gbs = stream_copy_gbs(device) if rank == 0 else None
 
     t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{device}")
@@ -427,6 +430,10 @@ def main():
                 "bytes_per_token": enc,
                 "bytes_model": enc_model,
                 "kernel_ms_timed_region": kern_ms,
+                "count_update": ("recount (the sampler writes z; k_recount rebuilds the shard's "
+                                 "rows from a word-sorted token index)" if sampler.recount else
+                                 "delta (device atomics per changed token)"),
+                "recount_ms_timed_region": recount_ms,
                 "measured_copy_gbs": copy_gbs,
                 # the bandwidth the kernel really moves (PMC bytes / its time)
                 "traffic_gbs": (traffic_gb / (kern_ms * 1e-3)) if traffic_gb else None,

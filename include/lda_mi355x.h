@@ -46,6 +46,7 @@ typedef int32_t lda_status;
 #define LDA_ERR_OUT_OF_MEMORY (-3)
 #define LDA_ERR_STATE (-4)        /* call out of order (e.g. sample with a pending delta) */
 #define LDA_ERR_UNSUPPORTED (-5)  /* e.g. K above the compiled maximum */
+#define LDA_ERR_INTERNAL (-6)     /* an unexpected C++ exception, caught at the ABI */
 
 #define LDA_MAX_TOPICS 4096       /* K <= 4096 (LDA_SAMPLER_SPARSE above 1024)       */
 #define LDA_MAX_TOPICS_DENSE 1024 /* the dense sampler's register-resident rows      */
@@ -94,14 +95,24 @@ void lda_destroy(lda_ctx* ctx);
  * setNumIterations(n) and optimizeInterval 0 [src/cmu_ron/TrainAndPredict.java:165-166]. */
 lda_status lda_sweep(lda_ctx* ctx, int32_t n);
 
-/* One sampling pass over the shard against the current nw/nwsum snapshot;
- * changes go to the delta buffer (one sweep of WorkerRunnable.run()). */
+/* One sampling pass over the shard against the current nw/nwsum snapshot
+ * (one sweep of WorkerRunnable.run()); its result goes to the exchange
+ * buffer below. */
 lda_status lda_sample(lda_ctx* ctx);
-/* Device pointer to the pending delta: int32[V*Kp + Kp] (nw delta row-major
- * with padded row length Kp = lda_padded_topics(), then nwsum delta).  Sum it
- * across ranks in place (the sumTypeTopicCounts analogue) before lda_apply. */
+/* Device pointer to the pending exchange buffer: int32[V*Kp + Kp] (an nw part
+ * row-major with padded row length Kp = lda_padded_topics(), then an nwsum
+ * part).  Sum it across ranks in place (the sumTypeTopicCounts analogue)
+ * before lda_apply.  What it holds depends on the count-update mode
+ * (lda_count_update_mode): the dense samplers RECOUNT -- the sampler writes
+ * only z and the buffer receives this shard's own (word, topic) counts, which
+ * lda_apply's sum replaces nw / nwsum with -- the sparse samplers keep a
+ * DELTA of the shard's changes, which lda_apply adds.  Either way the caller
+ * only sums it, and lda_apply leaves it zero. */
 lda_status lda_delta_buffer(lda_ctx* ctx, void** dev_ptr, size_t* count);
-/* nw += delta, nwsum += delta, delta = 0, refresh the per-topic tables. */
+/* recount = 1 when the buffer holds counts, 0 when it holds a delta. */
+lda_status lda_count_update_mode(lda_ctx* ctx, int32_t* recount);
+/* nw/nwsum := buffer (recount) or += buffer (delta), buffer = 0, refresh the
+ * per-topic tables. */
 lda_status lda_apply(lda_ctx* ctx);
 
 /* Split sweep: the exchange overlapped with sampling.
@@ -225,6 +236,9 @@ lda_status lda_last_sample_ms(lda_ctx* ctx, float* ms);
 /* Kernel durations (ms, oldest first) of the last n = min(max, launches, 256)
  * lda_sample calls: bench.py reads the launches of its timed region. */
 lda_status lda_sample_times(lda_ctx* ctx, int32_t max, float* ms, int32_t* n);
+/* The same for the recount kernel that follows each sampler launch in the
+ * recount mode (0 ms in the delta mode). */
+lda_status lda_recount_times(lda_ctx* ctx, int32_t max, float* ms, int32_t* n);
 
 /* Diagnostics: the sampler's own uniform draws on the current device.
  * out[i] = word 0 of Philox4x32-10 with counter {gtok[i] lo, gtok[i] hi, c2,
@@ -235,7 +249,18 @@ lda_status lda_philox_draws(uint64_t seed, uint32_t c2, uint32_t c3, const int64
                             uint32_t* out);
 
 const char* lda_last_error(void);
+/* Test hook: the nth host allocation of a caller-sized buffer on this thread
+ * (counted from this call; 0 = off) fails with std::bad_alloc, which the
+ * entry point reports as LDA_ERR_OUT_OF_MEMORY (tests/test_abi_guard*.py). */
+void lda_debug_fail_host_alloc(int32_t nth);
+/* "lda_mi355x <version> (gfx950; ABI <n>)".  ABI history: 2 -- lda_infer's
+ * last three ints became (num_iterations, thinning, burn_in), Mallet's
+ * getSampledDistribution order (was (n_iter, burn_in, thin)); 3 -- the dense
+ * samplers' exchange buffer holds recounted counts (lda_count_update_mode),
+ * lda_recount_times, lda_set_exchange_parts' reserve_cus < 0 = default. */
+#define LDA_ABI_VERSION 3
 const char* lda_version(void);
+int32_t lda_abi_version(void);
 
 #ifdef __cplusplus
 }

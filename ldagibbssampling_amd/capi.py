@@ -22,6 +22,7 @@ STATUS_NAMES = {
     -3: "LDA_ERR_OUT_OF_MEMORY",
     -4: "LDA_ERR_STATE",
     -5: "LDA_ERR_UNSUPPORTED",
+    -6: "LDA_ERR_INTERNAL",
 }
 MAX_TOPICS = 4096
 MAX_TOPICS_DENSE = 1024
@@ -98,6 +99,10 @@ SIGNATURES = {
     "lda_row_stats": (C.c_int32, [_vp, C.POINTER(C.c_double)]),
     "lda_sample_times": (C.c_int32, [_vp, C.c_int32, _vp, C.POINTER(C.c_int32)]),
     "lda_philox_draws": (C.c_int32, [C.c_uint64, C.c_uint32, C.c_uint32, _vp, C.c_int64, _vp]),
+    "lda_recount_times": (C.c_int32, [_vp, C.c_int32, _vp, C.POINTER(C.c_int32)]),
+    "lda_count_update_mode": (C.c_int32, [_vp, C.POINTER(C.c_int32)]),
+    "lda_abi_version": (C.c_int32, []),
+    "lda_debug_fail_host_alloc": (None, [C.c_int32]),
     "lda_last_error": (C.c_char_p, []),
     "lda_version": (C.c_char_p, []),
 }

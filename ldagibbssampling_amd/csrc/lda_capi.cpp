@@ -21,11 +21,13 @@
 #include <vector>
 
 #include "../../include/lda_mi355x.h"
+#include "lda_guard.h"
 #include "lda_kernels.h"
 
 namespace {
 
 thread_local std::string g_last_error;
+thread_local int32_t g_fail_alloc = 0;   // lda_debug_fail_host_alloc countdown (0 = off)
 
 lda_status fail(lda_status code, const std::string& msg) {
   g_last_error = msg;
@@ -123,6 +125,14 @@ hipError_t dalloc(T** p, size_t n) {
 
 }  // namespace
 
+namespace lda_abi {
+void set_error(const std::string& msg) { g_last_error = msg; }
+void check_host_alloc() {
+  if (g_fail_alloc > 0 && --g_fail_alloc == 0) throw std::bad_alloc();
+}
+}  // namespace lda_abi
+using lda_abi::host_vector;
+
 struct lda_ctx {
   int device = 0;
   hipStream_t own_stream = nullptr;
@@ -158,6 +168,15 @@ struct lda_ctx {
   uint8_t* wide = nullptr;
   int64_t tokens_per_range = 0;
   std::vector<int64_t> doc_off_h;
+  std::vector<int64_t> ranges_h;   // host copy of range_doc
+  // dense samplers' recount: the sampler writes only z, then
+  // every word row of the shard is recounted from a word-sorted token index
+  // into the exchange buffer, which then holds counts, not changes
+  bool recount = false;
+  uint32_t* perm = nullptr;        // [N] token indices grouped by (part, word)
+  int32_t* items = nullptr;        // int4 {word, first perm index, tokens, split} per work item
+  std::vector<int64_t> part_item{0, 0};
+  int recount_blocks = 0;
 
   int32_t* words = nullptr;
   int32_t* z = nullptr;
@@ -181,7 +200,7 @@ struct lda_ctx {
   int partial_blocks = 1024;
   // event pairs around the last LDA_TIME_RING sampler launches (lda_sample_times)
   static constexpr int LDA_TIME_RING = 256;
-  hipEvent_t ev0[LDA_TIME_RING] = {}, ev1[LDA_TIME_RING] = {};
+  hipEvent_t ev0[LDA_TIME_RING] = {}, ev1[LDA_TIME_RING] = {}, ev2[LDA_TIME_RING] = {};
   int64_t launches = 0;
 
   ~lda_ctx() {
@@ -190,13 +209,15 @@ struct lda_ctx {
                     (void*)nw, (void*)nwsum, (void*)delta, (void*)alpha_d, (void*)alpha_f,
                     (void*)inv, (void*)inv_m1, (void*)partial, (void*)nonzero, (void*)ent,
                     (void*)row_off, (void*)row_nnz, (void*)nw16, (void*)wide, (void*)inf_words,
-                    (void*)inf_z, (void*)inf_acc, (void*)inf_q, (void*)inf_doff, (void*)inf_range})
+                    (void*)inf_z, (void*)inf_acc, (void*)inf_q, (void*)inf_doff, (void*)inf_range,
+                    (void*)perm, (void*)items})
       if (p) (void)hipFree(p);
     for (int i = 1; i < LDA_MAX_EXCHANGE_PARTS; ++i)
       if (delta_part[i]) (void)hipFree(delta_part[i]);
     for (int i = 0; i < LDA_TIME_RING; ++i) {
       if (ev0[i]) (void)hipEventDestroy(ev0[i]);
       if (ev1[i]) (void)hipEventDestroy(ev1[i]);
+      if (ev2[i]) (void)hipEventDestroy(ev2[i]);
     }
     if (own_stream) (void)hipStreamDestroy(own_stream);
   }
@@ -257,6 +278,69 @@ static lda_status build_row_capacity(lda_ctx* c) {
   return LDA_OK;
 }
 
+// The recount's word-sorted token index for the current exchange parts:
+// tokens per (part, word) on the GPU, offsets and work items on the host
+// (words of more than RECOUNT_ITEM_TOKENS tokens in a part are split; each
+// part's items longest first, so the work queue ends on short ones), then
+// the scatter of token indices.  Words never change, so this runs at create
+// and when the parts change.
+static lda_status build_recount_index(lda_ctx* c) {
+  if (c->perm) (void)hipFree(c->perm);
+  if (c->items) (void)hipFree(c->items);
+  c->perm = nullptr;
+  c->items = nullptr;
+  c->part_item.assign((size_t)c->parts + 1, 0);
+  if (!c->recount || c->N == 0) return LDA_OK;
+  lda::PartSpans ps{};
+  ps.parts = c->parts;
+  for (int i = 0; i <= c->parts; ++i)
+    ps.tok[i] = c->doc_off_h[(size_t)c->ranges_h[(size_t)c->part_range[(size_t)i]]];
+  const size_t cells = (size_t)c->parts * (size_t)c->V;
+  uint32_t* cnt = nullptr;
+  HIP_TRY(dalloc(&cnt, cells));
+  std::vector<uint32_t> h(cells);
+  hipError_t e = hipMemsetAsync(cnt, 0, sizeof(uint32_t) * cells, c->stream);
+  if (e == hipSuccess) e = lda::launch_word_hist(c->words, c->N, ps, c->V, cnt, c->stream);
+  if (e == hipSuccess) e = hipMemcpyAsync(h.data(), cnt, sizeof(uint32_t) * cells, hipMemcpyDeviceToHost, c->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+  if (e != hipSuccess) {
+    (void)hipFree(cnt);
+    HIP_TRY(e);
+  }
+  std::vector<int32_t> it;
+  uint32_t off = 0;
+  const uint32_t S = (uint32_t)lda::RECOUNT_ITEM_TOKENS;
+  for (int pt = 0; pt < c->parts; ++pt) {
+    const size_t first = it.size() / 4;
+    for (int32_t w = 0; w < c->V; ++w) {
+      const uint32_t n = h[(size_t)pt * c->V + w];
+      h[(size_t)pt * c->V + w] = off;   // becomes the scatter cursor
+      for (uint32_t b = 0; b < n; b += S)
+        it.insert(it.end(), {w, (int32_t)(off + b), (int32_t)std::min(S, n - b), n > S ? 1 : 0});
+      off += n;
+    }
+    // longest items first within the part (stable: ties keep word order)
+    std::vector<size_t> order(it.size() / 4 - first);
+    for (size_t j = 0; j < order.size(); ++j) order[j] = first + j;
+    std::stable_sort(order.begin(), order.end(), [&](size_t a, size_t b) { return it[4 * a + 2] > it[4 * b + 2]; });
+    std::vector<int32_t> sorted;
+    sorted.reserve(order.size() * 4);
+    for (size_t j : order) sorted.insert(sorted.end(), it.begin() + 4 * j, it.begin() + 4 * j + 4);
+    std::copy(sorted.begin(), sorted.end(), it.begin() + 4 * first);
+    c->part_item[(size_t)pt + 1] = (int64_t)(it.size() / 4);
+  }
+  e = dalloc(&c->perm, (size_t)c->N);
+  if (e == hipSuccess) e = dalloc(&c->items, std::max<size_t>(it.size(), 4));
+  if (e == hipSuccess) e = hipMemcpyAsync(cnt, h.data(), sizeof(uint32_t) * cells, hipMemcpyHostToDevice, c->stream);
+  if (e == hipSuccess) e = lda::launch_word_scatter(c->words, c->N, ps, c->V, cnt, c->perm, c->stream);
+  if (e == hipSuccess && !it.empty())
+    e = hipMemcpyAsync(c->items, it.data(), sizeof(int32_t) * it.size(), hipMemcpyHostToDevice, c->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+  (void)hipFree(cnt);
+  HIP_TRY(e);
+  return LDA_OK;
+}
+
 static lda_status apply_impl(lda_ctx* c) {
   if (c->next_part != 0)
     return fail(LDA_ERR_STATE, "lda_apply inside a split sweep: sample every part first");
@@ -269,7 +353,7 @@ static lda_status apply_impl(lda_ctx* c) {
   if (c->sampler == LDA_SAMPLER_DENSE) {
     // one launch: apply, 16-bit rows, topic tables, queue reset (k_apply_packed)
     lda::TopicTables t{c->nwsum, c->alpha_d, c->alpha_f, c->inv, c->inv_m1,
-                       (float)((double)c->V * c->beta), c->K, c->queue};
+                       (float)((double)c->V * c->beta), c->K, c->queue, c->recount ? 1 : 0};
     HIP_TRY(lda::launch_apply_packed(c->nw, c->delta, c->V, c->Kp, c->nw16, c->wide, t, c->stream));
     c->pending = false;
     return LDA_OK;
@@ -307,11 +391,14 @@ static lda_status recount_impl(lda_ctx* c) {
 extern "C" {
 
 const char* lda_last_error(void) { return g_last_error.c_str(); }
-const char* lda_version(void) { return "lda_mi355x 0.1.0 (gfx950)"; }
+void lda_debug_fail_host_alloc(int32_t nth) { g_fail_alloc = nth > 0 ? nth : 0; }
+const char* lda_version(void) { return "lda_mi355x 0.3.0 (gfx950; ABI 3)"; }
+int32_t lda_abi_version(void) { return LDA_ABI_VERSION; }
 int32_t lda_padded_topics(int32_t num_topics) { return pad_topics(num_topics); }
 
 lda_status lda_create(lda_ctx** out, const lda_config* cfg, const int64_t* doc_off,
                       const int32_t* words, const int32_t* z_init) {
+  return lda_abi::guarded([&]() -> lda_status {
   if (!out || !cfg || !doc_off) return fail(LDA_ERR_INVALID_ARG, "null argument");
   *out = nullptr;
   if (cfg->num_topics < 1) return fail(LDA_ERR_INVALID_ARG, "num_topics must be >= 1");
@@ -333,7 +420,7 @@ lda_status lda_create(lda_ctx** out, const lda_config* cfg, const int64_t* doc_o
   for (int k = 0; k < cfg->num_topics; ++k)
     if (!(cfg->alpha[k] > 0.0)) return fail(LDA_ERR_INVALID_ARG, "alpha must be > 0");
   const int64_t D = cfg->num_docs;
-  std::vector<int64_t> off(D + 1);
+  std::vector<int64_t> off = host_vector<int64_t>((size_t)D + 1);
   for (int64_t d = 0; d <= D; ++d) {
     off[d] = doc_off[d] - doc_off[0];
     if (d > 0 && off[d] < off[d - 1]) return fail(LDA_ERR_INVALID_ARG, "doc_off not monotone");
@@ -401,6 +488,13 @@ lda_status lda_create(lda_ctx** out, const lda_config* cfg, const int64_t* doc_o
     c->sample_blocks_frozen = lda::sample_blocks_per_cu(c->C, true, c->K, c->half) * c->cus;
   }
   c->waves_per_block = lda::sample_waves_per_block(c->C, c->sampler == LDA_SAMPLER_SPARSE, c->half);
+  {
+    // the dense samplers recount (LDA_RECOUNT=0 keeps the delta atomics, for
+    // A/B); the index is uint32, so the shard must hold < 2^32 tokens
+    const char* rv = std::getenv("LDA_RECOUNT");
+    c->recount = c->sampler == LDA_SAMPLER_DENSE && !(rv && rv[0] == '0') && N < (int64_t(1) << 32);
+    c->recount_blocks = 8 * c->cus;
+  }
   const int64_t waves = (int64_t)c->sample_blocks * c->waves_per_block;
   int64_t tpr = cfg->tokens_per_range;
   // ~32 ranges per wave: fine enough that the launch tail stays short (C4: +5%
@@ -411,12 +505,13 @@ lda_status lda_create(lda_ctx** out, const lda_config* cfg, const int64_t* doc_o
   c->tokens_per_range = tpr;
   std::vector<int64_t> ranges = make_part_ranges(off, tpr, 1, c->part_range);
   c->R = (int64_t)ranges.size() - 1;
+  c->ranges_h = ranges;
 
   CT(dalloc(&c->words, N));
   CT(dalloc(&c->z, N));
   CT(dalloc(&c->doc_off, D + 1));
   CT(dalloc(&c->range_doc, ranges.size()));
-  CT(dalloc(&c->queue, LDA_MAX_EXCHANGE_PARTS));
+  CT(dalloc(&c->queue, 2 * LDA_MAX_EXCHANGE_PARTS));   // sampler and recount counters per part
   CT(dalloc(&c->nw, (size_t)c->V * c->Kp));
   CT(dalloc(&c->nwsum, c->Kp));
   if (c->sampler == LDA_SAMPLER_DENSE) {
@@ -434,7 +529,9 @@ lda_status lda_create(lda_ctx** out, const lda_config* cfg, const int64_t* doc_o
   for (int i = 0; i < lda_ctx::LDA_TIME_RING; ++i) {
     CT(hipEventCreate(&c->ev0[i]));
     CT(hipEventCreate(&c->ev1[i]));
+    CT(hipEventCreate(&c->ev2[i]));
   }
+  CT(hipMemsetAsync(c->queue, 0, sizeof(int32_t) * 2 * LDA_MAX_EXCHANGE_PARTS, c->stream));
 
   if (N > 0) CT(hipMemcpyAsync(c->words, words, sizeof(int32_t) * N, hipMemcpyHostToDevice, c->stream));
   CT(hipMemcpyAsync(c->doc_off, off.data(), sizeof(int64_t) * (D + 1), hipMemcpyHostToDevice, c->stream));
@@ -449,6 +546,7 @@ lda_status lda_create(lda_ctx** out, const lda_config* cfg, const int64_t* doc_o
   }
   {
     lda_status s = recount_impl(c);
+    if (s == LDA_OK) s = build_recount_index(c);
     if (s != LDA_OK) return bail(s);
   }
   CT(hipMemsetAsync(c->alpha_f, 0, sizeof(float) * c->Kp, c->stream));
@@ -456,42 +554,54 @@ lda_status lda_create(lda_ctx** out, const lda_config* cfg, const int64_t* doc_o
 #undef CT
   *out = c;
   return LDA_OK;
+  });
 }
 
 void lda_destroy(lda_ctx* ctx) { delete ctx; }
 
 lda_status lda_set_stream(lda_ctx* c, void* s) {
+  return lda_abi::guarded([&]() -> lda_status {
   if (!c) return fail(LDA_ERR_INVALID_ARG, "null ctx");
   c->stream = s ? (hipStream_t)s : c->own_stream;
   return LDA_OK;
+  });
 }
 
 lda_status lda_get_stream(lda_ctx* c, void** s) {
+  return lda_abi::guarded([&]() -> lda_status {
   if (!c || !s) return fail(LDA_ERR_INVALID_ARG, "null argument");
   *s = (void*)c->stream;
   return LDA_OK;
+  });
 }
 
 lda_status lda_synchronize(lda_ctx* c) {
+  return lda_abi::guarded([&]() -> lda_status {
   if (!c) return fail(LDA_ERR_INVALID_ARG, "null ctx");
   HIP_TRY(hipSetDevice(c->device));
   HIP_TRY(hipStreamSynchronize(c->stream));
   return LDA_OK;
+  });
 }
 
 lda_status lda_get_sweep(lda_ctx* c, uint32_t* s) {
+  return lda_abi::guarded([&]() -> lda_status {
   if (!c || !s) return fail(LDA_ERR_INVALID_ARG, "null argument");
   *s = c->sweep;
   return LDA_OK;
+  });
 }
 
 lda_status lda_set_sweep(lda_ctx* c, uint32_t s) {
+  return lda_abi::guarded([&]() -> lda_status {
   if (!c) return fail(LDA_ERR_INVALID_ARG, "null ctx");
   c->sweep = s;
   return LDA_OK;
+  });
 }
 
 lda_status lda_get_shape(lda_ctx* c, int32_t* K, int32_t* Kp, int32_t* V, int64_t* D, int64_t* N) {
+  return lda_abi::guarded([&]() -> lda_status {
   if (!c) return fail(LDA_ERR_INVALID_ARG, "null ctx");
   if (K) *K = c->K;
   if (Kp) *Kp = c->Kp;
@@ -499,11 +609,14 @@ lda_status lda_get_shape(lda_ctx* c, int32_t* K, int32_t* Kp, int32_t* V, int64_
   if (D) *D = c->D;
   if (N) *N = c->N;
   return LDA_OK;
+  });
 }
 
 lda_status lda_apply(lda_ctx* c) {
+  return lda_abi::guarded([&]() -> lda_status {
   if (!c) return fail(LDA_ERR_INVALID_ARG, "null ctx");
   return apply_impl(c);
+  });
 }
 
 // One launch of the sampler over part `part` of a (possibly split) sweep.
@@ -521,8 +634,8 @@ static lda_status sample_part_impl(lda_ctx* c, int part) {
     p.range_doc = c->range_doc + r0;
     p.num_ranges = r1 - r0;
     p.queue = c->queue + part;
-    p.delta = c->delta_part[part];
-    p.dsum = c->delta_part[part] + (int64_t)c->V * c->Kp;
+    p.delta = c->recount ? nullptr : c->delta_part[part];   // recount: the sampler writes z only
+    p.dsum = c->recount ? nullptr : c->delta_part[part] + (int64_t)c->V * c->Kp;
     const int64_t wpb = c->waves_per_block;
     // a split sweep leaves reserve_cus CUs' worth of sampler blocks free, so
     // the collective of the part before this one finds CUs to run on
@@ -537,6 +650,18 @@ static lda_status sample_part_impl(lda_ctx* c, int part) {
     else
       HIP_TRY(lda::launch_sample(c->C, false, p, blocks, c->stream, c->half));
     HIP_TRY(hipEventRecord(c->ev1[slot], c->stream));
+    if (c->recount) {
+      // this part's rows recounted into its exchange buffer (the apply left
+      // it zero and zeroed part 0's queue counter)
+      const int64_t i0 = c->part_item[(size_t)part], i1 = c->part_item[(size_t)part + 1];
+      if (part > 0)
+        HIP_TRY(hipMemsetAsync(c->queue + lda::RECOUNT_QUEUE + part, 0, sizeof(int32_t), c->stream));
+      HIP_TRY(lda::launch_recount(c->Kp, c->perm, c->items + 4 * i0, (int32_t)(i1 - i0),
+                                  c->queue + lda::RECOUNT_QUEUE + part, c->z, c->delta_part[part],
+                                  c->delta_part[part] + (int64_t)c->V * c->Kp, c->recount_blocks,
+                                  c->stream));
+    }
+    HIP_TRY(hipEventRecord(c->ev2[slot], c->stream));
     c->launches++;
   }
   c->pending = true;  // the part buffers hold this sweep's changes
@@ -548,6 +673,7 @@ static lda_status sample_part_impl(lda_ctx* c, int part) {
 }
 
 lda_status lda_sample(lda_ctx* c) {
+  return lda_abi::guarded([&]() -> lda_status {
   if (!c) return fail(LDA_ERR_INVALID_ARG, "null ctx");
   if (c->next_part != 0) return fail(LDA_ERR_STATE, "lda_sample inside a split sweep: finish it with lda_sample_part");
   for (int i = 0; i < c->parts; ++i) {
@@ -555,15 +681,19 @@ lda_status lda_sample(lda_ctx* c) {
     if (s) return s;
   }
   return LDA_OK;
+  });
 }
 
 lda_status lda_sample_part(lda_ctx* c, int32_t part) {
+  return lda_abi::guarded([&]() -> lda_status {
   if (!c) return fail(LDA_ERR_INVALID_ARG, "null ctx");
   if (part < 0 || part >= c->parts) return fail(LDA_ERR_INVALID_ARG, "part out of range [0, parts)");
   return sample_part_impl(c, part);
+  });
 }
 
 lda_status lda_set_exchange_parts(lda_ctx* c, int32_t parts, int32_t reserve_cus) {
+  return lda_abi::guarded([&]() -> lda_status {
   if (!c) return fail(LDA_ERR_INVALID_ARG, "null ctx");
   if (parts < 1 || parts > LDA_MAX_EXCHANGE_PARTS)
     return fail(LDA_ERR_INVALID_ARG, "parts must be in [1, LDA_MAX_EXCHANGE_PARTS]");
@@ -596,28 +726,35 @@ lda_status lda_set_exchange_parts(lda_ctx* c, int32_t parts, int32_t reserve_cus
   c->range_doc = dr;
   c->R = (int64_t)ranges.size() - 1;
   c->part_range = pr;
+  c->ranges_h = ranges;
   c->parts = parts;
   c->reserve_cus = reserve_cus;
-  return LDA_OK;
+  return build_recount_index(c);
+  });
 }
 
 lda_status lda_get_exchange_parts(lda_ctx* c, int32_t* parts) {
+  return lda_abi::guarded([&]() -> lda_status {
   if (!c || !parts) return fail(LDA_ERR_INVALID_ARG, "null argument");
   *parts = c->parts;
   return LDA_OK;
+  });
 }
 
 lda_status lda_delta_buffer_part(lda_ctx* c, int32_t part, void** dev_ptr, size_t* count) {
+  return lda_abi::guarded([&]() -> lda_status {
   if (!c || !dev_ptr || !count) return fail(LDA_ERR_INVALID_ARG, "null argument");
   if (part < 0 || part >= c->parts) return fail(LDA_ERR_INVALID_ARG, "part out of range [0, parts)");
   *dev_ptr = c->delta_part[part];
   *count = (size_t)c->V * c->Kp + c->Kp;
   return LDA_OK;
+  });
 }
 
 // Debug (not in the public header): one sparse sampling pass that also
 // records 8 floats per token (kn, sumB, sumA, thr, nnz, z_old, word, u).
 lda_status lda_debug_sample_trace(lda_ctx* c, float* host_trace) {
+  return lda_abi::guarded([&]() -> lda_status {
   if (!c || !host_trace) return fail(LDA_ERR_INVALID_ARG, "null argument");
   if (c->pending) return fail(LDA_ERR_STATE, "pending delta");
   if (c->sampler != LDA_SAMPLER_SPARSE) return fail(LDA_ERR_UNSUPPORTED, "sparse sampler only");
@@ -637,9 +774,11 @@ lda_status lda_debug_sample_trace(lda_ctx* c, float* host_trace) {
   c->sweep++;
   c->pending = true;
   return LDA_OK;
+  });
 }
 
 lda_status lda_last_sample_ms(lda_ctx* c, float* ms) {
+  return lda_abi::guarded([&]() -> lda_status {
   if (!c || !ms) return fail(LDA_ERR_INVALID_ARG, "null argument");
   *ms = 0.0f;
   if (c->launches == 0) return LDA_OK;
@@ -647,10 +786,12 @@ lda_status lda_last_sample_ms(lda_ctx* c, float* ms) {
   HIP_TRY(hipEventSynchronize(c->ev1[slot]));
   HIP_TRY(hipEventElapsedTime(ms, c->ev0[slot], c->ev1[slot]));
   return LDA_OK;
+  });
 }
 
 lda_status lda_philox_draws(uint64_t seed, uint32_t c2, uint32_t c3, const int64_t* gtok, int64_t n,
                             uint32_t* out) {
+  return lda_abi::guarded([&]() -> lda_status {
   if (n < 0 || (n > 0 && (!gtok || !out))) return fail(LDA_ERR_INVALID_ARG, "bad argument");
   if (n == 0) return LDA_OK;
   int64_t* dg = nullptr;
@@ -664,9 +805,11 @@ lda_status lda_philox_draws(uint64_t seed, uint32_t c2, uint32_t c3, const int64
   (void)hipFree(dout);
   HIP_TRY(e);
   return LDA_OK;
+  });
 }
 
 lda_status lda_sample_times(lda_ctx* c, int32_t max, float* ms, int32_t* n) {
+  return lda_abi::guarded([&]() -> lda_status {
   if (!c || !n || max < 0 || (max > 0 && !ms)) return fail(LDA_ERR_INVALID_ARG, "bad argument");
   const int64_t avail = std::min<int64_t>(c->launches, lda_ctx::LDA_TIME_RING);
   const int32_t k = (int32_t)std::min<int64_t>(avail, max);
@@ -677,16 +820,43 @@ lda_status lda_sample_times(lda_ctx* c, int32_t max, float* ms, int32_t* n) {
     HIP_TRY(hipEventElapsedTime(&ms[i], c->ev0[slot], c->ev1[slot]));
   }
   return LDA_OK;
+  });
+}
+
+lda_status lda_recount_times(lda_ctx* c, int32_t max, float* ms, int32_t* n) {
+  return lda_abi::guarded([&]() -> lda_status {
+  if (!c || !n || max < 0 || (max > 0 && !ms)) return fail(LDA_ERR_INVALID_ARG, "bad argument");
+  const int64_t avail = std::min<int64_t>(c->launches, lda_ctx::LDA_TIME_RING);
+  const int32_t k = (int32_t)std::min<int64_t>(avail, max);
+  *n = k;
+  for (int32_t i = 0; i < k; ++i) {
+    const int slot = (int)((c->launches - k + i) % lda_ctx::LDA_TIME_RING);
+    HIP_TRY(hipEventSynchronize(c->ev2[slot]));
+    HIP_TRY(hipEventElapsedTime(&ms[i], c->ev1[slot], c->ev2[slot]));
+  }
+  return LDA_OK;
+  });
+}
+
+lda_status lda_count_update_mode(lda_ctx* c, int32_t* recount) {
+  return lda_abi::guarded([&]() -> lda_status {
+  if (!c || !recount) return fail(LDA_ERR_INVALID_ARG, "null argument");
+  *recount = c->recount ? 1 : 0;
+  return LDA_OK;
+  });
 }
 
 lda_status lda_delta_buffer(lda_ctx* c, void** dev_ptr, size_t* count) {
+  return lda_abi::guarded([&]() -> lda_status {
   if (!c || !dev_ptr || !count) return fail(LDA_ERR_INVALID_ARG, "null argument");
   *dev_ptr = c->delta;
   *count = (size_t)c->V * c->Kp + c->Kp;
   return LDA_OK;
+  });
 }
 
 lda_status lda_sweep(lda_ctx* c, int32_t n) {
+  return lda_abi::guarded([&]() -> lda_status {
   if (!c) return fail(LDA_ERR_INVALID_ARG, "null ctx");
   if (n < 0) return fail(LDA_ERR_INVALID_ARG, "n must be >= 0");
   if (c->pending) {
@@ -700,17 +870,21 @@ lda_status lda_sweep(lda_ctx* c, int32_t n) {
     if (s) return s;
   }
   return LDA_OK;
+  });
 }
 
 lda_status lda_get_z(lda_ctx* c, int32_t* z) {
+  return lda_abi::guarded([&]() -> lda_status {
   if (!c || !z) return fail(LDA_ERR_INVALID_ARG, "null argument");
   HIP_TRY(hipSetDevice(c->device));
   if (c->N > 0) HIP_TRY(hipMemcpyAsync(z, c->z, sizeof(int32_t) * c->N, hipMemcpyDeviceToHost, c->stream));
   HIP_TRY(hipStreamSynchronize(c->stream));
   return LDA_OK;
+  });
 }
 
 lda_status lda_set_z(lda_ctx* c, const int32_t* z) {
+  return lda_abi::guarded([&]() -> lda_status {
   if (!c || !z) return fail(LDA_ERR_INVALID_ARG, "null argument");
   for (int64_t i = 0; i < c->N; ++i)
     if (z[i] < 0 || z[i] >= c->K) return fail(LDA_ERR_INVALID_ARG, "topic out of range [0, K)");
@@ -720,9 +894,11 @@ lda_status lda_set_z(lda_ctx* c, const int32_t* z) {
   if (s) return s;
   HIP_TRY(hipStreamSynchronize(c->stream));
   return LDA_OK;
+  });
 }
 
 lda_status lda_get_counts(lda_ctx* c, int32_t* nw, int32_t* nwsum, int32_t* nd, int32_t* ndsum) {
+  return lda_abi::guarded([&]() -> lda_status {
   if (!c) return fail(LDA_ERR_INVALID_ARG, "null ctx");
   HIP_TRY(hipSetDevice(c->device));
   if (nw) {
@@ -744,9 +920,11 @@ lda_status lda_get_counts(lda_ctx* c, int32_t* nw, int32_t* nwsum, int32_t* nd, 
     for (int64_t d = 0; d < c->D; ++d) ndsum[d] = (int32_t)(c->doc_off_h[d + 1] - c->doc_off_h[d]);
   HIP_TRY(hipStreamSynchronize(c->stream));
   return LDA_OK;
+  });
 }
 
 lda_status lda_set_alpha_beta(lda_ctx* c, const double* alpha, double beta) {
+  return lda_abi::guarded([&]() -> lda_status {
   if (!c || !alpha) return fail(LDA_ERR_INVALID_ARG, "null argument");
   if (!(beta > 0.0)) return fail(LDA_ERR_INVALID_ARG, "beta must be > 0");
   for (int k = 0; k < c->K; ++k)
@@ -764,9 +942,11 @@ lda_status lda_set_alpha_beta(lda_ctx* c, const double* alpha, double beta) {
   }
   HIP_TRY(hipStreamSynchronize(c->stream));
   return LDA_OK;
+  });
 }
 
 lda_status lda_log_likelihood_parts(lda_ctx* c, double* doc_part, double* word_part) {
+  return lda_abi::guarded([&]() -> lda_status {
   if (!c) return fail(LDA_ERR_INVALID_ARG, "null ctx");
   if (c->pending) return fail(LDA_ERR_STATE, "log likelihood with a pending delta: call lda_apply first");
   HIP_TRY(hipSetDevice(c->device));
@@ -802,27 +982,33 @@ lda_status lda_log_likelihood_parts(lda_ctx* c, double* doc_part, double* word_p
   if (doc_part) *doc_part = docs;
   if (word_part) *word_part = words_ll;
   return LDA_OK;
+  });
 }
 
 lda_status lda_log_likelihood(lda_ctx* c, double* out) {
+  return lda_abi::guarded([&]() -> lda_status {
   if (!out) return fail(LDA_ERR_INVALID_ARG, "null argument");
   double a = 0.0, b = 0.0;
   lda_status s = lda_log_likelihood_parts(c, &a, &b);
   if (s) return s;
   *out = a + b;
   return LDA_OK;
+  });
 }
 
 lda_status lda_max_doc_length(lda_ctx* c, int32_t* max_len) {
+  return lda_abi::guarded([&]() -> lda_status {
   if (!c || !max_len) return fail(LDA_ERR_INVALID_ARG, "null argument");
   int64_t m = 0;
   for (int64_t d = 0; d < c->D; ++d) m = std::max(m, c->doc_off_h[d + 1] - c->doc_off_h[d]);
   *max_len = (int32_t)m;
   return LDA_OK;
+  });
 }
 
 lda_status lda_doc_topic_histograms(lda_ctx* c, int32_t max_len, int32_t* doc_len_counts,
                                     int32_t* topic_doc_counts) {
+  return lda_abi::guarded([&]() -> lda_status {
   if (!c || !doc_len_counts || !topic_doc_counts) return fail(LDA_ERR_INVALID_ARG, "null argument");
   int32_t m = 0;
   lda_max_doc_length(c, &m);
@@ -833,7 +1019,13 @@ lda_status lda_doc_topic_histograms(lda_ctx* c, int32_t max_len, int32_t* doc_le
   const size_t n = (size_t)L1 + (size_t)c->K * L1;
   int32_t* buf = nullptr;
   HIP_TRY(dalloc(&buf, n));
-  std::vector<int32_t> h(n);
+  std::vector<int32_t> h;
+  try {
+    h = host_vector<int32_t>(n);
+  } catch (...) {
+    (void)hipFree(buf);
+    throw;
+  }
   hipError_t e = hipMemsetAsync(buf, 0, n * sizeof(int32_t), c->stream);
   if (e == hipSuccess)
     e = lda::launch_doc_hist(c->z, c->doc_off, c->D, c->K, c->Kp, max_len, buf, buf + L1, c->stream);
@@ -844,16 +1036,24 @@ lda_status lda_doc_topic_histograms(lda_ctx* c, int32_t max_len, int32_t* doc_le
   for (int64_t i = 0; i < L1; ++i) doc_len_counts[i] += h[i];
   for (size_t i = 0; i < (size_t)c->K * L1; ++i) topic_doc_counts[i] += h[L1 + i];
   return LDA_OK;
+  });
 }
 
 lda_status lda_count_histogram(lda_ctx* c, int64_t max_count, int32_t* count_hist) {
+  return lda_abi::guarded([&]() -> lda_status {
   if (!c || !count_hist || max_count < 0) return fail(LDA_ERR_INVALID_ARG, "bad argument");
   if (c->pending) return fail(LDA_ERR_STATE, "histogram with a pending delta: call lda_apply first");
   HIP_TRY(hipSetDevice(c->device));
   const size_t n = (size_t)max_count + 1;
   int32_t* buf = nullptr;
   HIP_TRY(dalloc(&buf, n + 1));
-  std::vector<int32_t> h(n + 1);
+  std::vector<int32_t> h;
+  try {
+    h = host_vector<int32_t>(n + 1);
+  } catch (...) {
+    (void)hipFree(buf);
+    throw;
+  }
   hipError_t e = hipMemsetAsync(buf, 0, (n + 1) * sizeof(int32_t), c->stream);
   if (e == hipSuccess)
     e = lda::launch_count_hist(c->nw, c->V, c->K, c->Kp, max_count, buf, buf + n, c->stream);
@@ -864,9 +1064,11 @@ lda_status lda_count_histogram(lda_ctx* c, int64_t max_count, int32_t* count_his
   if (h[n]) return fail(LDA_ERR_INVALID_ARG, "an nw cell exceeds max_count");
   for (size_t i = 0; i < n; ++i) count_hist[i] += h[i];
   return LDA_OK;
+  });
 }
 
 lda_status lda_row_stats(lda_ctx* c, double* mean_row_nnz) {
+  return lda_abi::guarded([&]() -> lda_status {
   if (!c || !mean_row_nnz) return fail(LDA_ERR_INVALID_ARG, "null argument");
   if (c->pending) return fail(LDA_ERR_STATE, "row statistics with a pending delta: call lda_apply first");
   HIP_TRY(hipSetDevice(c->device));
@@ -881,10 +1083,12 @@ lda_status lda_row_stats(lda_ctx* c, double* mean_row_nnz) {
   HIP_TRY(e);
   *mean_row_nnz = h[1] ? (double)h[0] / (double)h[1] : 0.0;
   return LDA_OK;
+  });
 }
 
 lda_status lda_infer(lda_ctx* c, int64_t Dh, const int64_t* doc_off, const int32_t* words_in,
                      int32_t n_iter, int32_t thin, int32_t burn_in, uint64_t seed, double* theta) {
+  return lda_abi::guarded([&]() -> lda_status {
   if (!c || !doc_off || !theta) return fail(LDA_ERR_INVALID_ARG, "null argument");
   if (Dh < 0 || n_iter < 0 || burn_in < 0 || thin < 1) return fail(LDA_ERR_INVALID_ARG, "bad sizes");
   if (c->pending) return fail(LDA_ERR_STATE, "inference with a pending delta: call lda_apply first");
@@ -983,7 +1187,7 @@ lda_status lda_infer(lda_ctx* c, int64_t Dh, const int64_t* doc_off, const int32
     nsamples = 1;
     if (e == hipSuccess) chk(lda::launch_doc_topics(dz, doff, Dh, c->K, c->Kp, acc, 1, c->stream));
   }
-  std::vector<int32_t> acc_h((size_t)Dh * c->K);
+  std::vector<int32_t> acc_h = host_vector<int32_t>((size_t)Dh * c->K);
   if (e == hipSuccess && Dh > 0)
     chk(hipMemcpyAsync(acc_h.data(), acc, sizeof(int32_t) * (size_t)Dh * c->K, hipMemcpyDeviceToHost, c->stream));
   if (e == hipSuccess) chk(hipStreamSynchronize(c->stream));
@@ -998,9 +1202,11 @@ lda_status lda_infer(lda_ctx* c, int64_t Dh, const int64_t* doc_off, const int32
     for (int k = 0; k < c->K; ++k) theta[(size_t)d * c->K + k] /= sum;
   }
   return LDA_OK;
+  });
 }
 
 lda_status lda_to_mallet_packed(lda_ctx* c, int32_t* rows, int64_t* row_off, int32_t* topic_bits) {
+  return lda_abi::guarded([&]() -> lda_status {
   if (!c || !row_off) return fail(LDA_ERR_INVALID_ARG, "null argument");
   if (c->pending) return fail(LDA_ERR_STATE, "pending delta: call lda_apply first");
   // ParallelTopicModel(numberOfTopics, ...): topicMask / topicBits [M]
@@ -1014,7 +1220,7 @@ lda_status lda_to_mallet_packed(lda_ctx* c, int32_t* rows, int64_t* row_off, int
   }
   const int32_t bits = __builtin_popcount((unsigned)mask);
   if (topic_bits) *topic_bits = bits;
-  std::vector<int32_t> nw((size_t)c->V * c->K);
+  std::vector<int32_t> nw = host_vector<int32_t>((size_t)c->V * c->K);
   lda_status s = lda_get_counts(c, nw.data(), nullptr, nullptr, nullptr);
   if (s) return s;
   // row length = min(K, typeTotal) exactly as addInstances allocates it
@@ -1042,6 +1248,7 @@ lda_status lda_to_mallet_packed(lda_ctx* c, int32_t* rows, int64_t* row_off, int
     for (int64_t i = 0; i < len; ++i) rows[o + i] = i < (int64_t)cell.size() ? cell[i] : 0;
   }
   return LDA_OK;
+  });
 }
 
 }  // extern "C"

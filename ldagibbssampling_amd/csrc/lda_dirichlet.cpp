@@ -22,6 +22,7 @@
 #include <vector>
 
 #include "../../include/lda_mi355x.h"
+#include "lda_guard.h"
 
 namespace {
 
@@ -63,13 +64,14 @@ double lda_digamma(double z) { return digamma(z); }
 lda_status lda_learn_parameters(double* params, int32_t K, const int32_t* observations,
                                 const int32_t* observation_lengths, int32_t max_len, double shape,
                                 double scale, int32_t iterations, double* params_sum) {
+  return lda_abi::guarded([&]() -> lda_status {
   if (!params || !observations || !observation_lengths || K < 1 || max_len < 0 || iterations < 0)
     return LDA_ERR_INVALID_ARG;
   const int64_t L1 = (int64_t)max_len + 1;
   double psum = 0.0;
   for (int k = 0; k < K; ++k) psum += params[k];
   // last index with a non-zero count in each topic's histogram (-1: none)
-  std::vector<int64_t> last(K, -1);
+  std::vector<int64_t> last = lda_abi::host_vector<int64_t>((size_t)K, -1);
   for (int k = 0; k < K; ++k)
     for (int64_t i = 0; i < L1; ++i)
       if (observations[k * L1 + i] > 0) last[k] = i;
@@ -97,12 +99,14 @@ lda_status lda_learn_parameters(double* params, int32_t K, const int32_t* observ
   }
   if (params_sum) *params_sum = psum;
   return psum < 0.0 ? LDA_ERR_INVALID_ARG : LDA_OK;
+  });
 }
 
 lda_status lda_learn_symmetric_concentration(const int32_t* count_hist, int64_t max_count,
                                              const int64_t* lengths, const int32_t* length_counts,
                                              int64_t n_lengths, int32_t num_dims, double current,
                                              double* out) {
+  return lda_abi::guarded([&]() -> lda_status {
   if (!count_hist || !out || max_count < 0 || n_lengths < 0 || num_dims < 1 ||
       (n_lengths > 0 && (!lengths || !length_counts)))
     return LDA_ERR_INVALID_ARG;
@@ -163,6 +167,7 @@ lda_status lda_learn_symmetric_concentration(const int32_t* count_hist, int64_t 
   }
   *out = value;
   return LDA_OK;
+  });
 }
 
 }  // extern "C"

@@ -365,7 +365,7 @@ void k_sample(SampleParams p) {
     // topic zo_ -> zn_): two wave-wide atomics per 64 tokens; the 32-bit cell
     // index is valid because lda_create keeps V*Kp < 2^32
     auto flush_delta = [&](int w_, int zo_, int zn_) {
-      if (!FROZEN && LDA_CHUNK_DELTA && zn_ != zo_) {
+      if (!FROZEN && LDA_CHUNK_DELTA && p.delta && zn_ != zo_) {
         const uint32_t row = (uint32_t)w_ * (uint32_t)KP;
         atomicAdd(p.delta + (row + (uint32_t)zo_), -1);
         atomicAdd(p.delta + (row + (uint32_t)zn_), 1);
@@ -690,7 +690,7 @@ void k_sample(SampleParams p) {
     wave_lds_fence();
   }
 
-  if (!FROZEN) {
+  if (!FROZEN && p.dsum) {
     __syncthreads();
     for (int i = threadIdx.x; i < KP; i += 256) {
       const int v = bsum[i];
@@ -815,7 +815,7 @@ __global__ __launch_bounds__(256) void k_sample_half(SampleParams p) {
     if ((lane >> 5) == h) {
       const int n = HS(h).nt - HS(h).cbase;
       if (hl < n) p.z[HS(h).t0 + HS(h).cbase + hl] = cn;
-      if (!FROZEN && cn != cz) {
+      if (!FROZEN && p.delta && cn != cz) {
         const uint32_t row = (uint32_t)(cw & kWordMask) * (uint32_t)KP;
         atomicAdd(p.delta + (row + (uint32_t)cz), -1);
         atomicAdd(p.delta + (row + (uint32_t)cn), 1);
@@ -1070,7 +1070,7 @@ __global__ __launch_bounds__(256) void k_sample_half(SampleParams p) {
   }
 done:
 #undef HS
-  if (!FROZEN) {
+  if (!FROZEN && p.dsum) {
     __syncthreads();
     for (int i = threadIdx.x; i < KP; i += 256) {
       const int v = bsum[i];
@@ -1209,7 +1209,7 @@ __global__ __launch_bounds__(256) QUARTER_ATTR void k_sample_quarter(SampleParam
             // the range is done (or none loaded yet): publish, clear, next range
             if (loaded) {
               if (ql < nt - cbase) p.z[t0 + cbase + ql] = cn;
-              if (!FROZEN && cn != cz) {
+              if (!FROZEN && p.delta && cn != cz) {
                 const uint32_t row = (uint32_t)cw * (uint32_t)KP;
                 atomicAdd(p.delta + (row + (uint32_t)cz), -1);
                 atomicAdd(p.delta + (row + (uint32_t)cn), 1);
@@ -1283,7 +1283,7 @@ __global__ __launch_bounds__(256) QUARTER_ATTR void k_sample_quarter(SampleParam
             if (t - cbase == 16) {
               // chunk switch: publish the finished chunk, shift
               p.z[t0 + cbase + ql] = cn;
-              if (!FROZEN && cn != cz) {
+              if (!FROZEN && p.delta && cn != cz) {
                 const uint32_t row = (uint32_t)cw * (uint32_t)KP;
                 atomicAdd(p.delta + (row + (uint32_t)cz), -1);
                 atomicAdd(p.delta + (row + (uint32_t)cn), 1);
@@ -1409,7 +1409,7 @@ __global__ __launch_bounds__(256) QUARTER_ATTR void k_sample_quarter(SampleParam
     }
   }
 done:
-  if (!FROZEN) {
+  if (!FROZEN && p.dsum) {
     __syncthreads();
     for (int i = threadIdx.x; i < KP; i += 256) {
       const int v = bsum[i];
@@ -1764,7 +1764,7 @@ __global__ __launch_bounds__(256) void k_sample_sparse(SampleParams p) {
     wave_lds_fence();
   }
 
-  if (!FROZEN) {
+  if (!FROZEN && p.dsum) {
     __syncthreads();
     for (int i = threadIdx.x; i < KP; i += 256) {
       const int v = bsum[i];
@@ -2367,7 +2367,7 @@ __global__ __launch_bounds__(256) void k_apply_packed(int32_t* __restrict__ nw, 
   if (blockIdx.x == 0) {
     int32_t* dsum = delta + V * KP;
     for (int k = threadIdx.x; k < KP; k += 256) {
-      const int32_t s = t.nwsum[k] + dsum[k];
+      const int32_t s = t.absolute ? dsum[k] : t.nwsum[k] + dsum[k];
       t.nwsum[k] = s;
       dsum[k] = 0;
       if (k < t.K) {
@@ -2380,20 +2380,32 @@ __global__ __launch_bounds__(256) void k_apply_packed(int32_t* __restrict__ nw, 
         t.inv_m1[k] = 0.0f;
       }
     }
-    if (threadIdx.x == 0 && t.queue) *t.queue = 0;
+    if (t.queue && threadIdx.x < 2) t.queue[threadIdx.x * RECOUNT_QUEUE] = 0;
   }
   for (int64_t w = (int64_t)blockIdx.x * 4 + wid; w < V; w += (int64_t)gridDim.x * 4) {
     int32_t c[C], d[C];
-    load_row<C>(c, nw + w * KP + lane * C);
     load_row<C>(d, delta + w * KP + lane * C);
+    if (t.absolute) {
+      // the buffer holds the recounted counts (k_recount, summed across
+      // shards): they replace the row, and the buffer is left zero
+#pragma unroll
+      for (int j = 0; j < C; ++j) {
+        c[j] = d[j];
+        nw[w * KP + lane * C + j] = c[j];
+      }
+    } else {
+      load_row<C>(c, nw + w * KP + lane * C);
+    }
     bool changed = false;
 #pragma unroll
     for (int j = 0; j < C; ++j) changed |= d[j] != 0;
     if (changed) {
 #pragma unroll
       for (int j = 0; j < C; ++j) {
-        c[j] += d[j];
-        nw[w * KP + lane * C + j] = c[j];
+        if (!t.absolute) {
+          c[j] += d[j];
+          nw[w * KP + lane * C + j] = c[j];
+        }
         delta[w * KP + lane * C + j] = 0;
       }
     }
@@ -2655,6 +2667,107 @@ __global__ __launch_bounds__(256) void k_infer_init(const int32_t* __restrict__ 
       }
     }
     if (lane == 0) z[i] = best_k;
+  }
+}
+
+// ---------------------------------------------------------------- recount
+// The dense samplers' count update without atomics in the sampler (DESIGN
+// §4 "Recount"): the sampler only writes z; afterwards every word's row of
+// THIS shard is recounted from a word-sorted token index, and the result is
+// the exchange buffer (summed across shards as Mallet's sumTypeTopicCounts
+// sums its workers' local typeTopicCounts [M]); k_apply_packed then replaces
+// nw by it.  Integer counts: the result does not depend on any order.
+
+// tokens per (part, word): cnt[part * V + w]
+__global__ __launch_bounds__(256) void k_word_hist(const int32_t* __restrict__ words, int64_t n,
+                                                   PartSpans ps, int64_t V,
+                                                   uint32_t* __restrict__ cnt) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    int part = 0;
+    while (part + 1 < ps.parts && i >= ps.tok[part + 1]) ++part;
+    atomicAdd(&cnt[(int64_t)part * V + words[i]], 1u);
+  }
+}
+
+// perm[cursor[part * V + w]++] = i: token indices grouped by (part, word)
+// (the order inside a group is whatever the atomics give; nothing depends
+// on it)
+__global__ __launch_bounds__(256) void k_word_scatter(const int32_t* __restrict__ words, int64_t n,
+                                                      PartSpans ps, int64_t V,
+                                                      uint32_t* __restrict__ cursor,
+                                                      uint32_t* __restrict__ perm) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    int part = 0;
+    while (part + 1 < ps.parts && i >= ps.tok[part + 1]) ++part;
+    const uint32_t pos = atomicAdd(&cursor[(int64_t)part * V + words[i]], 1u);
+    perm[pos] = (uint32_t)i;
+  }
+}
+
+// One wave per work item {word, first perm index, tokens, split}: the
+// item's topics are histogrammed in LDS (z gathered through perm, four
+// 64-token loads in flight per lane), then the row goes out -- stored whole
+// when the word is one item, added cell by cell (device atomics on the
+// nonzero cells) when it is split over several; the buffer is zero on entry
+// (k_apply_packed leaves it so).  The block's column sums go to bufsum.
+template <int C>
+__global__ __launch_bounds__(256) void k_recount(const uint32_t* __restrict__ perm,
+                                                 const int4* __restrict__ items, int32_t n_items,
+                                                 int32_t* __restrict__ queue,
+                                                 const int32_t* __restrict__ z,
+                                                 int32_t* __restrict__ buf,
+                                                 int32_t* __restrict__ bufsum) {
+  constexpr int KP = C * 64;
+  __shared__ __attribute__((aligned(16))) int32_t lds[5 * KP];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  int32_t* hist = lds + wid * KP;
+  int32_t* bs = lds + 4 * KP;
+  for (int i = threadIdx.x; i < 5 * KP; i += 256) lds[i] = 0;
+  __syncthreads();
+  while (true) {
+    int it = 0;
+    if (lane == 0) it = atomicAdd(queue, 1);
+    it = uniform_i(__shfl(it, 0));
+    if (it >= n_items) break;
+    const int4 m = items[it];
+    const uint32_t b = (uint32_t)m.y;
+    const int len = m.z;
+    for (int i = lane; i < len; i += 256) {
+      uint32_t tk[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) tk[u] = (i + 64 * u < len) ? perm[b + (uint32_t)(i + 64 * u)] : 0xFFFFFFFFu;
+      int k[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) k[u] = tk[u] != 0xFFFFFFFFu ? z[tk[u]] : -1;
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        if (k[u] >= 0) atomicAdd(&hist[k[u]], 1);
+    }
+    wave_lds_fence();
+    int32_t h[C];
+#pragma unroll
+    for (int j = 0; j < C; ++j) {
+      h[j] = hist[lane * C + j];
+      hist[lane * C + j] = 0;
+    }
+    int32_t* row = buf + (int64_t)m.x * KP + lane * C;
+    if (m.w == 0) {
+#pragma unroll
+      for (int j = 0; j < C; ++j) row[j] = h[j];
+    } else {
+#pragma unroll
+      for (int j = 0; j < C; ++j)
+        if (h[j]) atomicAdd(&row[j], h[j]);
+    }
+#pragma unroll
+    for (int j = 0; j < C; ++j)
+      if (h[j]) atomicAdd(&bs[lane * C + j], h[j]);
+    wave_lds_fence();
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < KP; i += 256) {
+    const int v = bs[i];
+    if (v != 0) atomicAdd(&bufsum[i], v);
   }
 }
 
@@ -3022,5 +3135,39 @@ hipError_t launch_infer_init(const int32_t* words, int32_t* z, int64_t n, const 
   hipLaunchKernelGGL(k_infer_init, dim3(blocks), dim3(256), 0, st, words, z, n, nw, K, Kp);
   return hipGetLastError();
 }
+
+hipError_t launch_word_hist(const int32_t* words, int64_t n, const PartSpans& ps, int64_t V,
+                            uint32_t* cnt, hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  const int blocks = (int)std::min<int64_t>((n + 255) / 256, 8192);
+  hipLaunchKernelGGL(k_word_hist, dim3(blocks), dim3(256), 0, st, words, n, ps, V, cnt);
+  return hipGetLastError();
+}
+
+hipError_t launch_word_scatter(const int32_t* words, int64_t n, const PartSpans& ps, int64_t V,
+                               uint32_t* cursor, uint32_t* perm, hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  const int blocks = (int)std::min<int64_t>((n + 255) / 256, 8192);
+  hipLaunchKernelGGL(k_word_scatter, dim3(blocks), dim3(256), 0, st, words, n, ps, V, cursor, perm);
+  return hipGetLastError();
+}
+
+hipError_t launch_recount(int32_t Kp, const uint32_t* perm, const int32_t* items, int32_t n_items,
+                          int32_t* queue, const int32_t* z, int32_t* buf, int32_t* bufsum, int blocks,
+                          hipStream_t st) {
+  if (n_items <= 0) return hipSuccess;
+  blocks = std::max(1, std::min(blocks, (n_items + 3) / 4));
+  const int4* it = reinterpret_cast<const int4*>(items);
+  switch (Kp / 64) {
+    case 1: hipLaunchKernelGGL(k_recount<1>, dim3(blocks), dim3(256), 0, st, perm, it, n_items, queue, z, buf, bufsum); break;
+    case 2: hipLaunchKernelGGL(k_recount<2>, dim3(blocks), dim3(256), 0, st, perm, it, n_items, queue, z, buf, bufsum); break;
+    case 4: hipLaunchKernelGGL(k_recount<4>, dim3(blocks), dim3(256), 0, st, perm, it, n_items, queue, z, buf, bufsum); break;
+    case 8: hipLaunchKernelGGL(k_recount<8>, dim3(blocks), dim3(256), 0, st, perm, it, n_items, queue, z, buf, bufsum); break;
+    case 16: hipLaunchKernelGGL(k_recount<16>, dim3(blocks), dim3(256), 0, st, perm, it, n_items, queue, z, buf, bufsum); break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
 
 }  // namespace lda

@@ -735,6 +735,9 @@ lda_status guard(F&& f) {
   } catch (const std::exception& e) {
     g_tm_error = e.what();
     return LDA_ERR_INVALID_ARG;
+  } catch (...) {
+    g_tm_error = "internal error: unknown exception";
+    return LDA_ERR_INTERNAL;
   }
 }
 
@@ -755,13 +758,16 @@ lda_status write_file(const char* path, const std::string& s) {
     g_tm_error = "null path";
     return LDA_ERR_INVALID_ARG;
   }
-  std::ofstream f(path, std::ios::binary);
-  if (!f) {
-    g_tm_error = std::string("cannot open ") + path;
-    return LDA_ERR_INVALID_ARG;
-  }
-  f << s;
-  return f.good() ? LDA_OK : LDA_ERR_INVALID_ARG;
+  bool ok = false;
+  const lda_status st = guard([&] {
+    std::ofstream f(path, std::ios::binary);
+    if (!f) throw lda_host::Error{LDA_ERR_INVALID_ARG, std::string("cannot open ") + path};
+    f << s;
+    ok = f.good();
+  });
+  if (st) return st;
+  if (!ok) g_tm_error = std::string("write failed: ") + path;
+  return ok ? LDA_OK : LDA_ERR_INVALID_ARG;
 }
 
 #define TM_CHECK(m)                 \
@@ -780,7 +786,9 @@ lda_status ldatm_format_double(double x, int32_t style, char* buf, size_t cap) {
     g_tm_error = "style must be 0 or 1";
     return LDA_ERR_INVALID_ARG;
   }
-  return copy_text(style == 0 ? lda_host::java_double(x) : lda_host::java_number5(x), buf, cap, nullptr);
+  std::string t;
+  const lda_status st = guard([&] { t = style == 0 ? lda_host::java_double(x) : lda_host::java_number5(x); });
+  return st ? st : copy_text(t, buf, cap, nullptr);
 }
 
 lda_status ldatm_create(ldatm** out, int32_t num_topics, double alpha_sum, double beta) {

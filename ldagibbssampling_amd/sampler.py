@@ -171,6 +171,23 @@ class GibbsSampler:
                                             C.byref(n)), "lda_sample_times")
         return ms[:n.value]
 
+    def recount_times(self, last: int) -> np.ndarray:
+        """Kernel durations (ms) of the recount after each of the last `last`
+        lda_sample launches (zeros in the delta mode)."""
+        ms = np.zeros(max(int(last), 0), dtype=np.float32)
+        n = C.c_int32()
+        capi.check(self._L.lda_recount_times(self._h, len(ms), ms.ctypes.data if len(ms) else None,
+                                             C.byref(n)), "lda_recount_times")
+        return ms[:n.value]
+
+    @property
+    def recount(self) -> bool:
+        """True when the exchange buffer holds recounted counts (dense samplers),
+        False when it holds a delta (lda_count_update_mode)."""
+        r = C.c_int32()
+        capi.check(self._L.lda_count_update_mode(self._h, C.byref(r)), "lda_count_update_mode")
+        return bool(r.value)
+
     # ---------------------------------------------------------------- state
     def z(self) -> np.ndarray:
         out = np.empty(self.N, dtype=np.int32)

@@ -24,6 +24,21 @@ import pytest
 
 pytestmark = [pytest.mark.gpu, pytest.mark.slow]
 
+ALPHA_SUM, BETA = 10.0, 0.01
+
+
+def score_state(oracle, K, V, train, z, held_obs, held_sc):
+    """Perplexity of a trained state z, scored on the CPU by cpu_exact (the
+    bit-exact restatement of the GPU's quarter-wave inference draw) with the
+    estimator of _perplexity: the fixture path for cpu_mallet's states."""
+    e = oracle.ExactSampler(K, V, train.doc_off, train.words, np.full(K, ALPHA_SUM / K), BETA, 1,
+                            z_init=z, half=2)
+    e.sweep(0)
+    theta = e.infer(held_obs.doc_off, held_obs.words, n_iter=100, burn_in=10, thin=10, seed=7)
+    nw, nwsum, _, _ = e.counts()
+    ll = oracle.doc_completion_loglik(K, V, nw, nwsum, BETA, theta, held_sc.doc_off, held_sc.words)
+    return float(np.exp(-ll / held_sc.num_tokens))
+
 
 def _perplexity(sampler, held_obs, held_sc, oracle):
     theta = sampler.infer(held_obs.doc_off, held_obs.words, n_iter=100, burn_in=10, thin=10, seed=7)
