@@ -239,8 +239,8 @@ def main():
     ap.add_argument("--exchange-parts", type=int, default=None,
                     help="N > 1: split every sweep into P parts whose all-reduces overlap the "
                          "next part's sampling (default 1: DESIGN.md §5)")
-    ap.add_argument("--reserve-cus", type=int, default=8,
-                    help="split sweeps: CUs' worth of sampler blocks left free for RCCL")
+    ap.add_argument("--reserve-cus", type=int, default=-1,
+                    help="split sweeps: CUs' worth of sampler blocks left free for RCCL (-1: the library default, 1/32 of the CUs)")
     args = ap.parse_args()
     if os.environ.get("LDA_BENCH_STACKS"):
         # diagnostics: every rank dumps its Python stacks every N s to stderr

@@ -126,7 +126,8 @@ lda_status lda_apply(lda_ctx* ctx);
  * lda_apply folds every buffer.  Results are identical for any `parts`
  * (integer sums; draws keyed by the global token index).  lda_sample runs
  * every part.  reserve_cus: CUs' worth of sampler blocks left free in a split
- * sweep for the collective's kernels (0 = none). */
+ * sweep for the collective's kernels (0 = none, < 0 = the default: 1/32 of
+ * the device's CUs, 8 on MI355X). */
 #define LDA_MAX_EXCHANGE_PARTS 4
 lda_status lda_set_exchange_parts(lda_ctx* ctx, int32_t parts, int32_t reserve_cus);
 lda_status lda_get_exchange_parts(lda_ctx* ctx, int32_t* parts);

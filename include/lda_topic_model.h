@@ -56,9 +56,26 @@ lda_status ldatm_set_symmetric_alpha(ldatm* m, int32_t on);    /* setSymmetricAl
 lda_status ldatm_set_topic_display(ldatm* m, int32_t interval, int32_t n); /* setTopicDisplay */
 lda_status ldatm_set_random_seed(ldatm* m, int64_t seed);      /* setRandomSeed      */
 /* setNumThreads: Mallet's document blocks.  Here a block is a GPU shard:
- * min(n, visible devices) GPUs, RCCL all-reduce of the delta between them.
- * Results do not depend on it (integer deltas, global Philox counters). */
+ * ldatm_plan_shards(n, visible devices, corpus) GPUs -- at most n and the
+ * devices, and ONE when the sweep is too short to pay for the exchange (the
+ * reference's own ~16k-token corpus with setNumThreads(4)) -- with an RCCL
+ * all-reduce of the exchange buffer between them.  Results do not depend on
+ * it (integer sums, global Philox counters). */
 lda_status ldatm_set_num_threads(ldatm* m, int32_t n);
+/* The shard plan of setNumThreads (host-only): min(num_threads, num_devices,
+ * num_docs) shards, reduced while (1 - 1/G) of the estimated sweep time
+ * (num_tokens x (2 Kp + 16) bytes at 5 TB/s) does not exceed the estimated
+ * ring all-reduce of 4 (V Kp + Kp) bytes (100 GB/s per link + 100 us). */
+int32_t ldatm_plan_shards(int32_t num_threads, int32_t num_devices, int64_t num_tokens,
+                          int32_t num_types, int32_t num_topics, int64_t num_docs);
+/* Explicit shard placement: n shards, shard g on HIP device devices[g]
+ * (n = 0: back to setNumThreads' plan).  Shards on distinct devices exchange
+ * through RCCL; shards that ALL share one device exchange through a
+ * device-side sum with the same streams, events and apply ordering (the
+ * multi-shard path on a one-GPU box).  Other mixes: LDA_ERR_UNSUPPORTED. */
+lda_status ldatm_set_devices(ldatm* m, int32_t n, const int32_t* devices);
+/* Shards the next estimate() runs on (creates them if needed). */
+lda_status ldatm_num_shards(ldatm* m, int32_t* shards);
 /* LDA_SAMPLER_* (default: DENSE for K <= 1024, SPARSE above) */
 lda_status ldatm_set_sampler(ldatm* m, int32_t sampler);
 /* With more than one GPU shard: cut every sweep into `parts` parts

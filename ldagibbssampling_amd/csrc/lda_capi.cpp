@@ -697,7 +697,9 @@ lda_status lda_set_exchange_parts(lda_ctx* c, int32_t parts, int32_t reserve_cus
   if (!c) return fail(LDA_ERR_INVALID_ARG, "null ctx");
   if (parts < 1 || parts > LDA_MAX_EXCHANGE_PARTS)
     return fail(LDA_ERR_INVALID_ARG, "parts must be in [1, LDA_MAX_EXCHANGE_PARTS]");
-  if (reserve_cus < 0) return fail(LDA_ERR_INVALID_ARG, "reserve_cus must be >= 0");
+  // < 0: the default, 1/32 of the CUs (8 on MI355X's 256; C4 split-sweep A/B
+  // on one GPU: DESIGN.md §5)
+  if (reserve_cus < 0) reserve_cus = std::max(1, c->cus / 32);
   if (c->next_part != 0) return fail(LDA_ERR_STATE, "inside a split sweep");
   HIP_TRY(hipSetDevice(c->device));
   HIP_TRY(hipStreamSynchronize(c->stream));

@@ -45,7 +45,50 @@ void check(lda_status s, const char* where) {
   }
 }
 
+// dst[i] += src[i]: the in-process sum of shard buffers that share one device
+// (ShardGroup's local exchange; RCCL refuses two ranks on one GPU)
+__global__ void k_sum_into(int4* __restrict__ dst, const int4* __restrict__ src, int64_t n4) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (int64_t)gridDim.x * blockDim.x) {
+    const int4 b = src[i];
+    if (b.x | b.y | b.z | b.w) {
+      int4 a = dst[i];
+      a.x += b.x;
+      a.y += b.y;
+      a.z += b.z;
+      a.w += b.w;
+      dst[i] = a;
+    }
+  }
+}
+
+void hip_check(hipError_t e, const char* what) {
+  if (e != hipSuccess) raise(e == hipErrorOutOfMemory ? LDA_ERR_OUT_OF_MEMORY : LDA_ERR_DEVICE,
+                             std::string(what) + ": " + hipGetErrorString(e));
+}
+
 }  // namespace
+
+// How many GPU shards setNumThreads(n) becomes (ldatm_plan_shards): at most
+// n, the visible devices and the documents, and one when splitting the
+// sweep saves less than the exchange costs.  Per sweep, the sampler moves
+// ~(2 Kp + 16) bytes per token (the 16-bit row + stream; the sparse kernels
+// read fewer bytes at a lower rate) at ~5 TB/s, the exchange is a ring
+// all-reduce of 4 (V Kp + Kp) bytes at ~100 GB/s per link plus ~100 us of
+// latency; G shards save (1 - 1/G) of the sweep.  The reference's own corpus
+// (C1: ~16k tokens, K = 500, V ~ 5000) with setNumThreads(4) gets one GPU: its
+// ~40 us sweep is far below a 10 MB all-reduce.
+int32_t plan_shards(int32_t num_threads, int32_t num_devices, int64_t num_tokens, int32_t num_types,
+                    int32_t num_topics, int64_t num_docs) {
+  const int64_t g = std::max<int64_t>(1, std::min<int64_t>({(int64_t)num_threads, (int64_t)num_devices,
+                                                            std::max<int64_t>(num_docs, 1)}));
+  if (g < 2) return 1;
+  const double kp = (double)lda_padded_topics(num_topics);
+  const double sweep_s = (double)num_tokens * (2.0 * kp + 16.0) / 5e12;
+  const double exch_s = 2.0 * 4.0 * ((double)num_types * kp + kp) / 1e11 + 1e-4;
+  for (int64_t k = g; k >= 2; --k)
+    if (sweep_s * (1.0 - 1.0 / (double)k) > exch_s) return (int32_t)k;
+  return 1;
+}
 
 // ----------------------------------------------------------------- shards
 // One lda_ctx per GPU over a contiguous, token-balanced document range; the
@@ -57,23 +100,84 @@ void check(lda_status s, const char* where) {
 // issued on a per-shard collective stream that waits only for part i, so it
 // runs while part i+1 samples, and the shards' streams wait for the last sum
 // before the apply.  Same sweep bit for bit (integer sums, fixed snapshot).
+//
+// Shards on distinct devices exchange through RCCL.  Shards that share one
+// device (ParallelTopicModel::setDevices, e.g. {0, 0, 0}: the multi-shard
+// path exercised on a one-GPU box) exchange through a device-side sum
+// instead -- shard 0's stream adds every other buffer into its own and copies
+// the sum back -- with the same events, streams and apply ordering.
 class ShardGroup {
  public:
   std::vector<lda_ctx*> ctx;
+  std::vector<int> dev;            // shard g runs on device dev[g]
   std::vector<int64_t> doc_begin;  // shard g owns documents [doc_begin[g], doc_begin[g+1])
+  bool local_sum = false;          // every shard on one device: no RCCL
   std::vector<ncclComm_t> comms;
   std::vector<hipStream_t> comm_streams;  // per shard, split sweeps only
   std::vector<hipEvent_t> events;
+  std::vector<hipEvent_t> sum_events;     // local_sum: per shard "sampled" / shard 0 "summed"
   int parts = 1;
 
   ~ShardGroup() {
     for (auto c : comms) ncclCommDestroy(c);
     for (size_t g = 0; g < comm_streams.size(); ++g) {
-      (void)hipSetDevice((int)g);
+      (void)hipSetDevice(dev[g]);
       (void)hipEventDestroy(events[g]);
       (void)hipStreamDestroy(comm_streams[g]);
     }
+    for (size_t g = 0; g < sum_events.size(); ++g) {
+      (void)hipSetDevice(dev[g]);
+      (void)hipEventDestroy(sum_events[g]);
+    }
     for (auto c : ctx) lda_destroy(c);
+  }
+
+  void init_exchange() {
+    const size_t G = ctx.size();
+    if (G < 2) return;
+    local_sum = std::all_of(dev.begin(), dev.end(), [&](int d) { return d == dev[0]; });
+    if (local_sum) {
+      sum_events.resize(G);
+      hip_check(hipSetDevice(dev[0]), "hipSetDevice");
+      for (size_t g = 0; g < G; ++g)
+        hip_check(hipEventCreateWithFlags(&sum_events[g], hipEventDisableTiming), "hipEventCreate");
+      return;
+    }
+    std::vector<int> sorted = dev;
+    std::sort(sorted.begin(), sorted.end());
+    if (std::adjacent_find(sorted.begin(), sorted.end()) != sorted.end())
+      raise(LDA_ERR_UNSUPPORTED, "shards share a device with others on different devices: place all on "
+                                 "one device or each on its own");
+    comms.resize(G);
+    const ncclResult_t r = ncclCommInitAll(comms.data(), (int)G, dev.data());
+    if (r != ncclSuccess) {
+      comms.clear();
+      raise(LDA_ERR_DEVICE, std::string("ncclCommInitAll: ") + ncclGetErrorString(r));
+    }
+  }
+
+  // local_sum: buffer 0 += buffer g, then every buffer = buffer 0, on
+  // streams[0] once every shard's streams[g] has reached this point; the
+  // other streams then wait for the sum
+  void local_reduce(const std::vector<void*>& ptr, size_t count, const std::vector<hipStream_t>& streams) {
+    const size_t G = ctx.size();
+    hip_check(hipSetDevice(dev[0]), "hipSetDevice");
+    for (size_t g = 1; g < G; ++g) {
+      hip_check(hipEventRecord(sum_events[g], streams[g]), "hipEventRecord");
+      hip_check(hipStreamWaitEvent(streams[0], sum_events[g], 0), "hipStreamWaitEvent");
+    }
+    const int64_t n4 = (int64_t)count / 4;   // V*Kp + Kp: a multiple of 4 (Kp % 64 == 0)
+    const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>((n4 + 255) / 256, 4096));
+    for (size_t g = 1; g < G; ++g) {
+      hipLaunchKernelGGL(k_sum_into, dim3(blocks), dim3(256), 0, streams[0], static_cast<int4*>(ptr[0]),
+                         static_cast<const int4*>(ptr[g]), n4);
+      hip_check(hipGetLastError(), "k_sum_into");
+    }
+    for (size_t g = 1; g < G; ++g)
+      hip_check(hipMemcpyAsync(ptr[g], ptr[0], count * sizeof(int32_t), hipMemcpyDeviceToDevice, streams[0]),
+                "hipMemcpyAsync");
+    hip_check(hipEventRecord(sum_events[0], streams[0]), "hipEventRecord");
+    for (size_t g = 1; g < G; ++g) hip_check(hipStreamWaitEvent(streams[g], sum_events[0], 0), "hipStreamWaitEvent");
   }
 
   hipStream_t stream(size_t g) {
@@ -89,6 +193,10 @@ class ShardGroup {
     size_t count = 0;
     for (size_t g = 0; g < ctx.size(); ++g)
       check(lda_delta_buffer_part(ctx[g], part, &ptr[g], &count), "lda_delta_buffer_part");
+    if (local_sum) {
+      local_reduce(ptr, count, streams);
+      return;
+    }
     ncclResult_t r = ncclGroupStart();
     for (size_t g = 0; g < ctx.size() && r == ncclSuccess; ++g)
       r = ncclAllReduce(ptr[g], ptr[g], count, ncclInt32, ncclSum, comms[g], streams[g]);
@@ -106,12 +214,13 @@ class ShardGroup {
 
   void set_parts(int p) {
     parts = ctx.size() < 2 ? 1 : p;   // nothing to overlap on one GPU
-    for (auto c : ctx) check(lda_set_exchange_parts(c, parts, parts > 1 ? 8 : 0), "lda_set_exchange_parts");
+    // reserve_cus < 0: the library's default share of CUs left to the collective
+    for (auto c : ctx) check(lda_set_exchange_parts(c, parts, parts > 1 ? -1 : 0), "lda_set_exchange_parts");
     if (parts > 1 && comm_streams.empty()) {
       comm_streams.resize(ctx.size());
       events.resize(ctx.size());
       for (size_t g = 0; g < ctx.size(); ++g) {
-        if (hipSetDevice((int)g) != hipSuccess ||
+        if (hipSetDevice(dev[g]) != hipSuccess ||
             hipStreamCreateWithFlags(&comm_streams[g], hipStreamNonBlocking) != hipSuccess ||
             hipEventCreateWithFlags(&events[g], hipEventDisableTiming) != hipSuccess)
           raise(LDA_ERR_DEVICE, "collective stream");
@@ -135,14 +244,14 @@ class ShardGroup {
     for (int i = 0; i < parts; ++i) {
       for (size_t g = 0; g < ctx.size(); ++g) {
         check(lda_sample_part(ctx[g], i), "lda_sample_part");
-        hip(hipSetDevice((int)g), "hipSetDevice");
+        hip(hipSetDevice(dev[g]), "hipSetDevice");
         hip(hipEventRecord(events[g], st[g]), "hipEventRecord");           // part i sampled
         hip(hipStreamWaitEvent(comm_streams[g], events[g], 0), "hipStreamWaitEvent");
       }
       reduce_part(i, comm_streams);
     }
     for (size_t g = 0; g < ctx.size(); ++g) {
-      hip(hipSetDevice((int)g), "hipSetDevice");
+      hip(hipSetDevice(dev[g]), "hipSetDevice");
       hip(hipEventRecord(events[g], comm_streams[g]), "hipEventRecord");   // every sum landed
       hip(hipStreamWaitEvent(st[g], events[g], 0), "hipStreamWaitEvent");
     }
@@ -216,6 +325,17 @@ void ParallelTopicModel::setNumThreads(int32_t n) {
   num_threads_ = n;
 }
 
+void ParallelTopicModel::setDevices(const int32_t* devices, int32_t n) {
+  if (n < 0 || (n > 0 && !devices)) raise(LDA_ERR_INVALID_ARG, "setDevices: bad argument");
+  devices_.assign(devices, devices + n);
+  markDirty();
+}
+
+int32_t ParallelTopicModel::numShards() {
+  ensureShards();
+  return (int32_t)shards_->ctx.size();
+}
+
 void ParallelTopicModel::setExchangeParts(int32_t parts) {
   if (parts < 1 || parts > LDA_MAX_EXCHANGE_PARTS) raise(LDA_ERR_INVALID_ARG, "parts out of range");
   exchange_parts_ = parts;
@@ -273,8 +393,13 @@ void ParallelTopicModel::ensureShards() {
   const int64_t D = numDocs(), N = numTokens();
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev < 1) raise(LDA_ERR_DEVICE, "no HIP device");
-  const int G = (int)std::max<int64_t>(1, std::min<int64_t>({(int64_t)num_threads_, (int64_t)ndev, std::max<int64_t>(D, 1)}));
+  // explicit placement (setDevices) or setNumThreads' plan
+  const int G = devices_.empty() ? plan_shards(num_threads_, ndev, N, V_, K_, D)
+                                 : (int)std::min<int64_t>((int64_t)devices_.size(), std::max<int64_t>(D, 1));
+  for (int32_t d : devices_)
+    if (d < 0 || d >= ndev) raise(LDA_ERR_INVALID_ARG, "setDevices: device ordinal out of range");
   auto sg = std::make_unique<ShardGroup>();
+  for (int g = 0; g < G; ++g) sg->dev.push_back(devices_.empty() ? g : devices_[(size_t)g]);
   // token-balanced contiguous document ranges (the cuts Mallet makes by
   // document count; tokens balance the GPUs' work)
   sg->doc_begin.push_back(0);
@@ -294,7 +419,7 @@ void ParallelTopicModel::ensureShards() {
     cfg.alpha = alpha_.data();
     cfg.beta = beta_;
     cfg.seed = seed_;
-    cfg.device = g;
+    cfg.device = sg->dev[(size_t)g];
     cfg.sampler = sampler_;
     cfg.token_base = doc_off_[d0];
     cfg.tokens_per_range = 0;
@@ -315,16 +440,7 @@ void ParallelTopicModel::ensureShards() {
       check(lda_set_z(sg->ctx[g], z.data()), "lda_set_z");
     }
   }
-  if (G > 1) {
-    std::vector<int> devs(G);
-    std::iota(devs.begin(), devs.end(), 0);
-    sg->comms.resize(G);
-    const ncclResult_t r = ncclCommInitAll(sg->comms.data(), G, devs.data());
-    if (r != ncclSuccess) {
-      sg->comms.clear();
-      raise(LDA_ERR_DEVICE, std::string("ncclCommInitAll: ") + ncclGetErrorString(r));
-    }
-  }
+  sg->init_exchange();
   // the shards' local counts are the pending delta: sum them, apply
   sg->reduce();
   sg->apply();
@@ -827,6 +943,21 @@ TM_SETTER(ldatm_set_symmetric_alpha, setSymmetricAlpha(n != 0))
 TM_SETTER(ldatm_set_num_threads, setNumThreads(n))
 TM_SETTER(ldatm_set_sampler, setSampler(n))
 TM_SETTER(ldatm_set_exchange_parts, setExchangeParts(n))
+
+lda_status ldatm_set_devices(ldatm* m, int32_t n, const int32_t* devices) {
+  TM_CHECK(m);
+  return guard([&] { m->model.setDevices(devices, n); });
+}
+
+lda_status ldatm_num_shards(ldatm* m, int32_t* shards) {
+  TM_CHECK(m && shards);
+  return guard([&] { *shards = m->model.numShards(); });
+}
+
+int32_t ldatm_plan_shards(int32_t num_threads, int32_t num_devices, int64_t num_tokens,
+                          int32_t num_types, int32_t num_topics, int64_t num_docs) {
+  return lda_host::plan_shards(num_threads, num_devices, num_tokens, num_types, num_topics, num_docs);
+}
 TM_SETTER(ldatm_set_verbosity, setVerbosity(n))
 TM_SETTER(ldatm_set_print_log_likelihood, setPrintLogLikelihood(n != 0))
 

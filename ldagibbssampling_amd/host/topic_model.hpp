@@ -23,6 +23,10 @@ struct Error {
 
 class ShardGroup;  // GPU shards + their all-reduce (topic_model.cpp)
 
+// GPU shards for setNumThreads(num_threads) over this corpus (ldatm_plan_shards)
+int32_t plan_shards(int32_t num_threads, int32_t num_devices, int64_t num_tokens, int32_t num_types,
+                    int32_t num_topics, int64_t num_docs);
+
 class ParallelTopicModel {
  public:
   ParallelTopicModel(int32_t num_topics, double alpha_sum, double beta);
@@ -51,6 +55,11 @@ class ParallelTopicModel {
   // split sweeps across GPU shards: each shard's sweep in `parts` parts, part
   // i's all-reduce overlapping part i+1's sampling (1 = one exchange per sweep)
   void setExchangeParts(int32_t parts);
+  // explicit shard placement: shard g on devices[g] (n shards; n = 0 returns
+  // to setNumThreads' plan).  Shards that share one device exchange through a
+  // device-side sum instead of RCCL (the multi-shard path on one GPU).
+  void setDevices(const int32_t* devices, int32_t n);
+  int32_t numShards();
   void setVerbosity(int32_t v) { verbosity_ = v; }
   // state a Java-side ParallelTopicModel already holds (GpuParallelTopicModel:
   // Mallet's own addInstances topics, alpha/beta optimised in an earlier
@@ -116,6 +125,7 @@ class ParallelTopicModel {
   uint64_t seed_ = 0;
   int32_t num_threads_ = 1, sampler_ = LDA_SAMPLER_DENSE, verbosity_ = 0, exchange_parts_ = 1;
 
+  std::vector<int32_t> devices_;  // setDevices (empty: plan_shards)
   std::unique_ptr<ShardGroup> shards_;
   bool shards_dirty_ = true;
   int32_t max_doc_len_ = -1;

@@ -51,6 +51,9 @@ TM_SIGNATURES = {
     "ldatm_set_num_threads": (_i32, [_vp, _i32]),
     "ldatm_set_sampler": (_i32, [_vp, _i32]),
     "ldatm_set_exchange_parts": (_i32, [_vp, _i32]),
+    "ldatm_set_devices": (_i32, [_vp, _i32, _vp]),
+    "ldatm_num_shards": (_i32, [_vp, C.POINTER(_i32)]),
+    "ldatm_plan_shards": (_i32, [_i32, _i32, C.c_int64, _i32, _i32, C.c_int64]),
     "ldatm_set_topics": (_i32, [_vp, C.c_int64, _vp]),
     "ldatm_set_hyper": (_i32, [_vp, _vp, C.c_double, C.c_double]),
     "ldatm_get_sweep": (_i32, [_vp, C.POINTER(C.c_uint32)]),
@@ -282,6 +285,19 @@ class ParallelTopicModel:
         """Split sweeps across GPU shards (exchange overlapped with sampling)."""
         _check(self._L.ldatm_set_exchange_parts(self._h, int(parts)), "setExchangeParts")
 
+    def setDevices(self, devices):
+        """Explicit shard placement: shard g on HIP device devices[g] (an empty
+        list returns to setNumThreads' plan).  Shards that all share one device
+        exchange through a device-side sum (the multi-shard path on one GPU)."""
+        d = np.ascontiguousarray(list(devices), dtype=np.int32)
+        _check(self._L.ldatm_set_devices(self._h, len(d), d.ctypes.data if len(d) else None),
+               "setDevices")
+
+    def numShards(self) -> int:
+        n = C.c_int32()
+        _check(self._L.ldatm_num_shards(self._h, C.byref(n)), "numShards")
+        return n.value
+
     # --------------------------------------------------------- training
     def estimate(self):
         _check(self._L.ldatm_estimate(self._h), "estimate")
@@ -411,3 +427,11 @@ class TopicInferencer:
         if not isinstance(instance, Instance):
             instance = Instance(instance)
         return self.getSampledDistributions([instance], numIterations, thinning, burnIn, seed)[0]
+
+
+def plan_shards(num_threads: int, num_devices: int, num_tokens: int, num_types: int,
+                num_topics: int, num_docs: int) -> int:
+    """GPU shards setNumThreads(num_threads) becomes for this corpus
+    (ldatm_plan_shards; host-only)."""
+    return int(load_tm().ldatm_plan_shards(int(num_threads), int(num_devices), int(num_tokens),
+                                           int(num_types), int(num_topics), int(num_docs)))

@@ -1,24 +1,35 @@
 """Held-out perplexity: the GPU sampler vs the Mallet 2.0.7 restatement
-(cpu_mallet), 1000 sweeps, seeds {1, 2, 3}, optimizeInterval = 0 on both.
+(cpu_mallet), 1000 sweeps, optimizeInterval = 0 on both.
 
 Estimator (the same for both trained states): document completion.  10% of
 the documents are held out; each held-out document's first floor(L/2) tokens
 are observed, theta is inferred against the frozen model with the GPU
 TopicInferencer analogue (lda_infer: 100 iterations, burn-in 10, thinning 10
-— the reference's getSampledDistribution(inst, 100, 10, 10),
+-- the reference's getSampledDistribution(inst, 100, 10, 10),
 src/cmu_ron/TrainAndPredict.java:144), and the other half is scored:
 perplexity = exp(-sum log sum_k theta_dk phi_kw / N_scored).
-The Mallet state is evaluated by loading its z into a GPU context.
 
-Tolerance: |median_gpu - median_mallet| <= 1% of median_mallet over seeds
-1..12 (BASELINE.json north_star).  The median, not the mean of a few seeds:
-the posterior is multimodal, and about one seed in six ends in a local
-optimum 5-12% worse in EVERY implementation -- cpu_mallet seeds 10 and 12,
-the full-wave kernel's 4 and 10, the quarter-wave kernel's 1, 4, 6 and 10 at
-K=20 (profiles/r02/quarter/ppl_k20.json, tools/perplexity_seeds.py) -- so a
-three-seed mean measures which seeds fell into one, not the sampler.  Parity with Mallet itself is unpinned (Mallet cannot run in
-this image); cpu_mallet is its restatement.
+The posterior is multimodal: at K=20 about 30% of seeds end in a local
+optimum 5-12% worse, in cpu_mallet (28 of 96 seeds) as in the GPU kernels,
+so a few seeds measure which seeds fell in, not the sampler.  The GPU leg
+runs SEEDS = 1..96 here; cpu_mallet's 96 per-seed values are the committed
+fixture tests/golden/mallet_ppl_k{K}.json (tools/ppl_mallet_seeds.py: the
+restatement trained on the CPU with 4 threads, scored by cpu_exact with the
+same estimator and the GPU default kernel's inference draw).  Bars, each
+against cpu_mallet (profiles/r03/ppl/ has the per-seed evidence and
+bootstrap CIs, tools/ppl_stats.py):
+  1. mean over the 96 seeds within 1% (north_star's tolerance);
+  2. median within 0.5%: a +1% shift of the typical (untrapped) chain fails
+     this bar with certainty (the median's bootstrap CI is ~+-0.1%);
+  3. trapped-seed rate (perplexity > 1.02 x the pooled median) not larger
+     than cpu_mallet's at one-sided Fisher p < 0.01: a mean shift carried by
+     more trapped seeds is caught here or by bar 1.
+Parity with Mallet itself is unpinned (Mallet cannot run in this image);
+cpu_mallet is its restatement.
 """
+import json
+import os
+
 import numpy as np
 import pytest
 
@@ -48,34 +59,48 @@ def _perplexity(sampler, held_obs, held_sc, oracle):
     return float(np.exp(-ll / held_sc.num_tokens))
 
 
-@pytest.mark.parametrize("K,alpha_sum,beta", [(20, 10.0, 0.01), (100, 10.0, 0.01)])
-def test_heldout_perplexity_within_1pct(oracle, K, alpha_sum, beta):
-    from ldagibbssampling_amd.corpus import synthetic_lda, document_completion_split
+SEEDS = range(1, 97)
+TRAP = 1.02
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def mallet_fixture(K):
+    with open(os.path.join(GOLDEN, f"mallet_ppl_k{K}.json")) as f:
+        d = json.load(f)
+    assert (d["K"], d["alpha_sum"], d["beta"], d["sweeps"]) == (K, ALPHA_SUM, BETA, 1000)
+    return np.asarray(d["perplexity"])
+
+
+def parity_bars(pg, pm):
+    """(mean rel diff, median rel diff, one-sided Fisher p of more trapped
+    seeds) of the GPU values pg against cpu_mallet's pm."""
+    from scipy.stats import fisher_exact
+    pg, pm = np.asarray(pg), np.asarray(pm)
+    thr = TRAP * np.median(np.concatenate([pg, pm]))
+    a, b = int((pg > thr).sum()), int((pm > thr).sum())
+    p = fisher_exact([[a, len(pg) - a], [b, len(pm) - b]], alternative="greater")[1]
+    return pg.mean() / pm.mean() - 1, np.median(pg) / np.median(pm) - 1, float(p), a, b
+
+
+@pytest.mark.parametrize("K", [20, 100])
+def test_heldout_perplexity_within_1pct(oracle, K):
     from ldagibbssampling_amd.sampler import GibbsSampler
-    c = synthetic_lda(num_docs=2200, num_types=3000, num_topics=K, doc_len=None, mean_len=80,
-                      min_len=10, max_len=300, seed=20261015, k_true=min(K, 50))
-    rng = np.random.default_rng(0)
-    perm = rng.permutation(c.num_docs)
-    n_held = c.num_docs // 10
-    train = c.subset(np.sort(perm[n_held:]))
-    held_obs, held_sc = document_completion_split(c.subset(np.sort(perm[:n_held])))
-    alpha = np.full(K, alpha_sum / K)
-    pg, pm = [], []
-    for seed in range(1, 13):
-        g = GibbsSampler(K, c.num_types, train.doc_off, train.words, alpha, beta, seed=seed)
+    c, train, held_obs, held_sc = _corpus_split(K)
+    alpha = np.full(K, ALPHA_SUM / K)
+    pg = []
+    for seed in SEEDS:
+        g = GibbsSampler(K, c.num_types, train.doc_off, train.words, alpha, BETA, seed=seed)
         g.sweep(1000)
         pg.append(_perplexity(g, held_obs, held_sc, oracle))
-        m = oracle.MalletModel(K, alpha_sum, beta, c.num_types, train.doc_off, train.words,
-                               seed=seed, num_threads=4)
-        m.estimate(1000)
-        gm = GibbsSampler(K, c.num_types, train.doc_off, train.words, alpha, beta, seed=seed,
-                          z_init=m.z())
-        gm.sweep(0)
-        pm.append(_perplexity(gm, held_obs, held_sc, oracle))
-    mg, mm = float(np.median(pg)), float(np.median(pm))
-    print(f"K={K}: gpu {pg} median {mg:.3f} | cpu_mallet {pm} median {mm:.3f} | "
-          f"rel diff {(mg - mm) / mm:+.4%}")
-    assert abs(mg - mm) <= 0.01 * mm
+        g.close()
+    pm = mallet_fixture(K)
+    dmean, dmed, p, a, b = parity_bars(pg, pm)
+    print(f"K={K}: gpu mean {np.mean(pg):.3f} median {np.median(pg):.3f} trapped {a}/{len(pg)} | "
+          f"cpu_mallet mean {pm.mean():.3f} median {np.median(pm):.3f} trapped {b}/{len(pm)} | "
+          f"mean {dmean:+.3%} median {dmed:+.3%} Fisher p {p:.3f}")
+    assert abs(dmean) <= 0.01
+    assert abs(dmed) <= 0.005
+    assert p >= 0.01
 
 
 def _corpus_split(K):

@@ -120,3 +120,22 @@ def test_checkpoint_round_trip_without_gpu(L, tmp_path):
     trunc.write_bytes(p.read_bytes()[:60])
     with pytest.raises(capi.LdaError):
         tm.ParallelTopicModel.load(str(trunc))
+
+
+def test_shard_plan():
+    """setNumThreads -> GPU shards (ldatm_plan_shards): capped by the devices
+    and the documents, and one GPU when the sweep is shorter than the
+    exchange (the reference's C1 corpus with setNumThreads(4))."""
+    from ldagibbssampling_amd.topic_model import plan_shards
+    # C1 at src/cmu_ron's K = 500 and src/cmu's K = 100, 8 GPUs visible
+    assert plan_shards(4, 8, 16_000, 5_000, 500, 2_000) == 1
+    assert plan_shards(4, 8, 16_000, 5_000, 100, 2_000) == 1
+    # C4 (2e9 tokens, V = 100k, K = 512): every GPU asked for
+    assert plan_shards(4, 8, 2_000_000_000, 100_000, 512, 10_000_000) == 4
+    assert plan_shards(8, 8, 2_000_000_000, 100_000, 512, 10_000_000) == 8
+    assert plan_shards(8, 2, 2_000_000_000, 100_000, 512, 10_000_000) == 2
+    # never more shards than documents, at least one
+    assert plan_shards(4, 8, 2_000_000_000, 100_000, 512, 3) == 3
+    assert plan_shards(0, 8, 10, 10, 10, 0) == 1
+    # C2 (2e7 tokens, V = 50k, K = 128): worth two GPUs or more
+    assert plan_shards(4, 8, 20_000_000, 50_000, 128, 100_000) >= 2

@@ -227,3 +227,50 @@ def test_checkpoint_resume_is_bit_exact(tmp_path):
     np.testing.assert_array_equal(r.alpha, m.alpha)
     assert r.beta == m.beta
     assert r.modelLogLikelihood() == m.modelLogLikelihood()
+
+
+@pytest.mark.parametrize("kind", ["dense", "sparse"])
+@pytest.mark.parametrize("shards,parts", [(2, 1), (3, 1), (2, 2), (3, 3)])
+def test_shard_group_on_one_device(oracle, shards, parts, kind):
+    """ShardGroup with G > 1 on the one GPU of the box (setDevices([0]*G)):
+    per-shard contexts, the exchange (a device-side sum standing in for
+    RCCL's), per-part events and collective streams in split sweeps, the
+    apply ordering -- with optimisation on, bit-exact against one context and
+    the oracle schedule (src/cmu_ron/TrainAndPredict.java:164, setNumThreads)."""
+    c = synthetic_lda(num_docs=240, num_types=700, num_topics=12, doc_len=None, mean_len=50,
+                      min_len=0, max_len=160, seed=13)
+    K = 16 if kind == "dense" else 1100
+    iters, interval, burnin, save = 30, 10, 10, 5
+    m, _ = _model(c, K, 8.0, 0.05, 3, setNumIterations=iters, setOptimizeInterval=interval,
+                  setBurninPeriod=burnin, setSaveSampleInterval=save)
+    m.setSampler(kind)
+    m.setDevices([0] * shards)
+    m.setExchangeParts(parts)
+    assert m.numShards() == shards
+    m.estimate()
+    o, alpha, alpha_sum, beta, ll = _oracle_estimate(oracle, c, K, 8.0, 0.05, 3, iters, interval,
+                                                     burnin, save)
+    if kind == "dense":      # the sparse draw is a different fp32 sum: the oracle above is dense
+        np.testing.assert_array_equal(m.topicAssignments(), o.z())
+        np.testing.assert_array_equal(m.alpha, alpha)
+        assert m.beta == beta
+    single, _ = _model(c, K, 8.0, 0.05, 3, setNumIterations=iters, setOptimizeInterval=interval,
+                       setBurninPeriod=burnin, setSaveSampleInterval=save)
+    single.setSampler(kind)
+    single.estimate()
+    assert single.numShards() == 1
+    np.testing.assert_array_equal(m.topicAssignments(), single.topicAssignments())
+    for a, b in zip(m.typeTopicCounts(), single.typeTopicCounts()):
+        np.testing.assert_array_equal(a, b)
+    np.testing.assert_array_equal(m.alpha, single.alpha)
+    assert m.beta == single.beta
+    np.testing.assert_allclose([v for _, v in m.llTrace()], [v for _, v in single.llTrace()], rtol=1e-12)
+
+
+def test_num_threads_at_reference_scale_uses_one_gpu():
+    """setNumThreads(4) (src/cmu_ron/TrainAndPredict.java:164) on the
+    reference's own corpus scale (C1: 2000 changelist docs, ~16k tokens) at
+    its K = 500: one GPU -- the sweep is far shorter than an exchange."""
+    c = synthetic_changelists(num_docs=2000, num_types=5000, seed=20261015)
+    m, _ = _model(c, 500, 100.0, 1.0, 1, setNumThreads=4, setNumIterations=1)
+    assert m.numShards() == 1

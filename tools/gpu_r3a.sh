@@ -7,8 +7,12 @@ O=gpurun_out/r3a; mkdir -p $O
 export TMPDIR=/tmp
 timeout -k 10 900 python -u -m pytest -x -v --timeout 300 --timeout-method thread \
   tests/test_recount_gpu.py tests/test_parity_gpu.py tests/test_configs_gpu.py tests/test_exchange_gpu.py \
-  tests/test_distributed_gpu.py tests/test_abi_guard.py > $O/pytest.log 2>&1 || { echo "PYTEST FAILED"; tail -30 $O/pytest.log; exit 1; }
+  tests/test_distributed_gpu.py tests/test_abi_guard.py tests/test_topic_model_gpu.py tests/test_jni_harness_gpu.py > $O/pytest.log 2>&1 || { echo "PYTEST FAILED"; tail -30 $O/pytest.log; exit 1; }
 tail -3 $O/pytest.log
+for K in 20 100; do
+  timeout -k 10 400 python tools/ppl_gpu_seeds.py $K 1 96 2,0 > $O/ppl_gpu_k$K.json 2> $O/ppl_gpu_k$K.err || { echo "PPL $K FAILED"; tail -5 $O/ppl_gpu_k$K.err; exit 1; }
+  cat $O/ppl_gpu_k$K.err
+done
 for cfg in c2 c3 c4; do
   for b in 0 30; do
     for m in 1 0; do
