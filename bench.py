@@ -338,9 +338,13 @@ def main():
     assert len(ks) == min(args.steps * parts, 256)
     # a split sweep is `parts` launches: the sampler's time per sweep is their sum
     kern_ms = float(np.mean(ks)) * parts
-    # the dense samplers' recount kernel after each launch (0 in the delta mode)
+    # the dense samplers' recount kernel after each launch of a recounting
+    # sweep (lda_set_count_update: AUTO recounts the first sweeps of a small
+    # corpus); the delta sweeps launch none
     rc = sampler.recount_times(args.steps * parts)
-    recount_ms = float(np.mean(rc)) * parts if sampler.recount else None
+    n_rc = int((rc > 0.002).sum())
+    recount_ms = float(rc[rc > 0.002].mean()) * parts if n_rc else None
+    count_mode = sampler.count_update()
     copy_gbs = stream_copy_gbs(device) if rank == 0 else None
 
     t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{device}")
@@ -430,9 +434,11 @@ def main():
                 "bytes_per_token": enc,
                 "bytes_model": enc_model,
                 "kernel_ms_timed_region": kern_ms,
-                "count_update": ("recount (the sampler writes z; k_recount rebuilds the shard's "
-                                 "rows from a word-sorted token index)" if sampler.recount else
-                                 "delta (device atomics per changed token)"),
+                "count_update": {"mode": count_mode[0], "recount_sweeps": count_mode[1],
+                                 "timed_launches_recounted": n_rc,
+                                 "model": "recount: the sampler writes z, k_recount rebuilds the "
+                                          "shard's rows from a word-sorted token index; delta: "
+                                          "device atomics per changed token"},
                 "recount_ms_timed_region": recount_ms,
                 "measured_copy_gbs": copy_gbs,
                 # the bandwidth the kernel really moves (PMC bytes / its time)

@@ -109,8 +109,28 @@ lda_status lda_sample(lda_ctx* ctx);
  * DELTA of the shard's changes, which lda_apply adds.  Either way the caller
  * only sums it, and lda_apply leaves it zero. */
 lda_status lda_delta_buffer(lda_ctx* ctx, void** dev_ptr, size_t* count);
-/* recount = 1 when the buffer holds counts, 0 when it holds a delta. */
+/* recount = 1 when the pending buffer holds counts (or, with nothing
+ * pending, when the next sweep will recount), 0 for a delta. */
 lda_status lda_count_update_mode(lda_ctx* ctx, int32_t* recount);
+/* Which sweeps recount (dense samplers; the sparse ones always keep a delta).
+ *  LDA_COUNT_AUTO     the first recount_sweeps sweeps after the counts are
+ *                     (re)seeded by lda_create / lda_set_z recount, later
+ *                     ones keep a delta (near init nearly every token
+ *                     changes, and the delta's device atomics cost more than
+ *                     the recount; later they cost less).  The default is
+ *                     LDA_RECOUNT_SWEEPS_DEFAULT when the shard's z fits the
+ *                     Infinity Cache (4 N <= 256 MiB), else 0.
+ *                     recount_sweeps < 0 keeps the current value.
+ *  LDA_COUNT_RECOUNT  every sweep;  LDA_COUNT_DELTA  none.
+ * Shards exchanging buffers must agree on it sweep by sweep: a distributed
+ * driver sets the same mode and count on every rank (ADLDATrainer: the
+ * minimum over ranks).  Results are identical in every mode. */
+#define LDA_COUNT_AUTO 0
+#define LDA_COUNT_RECOUNT 1
+#define LDA_COUNT_DELTA 2
+#define LDA_RECOUNT_SWEEPS_DEFAULT 10
+lda_status lda_set_count_update(lda_ctx* ctx, int32_t mode, int32_t recount_sweeps);
+lda_status lda_get_count_update(lda_ctx* ctx, int32_t* mode, int32_t* recount_sweeps);
 /* nw/nwsum := buffer (recount) or += buffer (delta), buffer = 0, refresh the
  * per-topic tables. */
 lda_status lda_apply(lda_ctx* ctx);

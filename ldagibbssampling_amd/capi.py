@@ -29,6 +29,7 @@ MAX_TOPICS_DENSE = 1024
 MAX_DOC_TOKENS_BIGK = 65535
 MAX_EXCHANGE_PARTS = 4
 SAMPLERS = {"dense": 0, "sparse": 1}
+COUNT_UPDATE = {"auto": 0, "recount": 1, "delta": 2}
 
 
 class LdaError(RuntimeError):
@@ -101,6 +102,8 @@ SIGNATURES = {
     "lda_philox_draws": (C.c_int32, [C.c_uint64, C.c_uint32, C.c_uint32, _vp, C.c_int64, _vp]),
     "lda_recount_times": (C.c_int32, [_vp, C.c_int32, _vp, C.POINTER(C.c_int32)]),
     "lda_count_update_mode": (C.c_int32, [_vp, C.POINTER(C.c_int32)]),
+    "lda_set_count_update": (C.c_int32, [_vp, C.c_int32, C.c_int32]),
+    "lda_get_count_update": (C.c_int32, [_vp, C.POINTER(C.c_int32), C.POINTER(C.c_int32)]),
     "lda_abi_version": (C.c_int32, []),
     "lda_debug_fail_host_alloc": (None, [C.c_int32]),
     "lda_last_error": (C.c_char_p, []),

@@ -171,8 +171,15 @@ struct lda_ctx {
   std::vector<int64_t> ranges_h;   // host copy of range_doc
   // dense samplers' recount: the sampler writes only z, then
   // every word row of the shard is recounted from a word-sorted token index
-  // into the exchange buffer, which then holds counts, not changes
-  bool recount = false;
+  // into the exchange buffer, which then holds counts, not changes.  Which
+  // sweeps recount: count_mode (LDA_COUNT_*) and, for AUTO, the first
+  // recount_sweeps sweeps since the counts were (re)seeded.
+  int count_mode = LDA_COUNT_AUTO;
+  int32_t recount_sweeps = 0;
+  int64_t sweeps_since_seed = 0;
+  bool sweep_recount = false;      // the sweep being sampled recounts
+  bool pending_absolute = false;   // the pending buffer holds counts (recount) rather than a delta
+  bool recount_ok = false;         // dense sampler, N < 2^32
   uint32_t* perm = nullptr;        // [N] token indices grouped by (part, word)
   int32_t* items = nullptr;        // int4 {word, first perm index, tokens, split} per work item
   std::vector<int64_t> part_item{0, 0};
@@ -290,7 +297,7 @@ static lda_status build_recount_index(lda_ctx* c) {
   c->perm = nullptr;
   c->items = nullptr;
   c->part_item.assign((size_t)c->parts + 1, 0);
-  if (!c->recount || c->N == 0) return LDA_OK;
+  if (!c->recount_ok || c->N == 0) return LDA_OK;
   lda::PartSpans ps{};
   ps.parts = c->parts;
   for (int i = 0; i <= c->parts; ++i)
@@ -353,7 +360,7 @@ static lda_status apply_impl(lda_ctx* c) {
   if (c->sampler == LDA_SAMPLER_DENSE) {
     // one launch: apply, 16-bit rows, topic tables, queue reset (k_apply_packed)
     lda::TopicTables t{c->nwsum, c->alpha_d, c->alpha_f, c->inv, c->inv_m1,
-                       (float)((double)c->V * c->beta), c->K, c->queue, c->recount ? 1 : 0};
+                       (float)((double)c->V * c->beta), c->K, c->queue, c->pending_absolute ? 1 : 0};
     HIP_TRY(lda::launch_apply_packed(c->nw, c->delta, c->V, c->Kp, c->nw16, c->wide, t, c->stream));
     c->pending = false;
     return LDA_OK;
@@ -375,7 +382,15 @@ static lda_status apply_impl(lda_ctx* c) {
   return LDA_OK;
 }
 
-static lda_status recount_impl(lda_ctx* c) {
+// Will the next sweep recount?
+static bool next_sweep_recounts(const lda_ctx* c) {
+  if (!c->recount_ok) return false;
+  if (c->count_mode == LDA_COUNT_RECOUNT) return true;
+  if (c->count_mode == LDA_COUNT_DELTA) return false;
+  return c->sweeps_since_seed < c->recount_sweeps;
+}
+
+static lda_status reseed_counts(lda_ctx* c) {
   // local (word, topic) counts of this shard become the pending delta
   for (int i = 0; i < c->parts; ++i)
     HIP_TRY(hipMemsetAsync(c->delta_part[i], 0, sizeof(int32_t) * ((size_t)c->V * c->Kp + c->Kp), c->stream));
@@ -385,6 +400,8 @@ static lda_status recount_impl(lda_ctx* c) {
   HIP_TRY(lda::launch_count(c->words, c->z, c->N, c->Kp, c->delta, c->delta + (int64_t)c->V * c->Kp,
                             c->stream));
   c->pending = true;
+  c->pending_absolute = false;   // nw is zero: adding the local counts sets them
+  c->sweeps_since_seed = 0;
   return LDA_OK;
 }
 
@@ -489,10 +506,17 @@ lda_status lda_create(lda_ctx** out, const lda_config* cfg, const int64_t* doc_o
   }
   c->waves_per_block = lda::sample_waves_per_block(c->C, c->sampler == LDA_SAMPLER_SPARSE, c->half);
   {
-    // the dense samplers recount (LDA_RECOUNT=0 keeps the delta atomics, for
-    // A/B); the index is uint32, so the shard must hold < 2^32 tokens
+    // the dense samplers can recount (a uint32 index: < 2^32 tokens).  AUTO
+    // recounts the first LDA_RECOUNT_SWEEPS_DEFAULT sweeps when z fits the
+    // 256 MB Infinity Cache (the recount gathers z through the index: C2 near
+    // init 1.62 -> 1.43 ms per sweep; C4's 1 GB z makes the gathers cost more
+    // than the atomics they replace).  LDA_RECOUNT=0 / 1 forces
+    // the delta / recount mode (A/B runs).
+    c->recount_ok = c->sampler == LDA_SAMPLER_DENSE && N < (int64_t(1) << 32);
+    c->recount_sweeps = c->recount_ok && N * 4 <= (int64_t(256) << 20) ? LDA_RECOUNT_SWEEPS_DEFAULT : 0;
     const char* rv = std::getenv("LDA_RECOUNT");
-    c->recount = c->sampler == LDA_SAMPLER_DENSE && !(rv && rv[0] == '0') && N < (int64_t(1) << 32);
+    if (rv && rv[0] == '0') c->count_mode = LDA_COUNT_DELTA;
+    if (rv && rv[0] == '1') c->count_mode = LDA_COUNT_RECOUNT;
     c->recount_blocks = 8 * c->cus;
   }
   const int64_t waves = (int64_t)c->sample_blocks * c->waves_per_block;
@@ -511,7 +535,7 @@ lda_status lda_create(lda_ctx** out, const lda_config* cfg, const int64_t* doc_o
   CT(dalloc(&c->z, N));
   CT(dalloc(&c->doc_off, D + 1));
   CT(dalloc(&c->range_doc, ranges.size()));
-  CT(dalloc(&c->queue, 2 * LDA_MAX_EXCHANGE_PARTS));   // sampler and recount counters per part
+  CT(dalloc(&c->queue, LDA_MAX_EXCHANGE_PARTS));
   CT(dalloc(&c->nw, (size_t)c->V * c->Kp));
   CT(dalloc(&c->nwsum, c->Kp));
   if (c->sampler == LDA_SAMPLER_DENSE) {
@@ -531,7 +555,7 @@ lda_status lda_create(lda_ctx** out, const lda_config* cfg, const int64_t* doc_o
     CT(hipEventCreate(&c->ev1[i]));
     CT(hipEventCreate(&c->ev2[i]));
   }
-  CT(hipMemsetAsync(c->queue, 0, sizeof(int32_t) * 2 * LDA_MAX_EXCHANGE_PARTS, c->stream));
+  CT(hipMemsetAsync(c->queue, 0, sizeof(int32_t) * LDA_MAX_EXCHANGE_PARTS, c->stream));
 
   if (N > 0) CT(hipMemcpyAsync(c->words, words, sizeof(int32_t) * N, hipMemcpyHostToDevice, c->stream));
   CT(hipMemcpyAsync(c->doc_off, off.data(), sizeof(int64_t) * (D + 1), hipMemcpyHostToDevice, c->stream));
@@ -545,8 +569,9 @@ lda_status lda_create(lda_ctx** out, const lda_config* cfg, const int64_t* doc_o
                           (uint32_t)(c->seed >> 32), c->stream));
   }
   {
-    lda_status s = recount_impl(c);
-    if (s == LDA_OK) s = build_recount_index(c);
+    lda_status s = reseed_counts(c);
+    if (s == LDA_OK && (c->recount_sweeps > 0 || c->count_mode == LDA_COUNT_RECOUNT))
+      s = build_recount_index(c);
     if (s != LDA_OK) return bail(s);
   }
   CT(hipMemsetAsync(c->alpha_f, 0, sizeof(float) * c->Kp, c->stream));
@@ -625,6 +650,13 @@ static lda_status sample_part_impl(lda_ctx* c, int part) {
     return fail(LDA_ERR_STATE, "split sweep parts must be sampled in order 0, 1, ...");
   if (part == 0 && c->pending) return fail(LDA_ERR_STATE, "lda_sample with a pending delta: call lda_apply first");
   HIP_TRY(hipSetDevice(c->device));
+  if (part == 0) {
+    c->sweep_recount = next_sweep_recounts(c);
+    if (c->sweep_recount && !c->perm && c->N > 0) {
+      lda_status s = build_recount_index(c);
+      if (s) return s;
+    }
+  }
   const int64_t r0 = c->part_range[(size_t)part], r1 = c->part_range[(size_t)part + 1];
   if (r1 > r0) {
     // the dense sampler's apply (which every sample follows) zeroed queue[0]
@@ -634,8 +666,8 @@ static lda_status sample_part_impl(lda_ctx* c, int part) {
     p.range_doc = c->range_doc + r0;
     p.num_ranges = r1 - r0;
     p.queue = c->queue + part;
-    p.delta = c->recount ? nullptr : c->delta_part[part];   // recount: the sampler writes z only
-    p.dsum = c->recount ? nullptr : c->delta_part[part] + (int64_t)c->V * c->Kp;
+    p.delta = c->sweep_recount ? nullptr : c->delta_part[part];   // recount: the sampler writes z only
+    p.dsum = c->sweep_recount ? nullptr : c->delta_part[part] + (int64_t)c->V * c->Kp;
     const int64_t wpb = c->waves_per_block;
     // a split sweep leaves reserve_cus CUs' worth of sampler blocks free, so
     // the collective of the part before this one finds CUs to run on
@@ -650,14 +682,11 @@ static lda_status sample_part_impl(lda_ctx* c, int part) {
     else
       HIP_TRY(lda::launch_sample(c->C, false, p, blocks, c->stream, c->half));
     HIP_TRY(hipEventRecord(c->ev1[slot], c->stream));
-    if (c->recount) {
+    if (c->sweep_recount) {
       // this part's rows recounted into its exchange buffer (the apply left
-      // it zero and zeroed part 0's queue counter)
+      // it zero)
       const int64_t i0 = c->part_item[(size_t)part], i1 = c->part_item[(size_t)part + 1];
-      if (part > 0)
-        HIP_TRY(hipMemsetAsync(c->queue + lda::RECOUNT_QUEUE + part, 0, sizeof(int32_t), c->stream));
-      HIP_TRY(lda::launch_recount(c->Kp, c->perm, c->items + 4 * i0, (int32_t)(i1 - i0),
-                                  c->queue + lda::RECOUNT_QUEUE + part, c->z, c->delta_part[part],
+      HIP_TRY(lda::launch_recount(c->Kp, c->perm, c->items + 4 * i0, (int32_t)(i1 - i0), c->z, c->delta_part[part],
                                   c->delta_part[part] + (int64_t)c->V * c->Kp, c->recount_blocks,
                                   c->stream));
     }
@@ -665,9 +694,11 @@ static lda_status sample_part_impl(lda_ctx* c, int part) {
     c->launches++;
   }
   c->pending = true;  // the part buffers hold this sweep's changes
+  c->pending_absolute = c->sweep_recount;
   if (++c->next_part == c->parts) {
     c->next_part = 0;
     c->sweep++;
+    c->sweeps_since_seed++;
   }
   return LDA_OK;
 }
@@ -731,7 +762,7 @@ lda_status lda_set_exchange_parts(lda_ctx* c, int32_t parts, int32_t reserve_cus
   c->ranges_h = ranges;
   c->parts = parts;
   c->reserve_cus = reserve_cus;
-  return build_recount_index(c);
+  return c->perm ? build_recount_index(c) : LDA_OK;   // the index is per part
   });
 }
 
@@ -840,10 +871,29 @@ lda_status lda_recount_times(lda_ctx* c, int32_t max, float* ms, int32_t* n) {
   });
 }
 
+lda_status lda_set_count_update(lda_ctx* c, int32_t mode, int32_t recount_sweeps) {
+  if (!c) return fail(LDA_ERR_INVALID_ARG, "null ctx");
+  if (mode != LDA_COUNT_AUTO && mode != LDA_COUNT_RECOUNT && mode != LDA_COUNT_DELTA)
+    return fail(LDA_ERR_INVALID_ARG, "mode must be LDA_COUNT_AUTO, _RECOUNT or _DELTA");
+  if (c->next_part != 0) return fail(LDA_ERR_STATE, "inside a split sweep");
+  if (mode == LDA_COUNT_RECOUNT && !c->recount_ok)
+    return fail(LDA_ERR_UNSUPPORTED, "the recount needs the dense sampler and < 2^32 tokens");
+  c->count_mode = mode;
+  if (mode == LDA_COUNT_AUTO && recount_sweeps >= 0) c->recount_sweeps = c->recount_ok ? recount_sweeps : 0;
+  return LDA_OK;
+}
+
+lda_status lda_get_count_update(lda_ctx* c, int32_t* mode, int32_t* recount_sweeps) {
+  if (!c) return fail(LDA_ERR_INVALID_ARG, "null ctx");
+  if (mode) *mode = c->count_mode;
+  if (recount_sweeps) *recount_sweeps = c->recount_sweeps;
+  return LDA_OK;
+}
+
 lda_status lda_count_update_mode(lda_ctx* c, int32_t* recount) {
   return lda_abi::guarded([&]() -> lda_status {
   if (!c || !recount) return fail(LDA_ERR_INVALID_ARG, "null argument");
-  *recount = c->recount ? 1 : 0;
+  *recount = (c->pending ? c->pending_absolute : next_sweep_recounts(c)) ? 1 : 0;
   return LDA_OK;
   });
 }
@@ -892,7 +942,7 @@ lda_status lda_set_z(lda_ctx* c, const int32_t* z) {
     if (z[i] < 0 || z[i] >= c->K) return fail(LDA_ERR_INVALID_ARG, "topic out of range [0, K)");
   HIP_TRY(hipSetDevice(c->device));
   if (c->N > 0) HIP_TRY(hipMemcpyAsync(c->z, z, sizeof(int32_t) * c->N, hipMemcpyHostToDevice, c->stream));
-  lda_status s = recount_impl(c);
+  lda_status s = reseed_counts(c);
   if (s) return s;
   HIP_TRY(hipStreamSynchronize(c->stream));
   return LDA_OK;

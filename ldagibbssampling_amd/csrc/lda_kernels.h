@@ -73,9 +73,6 @@ struct SampleParams {
   const uint8_t* wide;      // [V] 1 when the row holds a count > 65535 (read nw)
 };
 
-// The recount's work-queue counter of part i is queue[RECOUNT_QUEUE + i]
-// (the sampler's is queue[i]).
-constexpr int RECOUNT_QUEUE = 4;
 // Tokens [tok[i], tok[i+1]) of a shard belong to exchange part i.
 struct PartSpans {
   int64_t tok[5];
@@ -116,8 +113,7 @@ struct TopicTables {
   float* inv_m1;            // [Kp]
   float vbeta;              // (float)(V * beta)
   int32_t K;
-  int32_t* queue;           // work-queue counters zeroed for the next sample and recount
-                            // (queue[0], queue[RECOUNT_QUEUE]; nullable)
+  int32_t* queue;           // work-queue counter zeroed for the next sample (nullable)
   int32_t absolute;         // 1: the buffer holds recounted counts that replace nw / nwsum
 };
 // dense sampler's apply: nw += delta, delta = 0, 16-bit rows + wide flags,
@@ -130,8 +126,7 @@ hipError_t launch_word_hist(const int32_t* words, int64_t n, const PartSpans& ps
 hipError_t launch_word_scatter(const int32_t* words, int64_t n, const PartSpans& ps, int64_t V,
                                uint32_t* cursor, uint32_t* perm, hipStream_t st);
 hipError_t launch_recount(int32_t Kp, const uint32_t* perm, const int32_t* items, int32_t n_items,
-                          int32_t* queue, const int32_t* z, int32_t* buf, int32_t* bufsum, int blocks,
-                          hipStream_t st);
+                          const int32_t* z, int32_t* buf, int32_t* bufsum, int blocks, hipStream_t st);
 hipError_t launch_philox_draws(const int64_t* gtok, int64_t n, uint32_t c2, uint32_t c3, uint64_t seed,
                                uint32_t* out, hipStream_t st);
 hipError_t launch_init_z(int32_t* z, int64_t n, int32_t K, int64_t token_base, uint32_t k0,

@@ -2380,7 +2380,7 @@ __global__ __launch_bounds__(256) void k_apply_packed(int32_t* __restrict__ nw, 
         t.inv_m1[k] = 0.0f;
       }
     }
-    if (t.queue && threadIdx.x < 2) t.queue[threadIdx.x * RECOUNT_QUEUE] = 0;
+    if (threadIdx.x == 0 && t.queue) *t.queue = 0;
   }
   for (int64_t w = (int64_t)blockIdx.x * 4 + wid; w < V; w += (int64_t)gridDim.x * 4) {
     int32_t c[C], d[C];
@@ -2710,10 +2710,12 @@ __global__ __launch_bounds__(256) void k_word_scatter(const int32_t* __restrict_
 // when the word is one item, added cell by cell (device atomics on the
 // nonzero cells) when it is split over several; the buffer is zero on entry
 // (k_apply_packed leaves it so).  The block's column sums go to bufsum.
+// Items are dealt to waves round-robin (they are sorted longest first): a
+// work-queue counter, one same-address atomic per item, had capped the
+// kernel at ~60M items/s (C2: 0.81 ms for 50k items).
 template <int C>
 __global__ __launch_bounds__(256) void k_recount(const uint32_t* __restrict__ perm,
                                                  const int4* __restrict__ items, int32_t n_items,
-                                                 int32_t* __restrict__ queue,
                                                  const int32_t* __restrict__ z,
                                                  int32_t* __restrict__ buf,
                                                  int32_t* __restrict__ bufsum) {
@@ -2724,11 +2726,7 @@ __global__ __launch_bounds__(256) void k_recount(const uint32_t* __restrict__ pe
   int32_t* bs = lds + 4 * KP;
   for (int i = threadIdx.x; i < 5 * KP; i += 256) lds[i] = 0;
   __syncthreads();
-  while (true) {
-    int it = 0;
-    if (lane == 0) it = atomicAdd(queue, 1);
-    it = uniform_i(__shfl(it, 0));
-    if (it >= n_items) break;
+  for (int it = (int)blockIdx.x * 4 + wid; it < n_items; it += (int)gridDim.x * 4) {
     const int4 m = items[it];
     const uint32_t b = (uint32_t)m.y;
     const int len = m.z;
@@ -3153,17 +3151,16 @@ hipError_t launch_word_scatter(const int32_t* words, int64_t n, const PartSpans&
 }
 
 hipError_t launch_recount(int32_t Kp, const uint32_t* perm, const int32_t* items, int32_t n_items,
-                          int32_t* queue, const int32_t* z, int32_t* buf, int32_t* bufsum, int blocks,
-                          hipStream_t st) {
+                          const int32_t* z, int32_t* buf, int32_t* bufsum, int blocks, hipStream_t st) {
   if (n_items <= 0) return hipSuccess;
   blocks = std::max(1, std::min(blocks, (n_items + 3) / 4));
   const int4* it = reinterpret_cast<const int4*>(items);
   switch (Kp / 64) {
-    case 1: hipLaunchKernelGGL(k_recount<1>, dim3(blocks), dim3(256), 0, st, perm, it, n_items, queue, z, buf, bufsum); break;
-    case 2: hipLaunchKernelGGL(k_recount<2>, dim3(blocks), dim3(256), 0, st, perm, it, n_items, queue, z, buf, bufsum); break;
-    case 4: hipLaunchKernelGGL(k_recount<4>, dim3(blocks), dim3(256), 0, st, perm, it, n_items, queue, z, buf, bufsum); break;
-    case 8: hipLaunchKernelGGL(k_recount<8>, dim3(blocks), dim3(256), 0, st, perm, it, n_items, queue, z, buf, bufsum); break;
-    case 16: hipLaunchKernelGGL(k_recount<16>, dim3(blocks), dim3(256), 0, st, perm, it, n_items, queue, z, buf, bufsum); break;
+    case 1: hipLaunchKernelGGL(k_recount<1>, dim3(blocks), dim3(256), 0, st, perm, it, n_items, z, buf, bufsum); break;
+    case 2: hipLaunchKernelGGL(k_recount<2>, dim3(blocks), dim3(256), 0, st, perm, it, n_items, z, buf, bufsum); break;
+    case 4: hipLaunchKernelGGL(k_recount<4>, dim3(blocks), dim3(256), 0, st, perm, it, n_items, z, buf, bufsum); break;
+    case 8: hipLaunchKernelGGL(k_recount<8>, dim3(blocks), dim3(256), 0, st, perm, it, n_items, z, buf, bufsum); break;
+    case 16: hipLaunchKernelGGL(k_recount<16>, dim3(blocks), dim3(256), 0, st, perm, it, n_items, z, buf, bufsum); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();

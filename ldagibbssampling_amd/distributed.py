@@ -129,8 +129,28 @@ class ADLDATrainer:
         evs[-1][1].synchronize()
         return sum(a.elapsed_time(b) for a, b in evs) / len(evs)
 
+    def _agree_count_update(self):
+        """Every rank must recount or keep a delta in the same sweeps (the
+        buffers they sum hold counts or changes accordingly): the same mode,
+        and for AUTO the smallest recount_sweeps of any rank."""
+        if self.world < 2 or not hasattr(self.engine, "count_update"):
+            return
+        import torch
+        from . import capi
+        mode, r = self.engine.count_update()
+        dev = self._delta.device if self.dist.get_backend(self.group) == "nccl" else "cpu"
+        t = torch.tensor([capi.COUNT_UPDATE[mode], -capi.COUNT_UPDATE[mode], r], dtype=torch.int64,
+                         device=dev)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MIN, group=self.group)
+        lo, hi, rmin = int(t[0]), -int(t[1]), int(t[2])
+        if lo != hi:
+            raise ValueError("ranks disagree on the count-update mode (lda_set_count_update)")
+        if mode == "auto" and rmin != r:
+            self.engine.set_count_update("auto", rmin)
+
     def init_counts(self):
         """Global nw/nwsum from every rank's local counts (addInstances)."""
+        self._agree_count_update()
         self._reduce()
         self.engine.apply()
         self._initialised = True

@@ -23,6 +23,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <climits>
 #include <cstdio>
 #include <cstring>
 #include <fstream>
@@ -441,6 +442,21 @@ void ParallelTopicModel::ensureShards() {
     }
   }
   sg->init_exchange();
+  if (G > 1) {
+    // shards recount (or keep a delta) in the same sweeps: the smallest
+    // AUTO recount count of any shard on all of them
+    int32_t rmin = INT32_MAX;
+    for (auto c : sg->ctx) {
+      int32_t mode = 0, r = 0;
+      check(lda_get_count_update(c, &mode, &r), "lda_get_count_update");
+      rmin = std::min(rmin, r);
+    }
+    for (auto c : sg->ctx) {
+      int32_t mode = 0;
+      check(lda_get_count_update(c, &mode, nullptr), "lda_get_count_update");
+      if (mode == LDA_COUNT_AUTO) check(lda_set_count_update(c, LDA_COUNT_AUTO, rmin), "lda_set_count_update");
+    }
+  }
   // the shards' local counts are the pending delta: sum them, apply
   sg->reduce();
   sg->apply();

@@ -180,6 +180,19 @@ class GibbsSampler:
                                              C.byref(n)), "lda_recount_times")
         return ms[:n.value]
 
+    def set_count_update(self, mode: str = "auto", recount_sweeps: int = -1):
+        """Which sweeps recount (lda_set_count_update): "auto" (the first
+        `recount_sweeps` sweeps after the counts are seeded; -1 keeps the
+        library's choice), "recount" (all) or "delta" (none)."""
+        capi.check(self._L.lda_set_count_update(self._h, capi.COUNT_UPDATE[mode], int(recount_sweeps)),
+                   "lda_set_count_update")
+
+    def count_update(self):
+        """(mode name, recount_sweeps)."""
+        m, r = C.c_int32(), C.c_int32()
+        capi.check(self._L.lda_get_count_update(self._h, C.byref(m), C.byref(r)), "lda_get_count_update")
+        return {v: k for k, v in capi.COUNT_UPDATE.items()}[m.value], r.value
+
     @property
     def recount(self) -> bool:
         """True when the exchange buffer holds recounted counts (dense samplers),

@@ -68,7 +68,7 @@ def test_modes_bit_exact(oracle, K, mode):
     # tokens, i.e. several recount items each (device-atomic rows)
     c = _corpus(D=400, V=60 if K <= 200 else 600, seed=K, heavy=3000)
     g = _sampler(c, K, 5 + K, mode, tokens_per_range=200)
-    assert g.recount == (mode == "recount")
+    assert g.count_update()[0] == mode
     o = oracle.ExactSampler(K, c.num_types, c.doc_off, c.words, np.full(K, 0.1), 0.01, 5 + K)
     for n in (0, 1, 3):
         g.sweep(n)
@@ -165,3 +165,36 @@ def test_recount_shards_sum(oracle):
     for s in shards:
         np.testing.assert_array_equal(s.counts()[0], onw)
         np.testing.assert_array_equal(s.counts()[1], ons)
+
+
+def test_auto_mode_switches_to_delta(oracle):
+    """LDA_COUNT_AUTO (the default): the first recount_sweeps sweeps after the
+    counts are seeded recount, later ones keep a delta; lda_set_z re-seeds.
+    Bit-exact throughout."""
+    c = _corpus(D=300, V=200, seed=8, heavy=1500)
+    K = 64
+    from ldagibbssampling_amd.sampler import GibbsSampler
+    g = GibbsSampler(K, c.num_types, c.doc_off, c.words, np.full(K, 0.1), 0.01, seed=2)
+    assert g.count_update() == ("auto", 10)
+    g.set_count_update("auto", 3)
+    o = oracle.ExactSampler(K, c.num_types, c.doc_off, c.words, np.full(K, 0.1), 0.01, 2)
+    g.sweep(0)
+    o.sweep(0)
+    modes = []
+    for _ in range(6):
+        modes.append(g.recount)           # the mode the next sweep will use
+        g.sweep(1)
+        o.sweep(1)
+        _same(g, o)
+    assert modes == [True, True, True, False, False, False]
+    rc = g.recount_times(6)
+    assert np.all(rc[:3] > 0)
+    g.set_z(o.z())                        # re-seeded: recounts again
+    assert g.recount is False             # the seeded counts are pending as a delta
+    g.sweep(0)
+    assert g.recount is True
+    g.set_count_update("delta")
+    assert g.recount is False
+    g.sweep(2)
+    o.sweep(2)
+    _same(g, o)
