@@ -1,11 +1,14 @@
 #!/usr/bin/env python3
 """Benchmark: Gibbs tokens sampled/sec at K=512 (BASELINE.json metric).
 
-Workload (one "step" = one full Gibbs sweep over the GPU's shard = sample
-kernel + [RCCL all-reduce of the nw/nwsum delta when N > 1] + apply):
-  config C4 of BASELINE.json (10M docs x 200 tokens, V=100k, K=512, 8 GPUs)
-  sharded AD-LDA style: every GPU holds 1.25M docs x 200 tokens (2.5e8
-  tokens), so N=8 is exactly C4 and N=1 is one C4 shard (weak scaling).
+Workload (one "step" = one full Gibbs sweep over the corpus = sample kernel
++ [RCCL all-reduce of the nw/nwsum exchange buffer when N > 1] + apply):
+  config C4 of BASELINE.json, the whole corpus (10M docs x 200 tokens = 2e9
+  tokens, V=100k, K=512), drawn as 8 blocks of 1.25M documents; with N GPUs
+  rank r holds blocks [8r/N, 8(r+1)/N) (AD-LDA document shards), so every N
+  runs the same corpus (strong scaling: N=1 is all of C4 on one MI355X, N=8
+  is BASELINE's 8-GPU C4).  --config c4shard keeps 1.25M docs per GPU (weak
+  scaling, the round-2 headline).
 Synthetic corpus: LDA generative process, drawn on the GPU.
 
 Prints ONE JSON line (rank 0).  value = tokens sampled by all ranks per
@@ -33,11 +36,11 @@ CONFIGS = {
     # inverse_docs corpus; K=20, alphaSum 10 as src/cmu, 100 sweeps)
     "c1": dict(docs=2_000, doc_len=None, V=5_000, K=20, alpha_sum=10.0, steps=100,
                desc="C1: changelist-shaped corpus, 2000 docs x Poisson(8) tok, Zipf(1.1) over 5000 paths, K=20"),
-    "c4": dict(docs=1_250_000, doc_len=200, V=100_000, K=512,
-               desc="C4 shard: 1.25M docs x 200 tok per GPU, V=100k, K=512 (N=8 == C4: 10M docs)"),
-    # the whole C4 corpus in one context (2e9 tokens: int64 offsets, a DESIGN figure)
-    "c4full": dict(docs=10_000_000, doc_len=200, V=100_000, K=512,
-                   desc="C4 whole corpus on one GPU: 10M docs x 200 tok, V=100k, K=512"),
+    # the headline: the whole C4 corpus, 8 blocks of 1.25M docs split over the ranks
+    "c4": dict(docs=10_000_000, blocks=8, doc_len=200, V=100_000, K=512, scaling="strong",
+               desc="C4: 10M docs x 200 tok (2e9 tokens), V=100k, K=512, documents split over the GPUs"),
+    "c4shard": dict(docs=1_250_000, doc_len=200, V=100_000, K=512,
+                    desc="C4 shard: 1.25M docs x 200 tok per GPU, V=100k, K=512 (weak scaling)"),
     "c2": dict(docs=100_000, doc_len=200, V=50_000, K=128, desc="C2: 100k docs x 200 tok, V=50k, K=128"),
     "c3": dict(docs=100_000, doc_len=200, V=50_000, K=1024, desc="C3: 100k docs x 200 tok, V=50k, K=1024"),
     "c5": dict(docs=1_250_000, doc_len=200, V=262_144, K=4096, sampler="sparse",
@@ -224,7 +227,8 @@ def main():
     ap.add_argument("--steps", type=int, default=None, help="timed sweeps (default 10; 100 for c1)")
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="c4", choices=sorted(CONFIGS))
-    ap.add_argument("--docs", type=int, default=0, help="override docs per GPU")
+    ap.add_argument("--docs", type=int, default=0,
+                    help="override docs per GPU (per block for a blocked config)")
     ap.add_argument("--sampler", default=None, choices=["dense", "sparse"],
                     help="draw kernel (default: dense, sparse for c5)")
     ap.add_argument("--burnin", type=int, default=0,
@@ -277,7 +281,30 @@ def main():
     docs = args.docs or cfg["docs"]
     alpha_sum, beta = cfg.get("alpha_sum", 0.1 * K), 0.01
     t_gen = time.perf_counter()
-    if args.config == "c1":
+    token_base = None
+    blocks_info = None
+    if cfg.get("blocks"):
+        # one corpus for every N: block b is drawn with doc_seed 20261015 + b
+        # (the topics, phi, from one seed); rank r takes a contiguous run of blocks
+        nb = cfg["blocks"]
+        total_docs = args.docs * nb if args.docs else cfg["docs"]
+        if nb % world:
+            nb = world            # N not dividing 8: N blocks (a different draw, noted in config)
+        per_block = total_docs // nb
+        b0, b1 = rank * nb // world, (rank + 1) * nb // world
+        parts = [synthetic_lda_torch(per_block, V, K, doc_len=L, seed=20261015, doc_seed=20261015 + b,
+                                     device=f"cuda:{device}") for b in range(b0, b1)]
+        from ldagibbssampling_amd.corpus import Corpus
+        offs = [parts[0].doc_off]
+        for c_ in parts[1:]:
+            offs.append(c_.doc_off[1:] + offs[-1][-1])
+        corpus = Corpus(np.concatenate(offs), np.concatenate([c_.words for c_ in parts]), V)
+        del parts
+        docs = corpus.num_docs
+        token_base = b0 * per_block * L
+        blocks_info = {"blocks": nb, "docs_per_block": per_block, "doc_seeds": "20261015 + block",
+                       "rank0_blocks": [0, nb // world]}
+    elif args.config == "c1":
         from ldagibbssampling_amd.corpus import synthetic_changelists
         corpus = synthetic_changelists(num_docs=docs, num_types=V, seed=20261015 + rank)
         V = corpus.num_types          # the alphabet: paths seen in this shard
@@ -291,7 +318,8 @@ def main():
     sampler = GibbsSampler(K, V, corpus.doc_off, corpus.words, np.full(K, alpha_sum / K), beta,
                            seed=1, device=device,
                            # unique Philox counters per rank (c1 shards differ in size)
-                           token_base=(rank << 32) if args.config == "c1" else rank * n_local,
+                           token_base=(token_base if token_base is not None else
+                                       (rank << 32) if args.config == "c1" else rank * n_local),
                            tokens_per_range=args.tokens_per_range, sampler=args.sampler)
     # one non-default stream carries the sampler kernels and (as torch's
     # current stream) orders the all-reduce behind them: no host sync per sweep.
@@ -351,7 +379,11 @@ def main():
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = float(t.item())
-    total_tokens = n_local * world * args.steps
+    nt = torch.tensor([n_local], dtype=torch.int64, device=f"cuda:{device}")
+    if world > 1:
+        dist.all_reduce(nt, op=dist.ReduceOp.SUM)
+    tokens_all = int(nt.item())
+    total_tokens = tokens_all * args.steps
     value = total_tokens / elapsed
     ll = trainer.log_likelihood()
 
@@ -406,7 +438,7 @@ def main():
             "sampler": args.sampler,
             "ms_per_step": elapsed * 1e3 / args.steps,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": cfg.get("scaling", "weak"),
             "vs_baseline": None,
             "dtype": "fp32 weights / int32 counts",
             "data": ("synthetic (changelist-shaped inverse_docs corpus, SURVEY.md §8d; corpus.synthetic_changelists)"
@@ -417,6 +449,8 @@ def main():
                 "docs_per_gpu": docs,
                 "doc_len": L,
                 "tokens_per_gpu": n_local,
+                "tokens_all_gpus": tokens_all,
+                "corpus_blocks": blocks_info,
                 "num_types": V,
                 "num_topics": K,
                 "alpha_sum": alpha_sum,
@@ -455,7 +489,7 @@ def main():
                 "issue": issue_roofline(rec, tok_s_kernel),
             },
             "collective": coll,
-            "ll_per_token": ll / (n_local * world),
+            "ll_per_token": ll / tokens_all,
             "corpus_gen_s": t_gen,
         }
         if nnz0 is not None:

@@ -84,11 +84,17 @@ SIGNATURES = {
     "lda_set_alpha_beta": (C.c_int32, [_vp, _f64p, C.c_double]),
     "lda_log_likelihood_parts": (C.c_int32, [_vp, C.POINTER(C.c_double), C.POINTER(C.c_double)]),
     "lda_log_likelihood": (C.c_int32, [_vp, C.POINTER(C.c_double)]),
+    "lda_log_likelihood_enqueue": (C.c_int32, [_vp, C.POINTER(C.c_int64)]),
+    "lda_log_likelihood_collect": (C.c_int32, [_vp, C.c_int64, C.POINTER(C.c_double),
+                                               C.POINTER(C.c_double)]),
     "lda_infer": (C.c_int32, [_vp, C.c_int64, _i64p, _i32p, C.c_int32, C.c_int32, C.c_int32,
                               C.c_uint64, _f64p]),
     "lda_to_mallet_packed": (C.c_int32, [_vp, _vp, _i64p, C.POINTER(C.c_int32)]),
     "lda_max_doc_length": (C.c_int32, [_vp, C.POINTER(C.c_int32)]),
     "lda_doc_topic_histograms": (C.c_int32, [_vp, C.c_int32, _i32p, _i32p]),
+    "lda_doc_topic_histograms_accumulate": (C.c_int32, [_vp, C.c_int32]),
+    "lda_doc_topic_histograms_take": (C.c_int32, [_vp, C.c_int32, _i32p, _i32p]),
+    "lda_doc_topic_histograms_clear": (C.c_int32, [_vp]),
     "lda_count_histogram": (C.c_int32, [_vp, C.c_int64, _i32p]),
     "lda_learn_parameters": (C.c_int32, [_f64p, C.c_int32, _i32p, _i32p, C.c_int32, C.c_double,
                                          C.c_double, C.c_int32, C.POINTER(C.c_double)]),
@@ -103,6 +109,9 @@ SIGNATURES = {
     "lda_recount_times": (C.c_int32, [_vp, C.c_int32, _vp, C.POINTER(C.c_int32)]),
     "lda_count_update_mode": (C.c_int32, [_vp, C.POINTER(C.c_int32)]),
     "lda_set_count_update": (C.c_int32, [_vp, C.c_int32, C.c_int32]),
+    "lda_set_warm_start": (C.c_int32, [_vp, C.c_int32, C.c_int32]),
+    "lda_get_warm_start": (C.c_int32, [_vp, C.POINTER(C.c_int32), C.POINTER(C.c_int32)]),
+    "lda_sweep_parts": (C.c_int32, [_vp, C.POINTER(C.c_int32), C.POINTER(C.c_int32)]),
     "lda_get_count_update": (C.c_int32, [_vp, C.POINTER(C.c_int32), C.POINTER(C.c_int32)]),
     "lda_abi_version": (C.c_int32, []),
     "lda_debug_fail_host_alloc": (None, [C.c_int32]),

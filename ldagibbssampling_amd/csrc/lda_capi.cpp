@@ -180,6 +180,14 @@ struct lda_ctx {
   bool sweep_recount = false;      // the sweep being sampled recounts
   bool pending_absolute = false;   // the pending buffer holds counts (recount) rather than a delta
   bool recount_ok = false;         // dense sampler, N < 2^32
+  // warm start (lda_set_warm_start): sweeps with a sweep counter below
+  // warm_sweeps run in warm_parts SEQUENTIAL parts (each applied before
+  // the next part samples; all through buffer 0), over their own ranges
+  int warm_parts = 1;
+  int32_t warm_sweeps = 0;
+  int64_t* warm_range_doc = nullptr;
+  std::vector<int64_t> warm_part_range{0, 0};
+  bool sweep_seq = false;          // the sweep being sampled is a warm-start sweep
   uint32_t* perm = nullptr;        // [N] token indices grouped by (part, word)
   int32_t* items = nullptr;        // int4 {word, first perm index, tokens, split} per work item
   std::vector<int64_t> part_item{0, 0};
@@ -205,6 +213,21 @@ struct lda_ctx {
   double* partial = nullptr;
   unsigned long long* nonzero = nullptr;
   int partial_blocks = 1024;
+  // lda_log_likelihood_enqueue / _collect: results in flight, each copied into
+  // pinned host memory [doc partials | word partials | nonzero counts | nwsum]
+  struct LLSlot {
+    void* host = nullptr;
+    hipEvent_t done = nullptr;
+    int64_t ticket = -1;
+    double alpha_sum = 0.0, beta = 0.0;
+  };
+  static constexpr int LL_SLOTS = 16;
+  LLSlot ll[LL_SLOTS];
+  int64_t ll_next = 0;
+  // lda_doc_topic_histograms_accumulate / _take: alpha statistics summed on
+  // the device over sampled sweeps [doc lengths (L+1) | topics K x (L+1)]
+  int32_t* stat_buf = nullptr;
+  int32_t stat_len = -1;
   // event pairs around the last LDA_TIME_RING sampler launches (lda_sample_times)
   static constexpr int LDA_TIME_RING = 256;
   hipEvent_t ev0[LDA_TIME_RING] = {}, ev1[LDA_TIME_RING] = {}, ev2[LDA_TIME_RING] = {};
@@ -217,10 +240,16 @@ struct lda_ctx {
                     (void*)inv, (void*)inv_m1, (void*)partial, (void*)nonzero, (void*)ent,
                     (void*)row_off, (void*)row_nnz, (void*)nw16, (void*)wide, (void*)inf_words,
                     (void*)inf_z, (void*)inf_acc, (void*)inf_q, (void*)inf_doff, (void*)inf_range,
-                    (void*)perm, (void*)items})
+                    (void*)perm, (void*)items, (void*)warm_range_doc})
       if (p) (void)hipFree(p);
     for (int i = 1; i < LDA_MAX_EXCHANGE_PARTS; ++i)
       if (delta_part[i]) (void)hipFree(delta_part[i]);
+    for (auto& sl : ll) {
+      if (sl.done) (void)hipEventSynchronize(sl.done);
+      if (sl.host) (void)hipHostFree(sl.host);
+      if (sl.done) (void)hipEventDestroy(sl.done);
+    }
+    if (stat_buf) (void)hipFree(stat_buf);
     for (int i = 0; i < LDA_TIME_RING; ++i) {
       if (ev0[i]) (void)hipEventDestroy(ev0[i]);
       if (ev1[i]) (void)hipEventDestroy(ev1[i]);
@@ -349,14 +378,15 @@ static lda_status build_recount_index(lda_ctx* c) {
 }
 
 static lda_status apply_impl(lda_ctx* c) {
-  if (c->next_part != 0)
+  if (c->next_part != 0 && !c->sweep_seq)
     return fail(LDA_ERR_STATE, "lda_apply inside a split sweep: sample every part first");
   c->apply_gen++;
   HIP_TRY(hipSetDevice(c->device));
   // a split sweep's later parts are folded into part 0's buffer (the one the
-  // apply kernels read) and zeroed
-  for (int i = 1; i < c->parts; ++i)
-    HIP_TRY(lda::launch_fold_delta(c->delta, c->delta_part[i], (int64_t)c->V * c->Kp + c->Kp, c->stream));
+  // apply kernels read) and zeroed; a warm-start sweep's parts all use buffer 0
+  if (!c->sweep_seq)
+    for (int i = 1; i < c->parts; ++i)
+      HIP_TRY(lda::launch_fold_delta(c->delta, c->delta_part[i], (int64_t)c->V * c->Kp + c->Kp, c->stream));
   if (c->sampler == LDA_SAMPLER_DENSE) {
     // one launch: apply, 16-bit rows, topic tables, queue reset (k_apply_packed)
     lda::TopicTables t{c->nwsum, c->alpha_d, c->alpha_f, c->inv, c->inv_m1,
@@ -382,9 +412,22 @@ static lda_status apply_impl(lda_ctx* c) {
   return LDA_OK;
 }
 
-// Will the next sweep recount?
+// Is the next sweep a warm-start sweep (sequential parts)?
+// (keyed by the sweep counter, which a resumed model carries: estimate(15) +
+// estimate(25) runs the same warm start as estimate(40))
+static bool next_sweep_sequential(const lda_ctx* c) {
+  return c->warm_parts > 1 && (int64_t)c->sweep < (int64_t)c->warm_sweeps;
+}
+// Parts of the sweep in progress, or of the next one
+static int sweep_parts(const lda_ctx* c) {
+  const bool seq = c->next_part != 0 ? c->sweep_seq : next_sweep_sequential(c);
+  return seq ? c->warm_parts : c->parts;
+}
+
+// Will the next sweep recount?  (never a warm-start sweep: its parts are
+// applied one by one as changes)
 static bool next_sweep_recounts(const lda_ctx* c) {
-  if (!c->recount_ok) return false;
+  if (!c->recount_ok || next_sweep_sequential(c)) return false;
   if (c->count_mode == LDA_COUNT_RECOUNT) return true;
   if (c->count_mode == LDA_COUNT_DELTA) return false;
   return c->sweeps_since_seed < c->recount_sweeps;
@@ -648,31 +691,38 @@ lda_status lda_apply(lda_ctx* c) {
 static lda_status sample_part_impl(lda_ctx* c, int part) {
   if (part != c->next_part)
     return fail(LDA_ERR_STATE, "split sweep parts must be sampled in order 0, 1, ...");
-  if (part == 0 && c->pending) return fail(LDA_ERR_STATE, "lda_sample with a pending delta: call lda_apply first");
+  if (c->pending && (part == 0 || c->sweep_seq))
+    return fail(LDA_ERR_STATE, part == 0 ? "lda_sample with a pending delta: call lda_apply first"
+                                         : "warm-start sweep: apply each part before sampling the next");
   HIP_TRY(hipSetDevice(c->device));
   if (part == 0) {
+    c->sweep_seq = next_sweep_sequential(c);
     c->sweep_recount = next_sweep_recounts(c);
     if (c->sweep_recount && !c->perm && c->N > 0) {
       lda_status s = build_recount_index(c);
       if (s) return s;
     }
   }
-  const int64_t r0 = c->part_range[(size_t)part], r1 = c->part_range[(size_t)part + 1];
+  const bool seq = c->sweep_seq;
+  const int nparts = seq ? c->warm_parts : c->parts;
+  const std::vector<int64_t>& prange = seq ? c->warm_part_range : c->part_range;
+  const int64_t r0 = prange[(size_t)part], r1 = prange[(size_t)part + 1];
+  int32_t* buf = c->delta_part[seq ? 0 : part];
   if (r1 > r0) {
     // the dense sampler's apply (which every sample follows) zeroed queue[0]
     if (c->sampler != LDA_SAMPLER_DENSE || part > 0)
       HIP_TRY(hipMemsetAsync(c->queue + part, 0, sizeof(int32_t), c->stream));
     lda::SampleParams p = c->params(false);
-    p.range_doc = c->range_doc + r0;
+    p.range_doc = (seq ? c->warm_range_doc : c->range_doc) + r0;
     p.num_ranges = r1 - r0;
     p.queue = c->queue + part;
-    p.delta = c->sweep_recount ? nullptr : c->delta_part[part];   // recount: the sampler writes z only
-    p.dsum = c->sweep_recount ? nullptr : c->delta_part[part] + (int64_t)c->V * c->Kp;
+    p.delta = c->sweep_recount ? nullptr : buf;   // recount: the sampler writes z only
+    p.dsum = c->sweep_recount ? nullptr : buf + (int64_t)c->V * c->Kp;
     const int64_t wpb = c->waves_per_block;
     // a split sweep leaves reserve_cus CUs' worth of sampler blocks free, so
     // the collective of the part before this one finds CUs to run on
     int64_t cap = c->sample_blocks;
-    if (c->parts > 1 && c->reserve_cus > 0)
+    if (c->parts > 1 && !seq && c->reserve_cus > 0)
       cap = std::max<int64_t>(1, (int64_t)c->sample_blocks * std::max(1, c->cus - c->reserve_cus) / c->cus);
     const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>(cap, (r1 - r0 + wpb - 1) / wpb));
     const int slot = (int)(c->launches % lda_ctx::LDA_TIME_RING);
@@ -695,7 +745,7 @@ static lda_status sample_part_impl(lda_ctx* c, int part) {
   }
   c->pending = true;  // the part buffers hold this sweep's changes
   c->pending_absolute = c->sweep_recount;
-  if (++c->next_part == c->parts) {
+  if (++c->next_part == nparts) {
     c->next_part = 0;
     c->sweep++;
     c->sweeps_since_seed++;
@@ -707,8 +757,12 @@ lda_status lda_sample(lda_ctx* c) {
   return lda_abi::guarded([&]() -> lda_status {
   if (!c) return fail(LDA_ERR_INVALID_ARG, "null ctx");
   if (c->next_part != 0) return fail(LDA_ERR_STATE, "lda_sample inside a split sweep: finish it with lda_sample_part");
-  for (int i = 0; i < c->parts; ++i) {
+  // a warm-start sweep applies each part before the next one samples; its
+  // last part stays pending for the caller's lda_apply, like any sweep
+  const int n = sweep_parts(c);
+  for (int i = 0; i < n; ++i) {
     lda_status s = sample_part_impl(c, i);
+    if (s == LDA_OK && c->sweep_seq && i + 1 < n) s = apply_impl(c);
     if (s) return s;
   }
   return LDA_OK;
@@ -718,7 +772,7 @@ lda_status lda_sample(lda_ctx* c) {
 lda_status lda_sample_part(lda_ctx* c, int32_t part) {
   return lda_abi::guarded([&]() -> lda_status {
   if (!c) return fail(LDA_ERR_INVALID_ARG, "null ctx");
-  if (part < 0 || part >= c->parts) return fail(LDA_ERR_INVALID_ARG, "part out of range [0, parts)");
+  if (part < 0 || part >= sweep_parts(c)) return fail(LDA_ERR_INVALID_ARG, "part out of range [0, parts)");
   return sample_part_impl(c, part);
   });
 }
@@ -777,8 +831,10 @@ lda_status lda_get_exchange_parts(lda_ctx* c, int32_t* parts) {
 lda_status lda_delta_buffer_part(lda_ctx* c, int32_t part, void** dev_ptr, size_t* count) {
   return lda_abi::guarded([&]() -> lda_status {
   if (!c || !dev_ptr || !count) return fail(LDA_ERR_INVALID_ARG, "null argument");
-  if (part < 0 || part >= c->parts) return fail(LDA_ERR_INVALID_ARG, "part out of range [0, parts)");
-  *dev_ptr = c->delta_part[part];
+  if (part < 0 || part >= sweep_parts(c)) return fail(LDA_ERR_INVALID_ARG, "part out of range [0, parts)");
+  // a warm-start sweep's parts all go through buffer 0
+  const bool seq = c->next_part != 0 || c->pending ? c->sweep_seq : next_sweep_sequential(c);
+  *dev_ptr = c->delta_part[seq ? 0 : part];
   *count = (size_t)c->V * c->Kp + c->Kp;
   return LDA_OK;
   });
@@ -869,6 +925,47 @@ lda_status lda_recount_times(lda_ctx* c, int32_t max, float* ms, int32_t* n) {
   }
   return LDA_OK;
   });
+}
+
+lda_status lda_set_warm_start(lda_ctx* c, int32_t parts, int32_t sweeps) {
+  return lda_abi::guarded([&]() -> lda_status {
+  if (!c) return fail(LDA_ERR_INVALID_ARG, "null ctx");
+  if (parts < 1 || parts > LDA_MAX_EXCHANGE_PARTS || sweeps < 0)
+    return fail(LDA_ERR_INVALID_ARG, "parts must be in [1, LDA_MAX_EXCHANGE_PARTS], sweeps >= 0");
+  if (c->next_part != 0) return fail(LDA_ERR_STATE, "inside a split sweep");
+  HIP_TRY(hipSetDevice(c->device));
+  if (parts > 1) {
+    std::vector<int64_t> pr;
+    std::vector<int64_t> ranges = make_part_ranges(c->doc_off_h, c->tokens_per_range, parts, pr);
+    int64_t* dr = nullptr;
+    HIP_TRY(dalloc(&dr, ranges.size()));
+    hipError_t e = hipMemcpyAsync(dr, ranges.data(), sizeof(int64_t) * ranges.size(), hipMemcpyHostToDevice, c->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    if (e != hipSuccess) (void)hipFree(dr);
+    HIP_TRY(e);
+    if (c->warm_range_doc) (void)hipFree(c->warm_range_doc);
+    c->warm_range_doc = dr;
+    c->warm_part_range = pr;
+  }
+  c->warm_parts = parts;
+  c->warm_sweeps = parts > 1 ? sweeps : 0;
+  return LDA_OK;
+  });
+}
+
+lda_status lda_get_warm_start(lda_ctx* c, int32_t* parts, int32_t* sweeps) {
+  if (!c) return fail(LDA_ERR_INVALID_ARG, "null ctx");
+  if (parts) *parts = c->warm_parts;
+  if (sweeps) *sweeps = c->warm_sweeps;
+  return LDA_OK;
+}
+
+lda_status lda_sweep_parts(lda_ctx* c, int32_t* parts, int32_t* sequential) {
+  if (!c) return fail(LDA_ERR_INVALID_ARG, "null ctx");
+  const bool seq = c->next_part != 0 ? c->sweep_seq : next_sweep_sequential(c);
+  if (parts) *parts = seq ? c->warm_parts : c->parts;
+  if (sequential) *sequential = seq ? 1 : 0;
+  return LDA_OK;
 }
 
 lda_status lda_set_count_update(lda_ctx* c, int32_t mode, int32_t recount_sweeps) {
@@ -997,43 +1094,84 @@ lda_status lda_set_alpha_beta(lda_ctx* c, const double* alpha, double beta) {
   });
 }
 
-lda_status lda_log_likelihood_parts(lda_ctx* c, double* doc_part, double* word_part) {
+lda_status lda_log_likelihood_enqueue(lda_ctx* c, int64_t* ticket) {
   return lda_abi::guarded([&]() -> lda_status {
-  if (!c) return fail(LDA_ERR_INVALID_ARG, "null ctx");
+  if (!c || !ticket) return fail(LDA_ERR_INVALID_ARG, "null argument");
   if (c->pending) return fail(LDA_ERR_STATE, "log likelihood with a pending delta: call lda_apply first");
   HIP_TRY(hipSetDevice(c->device));
+  const int nb = c->partial_blocks;
+  lda_ctx::LLSlot& sl = c->ll[c->ll_next % lda_ctx::LL_SLOTS];
+  if (!sl.host) {
+    HIP_TRY(hipHostMalloc(&sl.host, sizeof(double) * 2 * nb + sizeof(unsigned long long) * nb +
+                                        sizeof(int32_t) * c->K, hipHostMallocDefault));
+    HIP_TRY(hipEventCreateWithFlags(&sl.done, hipEventDisableTiming));
+  } else {
+    HIP_TRY(hipEventSynchronize(sl.done));   // an uncollected older result is overwritten
+  }
+  double* hd = static_cast<double*>(sl.host);
+  double* hw = hd + nb;
+  auto* hz = reinterpret_cast<unsigned long long*>(hw + nb);
+  auto* hs = reinterpret_cast<int32_t*>(hz + nb);
   double alpha_sum = 0.0;
   for (double a : c->alpha) alpha_sum += a;
-  const int nb = c->partial_blocks;
-  std::vector<double> part(nb);
-  std::vector<unsigned long long> nz(nb);
-  double docs = 0.0;
   if (c->D > 0) {
     HIP_TRY(lda::launch_ll_docs(c->z, c->doc_off, c->D, c->alpha_d, alpha_sum, c->K, c->Kp,
                                 c->partial, nb, c->stream));
-    HIP_TRY(hipMemcpyAsync(part.data(), c->partial, sizeof(double) * nb, hipMemcpyDeviceToHost, c->stream));
-    HIP_TRY(hipStreamSynchronize(c->stream));
-    for (int b = 0; b < nb; ++b) docs += part[b];
+    HIP_TRY(hipMemcpyAsync(hd, c->partial, sizeof(double) * nb, hipMemcpyDeviceToHost, c->stream));
+  } else {
+    std::fill(hd, hd + nb, 0.0);
   }
-  docs += (double)c->D * log_gamma_stirling(alpha_sum);
+  // stream order: the copy above has read c->partial before k_ll_words writes it
   HIP_TRY(lda::launch_ll_words(c->nw, c->V, c->K, c->Kp, c->beta, c->partial, c->nonzero, nb, c->stream));
-  HIP_TRY(hipMemcpyAsync(part.data(), c->partial, sizeof(double) * nb, hipMemcpyDeviceToHost, c->stream));
-  HIP_TRY(hipMemcpyAsync(nz.data(), c->nonzero, sizeof(unsigned long long) * nb, hipMemcpyDeviceToHost, c->stream));
-  std::vector<int32_t> nws(c->K);
-  HIP_TRY(hipMemcpyAsync(nws.data(), c->nwsum, sizeof(int32_t) * c->K, hipMemcpyDeviceToHost, c->stream));
-  HIP_TRY(hipStreamSynchronize(c->stream));
-  double words_ll = 0.0;
+  HIP_TRY(hipMemcpyAsync(hw, c->partial, sizeof(double) * nb, hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipMemcpyAsync(hz, c->nonzero, sizeof(unsigned long long) * nb, hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipMemcpyAsync(hs, c->nwsum, sizeof(int32_t) * c->K, hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipEventRecord(sl.done, c->stream));
+  sl.alpha_sum = alpha_sum;
+  sl.beta = c->beta;
+  sl.ticket = c->ll_next;
+  *ticket = c->ll_next++;
+  return LDA_OK;
+  });
+}
+
+lda_status lda_log_likelihood_collect(lda_ctx* c, int64_t ticket, double* doc_part, double* word_part) {
+  return lda_abi::guarded([&]() -> lda_status {
+  if (!c || ticket < 0) return fail(LDA_ERR_INVALID_ARG, "bad argument");
+  lda_ctx::LLSlot& sl = c->ll[ticket % lda_ctx::LL_SLOTS];
+  if (sl.ticket != ticket)
+    return fail(LDA_ERR_STATE, "log-likelihood ticket already collected or overwritten (at most 16 in flight)");
+  HIP_TRY(hipSetDevice(c->device));
+  HIP_TRY(hipEventSynchronize(sl.done));
+  const int nb = c->partial_blocks;
+  const double* hd = static_cast<const double*>(sl.host);
+  const double* hw = hd + nb;
+  const auto* hz = reinterpret_cast<const unsigned long long*>(hw + nb);
+  const auto* hs = reinterpret_cast<const int32_t*>(hz + nb);
+  double docs = 0.0, words_ll = 0.0;
   unsigned long long nonzero = 0;
   for (int b = 0; b < nb; ++b) {
-    words_ll += part[b];
-    nonzero += nz[b];
+    docs += hd[b];
+    words_ll += hw[b];
+    nonzero += hz[b];
   }
-  for (int k = 0; k < c->K; ++k) words_ll -= log_gamma_stirling(c->beta * c->V + nws[k]);
-  words_ll += log_gamma_stirling(c->beta * c->V) * c->K;
-  words_ll -= log_gamma_stirling(c->beta) * (double)nonzero;
+  docs += (double)c->D * log_gamma_stirling(sl.alpha_sum);
+  for (int k = 0; k < c->K; ++k) words_ll -= log_gamma_stirling(sl.beta * c->V + hs[k]);
+  words_ll += log_gamma_stirling(sl.beta * c->V) * c->K;
+  words_ll -= log_gamma_stirling(sl.beta) * (double)nonzero;
   if (doc_part) *doc_part = docs;
   if (word_part) *word_part = words_ll;
+  sl.ticket = -1;
   return LDA_OK;
+  });
+}
+
+lda_status lda_log_likelihood_parts(lda_ctx* c, double* doc_part, double* word_part) {
+  return lda_abi::guarded([&]() -> lda_status {
+  int64_t t = -1;
+  lda_status s = lda_log_likelihood_enqueue(c, &t);
+  if (s) return s;
+  return lda_log_likelihood_collect(c, t, doc_part, word_part);
   });
 }
 
@@ -1087,6 +1225,59 @@ lda_status lda_doc_topic_histograms(lda_ctx* c, int32_t max_len, int32_t* doc_le
   HIP_TRY(e);
   for (int64_t i = 0; i < L1; ++i) doc_len_counts[i] += h[i];
   for (size_t i = 0; i < (size_t)c->K * L1; ++i) topic_doc_counts[i] += h[L1 + i];
+  return LDA_OK;
+  });
+}
+
+lda_status lda_doc_topic_histograms_accumulate(lda_ctx* c, int32_t max_len) {
+  return lda_abi::guarded([&]() -> lda_status {
+  if (!c) return fail(LDA_ERR_INVALID_ARG, "null ctx");
+  int32_t m = 0;
+  lda_max_doc_length(c, &m);
+  if (max_len < m) return fail(LDA_ERR_INVALID_ARG, "max_len below the longest document");
+  if (c->pending) return fail(LDA_ERR_STATE, "histograms with a pending delta: call lda_apply first");
+  if (c->stat_buf && c->stat_len != max_len)
+    return fail(LDA_ERR_STATE, "max_len differs from the accumulated histograms': take them first");
+  HIP_TRY(hipSetDevice(c->device));
+  const int64_t L1 = (int64_t)max_len + 1;
+  const size_t n = (size_t)L1 + (size_t)c->K * L1;
+  if (!c->stat_buf) {
+    HIP_TRY(dalloc(&c->stat_buf, n));
+    HIP_TRY(hipMemsetAsync(c->stat_buf, 0, n * sizeof(int32_t), c->stream));
+    c->stat_len = max_len;
+  }
+  HIP_TRY(lda::launch_doc_hist(c->z, c->doc_off, c->D, c->K, c->Kp, max_len, c->stat_buf, c->stat_buf + L1,
+                               c->stream));
+  return LDA_OK;
+  });
+}
+
+lda_status lda_doc_topic_histograms_take(lda_ctx* c, int32_t max_len, int32_t* doc_len_counts,
+                                         int32_t* topic_doc_counts) {
+  return lda_abi::guarded([&]() -> lda_status {
+  if (!c || !doc_len_counts || !topic_doc_counts) return fail(LDA_ERR_INVALID_ARG, "null argument");
+  if (!c->stat_buf) return LDA_OK;           // nothing accumulated
+  if (c->stat_len != max_len) return fail(LDA_ERR_INVALID_ARG, "max_len differs from the accumulated histograms'");
+  HIP_TRY(hipSetDevice(c->device));
+  const int64_t L1 = (int64_t)max_len + 1;
+  const size_t n = (size_t)L1 + (size_t)c->K * L1;
+  std::vector<int32_t> h = host_vector<int32_t>(n);
+  HIP_TRY(hipMemcpyAsync(h.data(), c->stat_buf, n * sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipMemsetAsync(c->stat_buf, 0, n * sizeof(int32_t), c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  for (int64_t i = 0; i < L1; ++i) doc_len_counts[i] += h[(size_t)i];
+  for (size_t i = 0; i < (size_t)c->K * L1; ++i) topic_doc_counts[i] += h[L1 + i];
+  return LDA_OK;
+  });
+}
+
+lda_status lda_doc_topic_histograms_clear(lda_ctx* c) {
+  return lda_abi::guarded([&]() -> lda_status {
+  if (!c) return fail(LDA_ERR_INVALID_ARG, "null ctx");
+  if (!c->stat_buf) return LDA_OK;
+  HIP_TRY(hipSetDevice(c->device));
+  const size_t n = (size_t)(c->stat_len + 1) * (size_t)(c->K + 1);
+  HIP_TRY(hipMemsetAsync(c->stat_buf, 0, n * sizeof(int32_t), c->stream));
   return LDA_OK;
   });
 }

@@ -138,7 +138,8 @@ class ADLDATrainer:
         import torch
         from . import capi
         mode, r = self.engine.count_update()
-        dev = self._delta.device if self.dist.get_backend(self.group) == "nccl" else "cpu"
+        backend = getattr(self.dist, "get_backend", None)
+        dev = "cpu" if backend is not None and backend(self.group) != "nccl" else self._delta.device
         t = torch.tensor([capi.COUNT_UPDATE[mode], -capi.COUNT_UPDATE[mode], r], dtype=torch.int64,
                          device=dev)
         self.dist.all_reduce(t, op=self.dist.ReduceOp.MIN, group=self.group)
@@ -187,18 +188,39 @@ class ADLDATrainer:
             torch.cuda.current_stream(self._delta.device).synchronize()
 
     def _part_delta(self, i: int):
+        """Tensor view of part i's buffer, re-made whenever the engine's buffer
+        moved (lda_set_exchange_parts frees and reallocates part buffers when
+        the part count changes: a stale view would reduce freed memory)."""
         if i == 0:
             return self._delta
-        if i not in self._part_deltas:
-            self._part_deltas[i] = self.engine.delta_tensor(i)
-        return self._part_deltas[i]
+        key = self.engine.delta_buffer(i)[0] if hasattr(self.engine, "delta_buffer") else None
+        cached = self._part_deltas.get(i)
+        if cached is None or key is None or cached[0] != key:
+            cached = (key, self.engine.delta_tensor(i))
+            self._part_deltas[i] = cached
+        return cached[1]
+
+    def _sequential_sweep(self, parts: int):
+        """A warm-start sweep (lda_set_warm_start): each part sampled, its
+        changes (always buffer 0) summed across ranks and applied before the
+        next part samples."""
+        for i in range(parts):
+            self.engine.sample_part(i)
+            self._reduce()
+            self.engine.apply()
 
     def sweep(self, n: int = 1):
         if not self._initialised:
             self.init_counts()
-        parts = self.parts if self.world > 1 else 1
         for _ in range(n):
-            if parts > 1:
+            parts, seq = (self.engine.sweep_parts() if hasattr(self.engine, "sweep_parts")
+                          else (self.parts, False))
+            if seq:
+                self._sequential_sweep(parts)
+                continue
+            if self.world < 2:
+                self.engine.sample()
+            elif parts > 1:
                 self._split_sweep(parts)
             else:
                 self.engine.sample()

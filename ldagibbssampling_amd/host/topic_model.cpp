@@ -231,6 +231,17 @@ class ShardGroup {
 
   // sample + exchange + apply of one sweep
   void sweep() {
+    int32_t np = 1, seq = 0;
+    check(lda_sweep_parts(ctx[0], &np, &seq), "lda_sweep_parts");
+    if (seq) {
+      // a warm-start sweep: every part sampled, summed and applied in turn
+      for (int i = 0; i < np; ++i) {
+        for (auto c : ctx) check(lda_sample_part(c, i), "lda_sample_part");
+        reduce();
+        apply();
+      }
+      return;
+    }
     if (ctx.size() < 2 || parts < 2) {
       for (auto c : ctx) check(lda_sample(c), "lda_sample");
       reduce();
@@ -324,6 +335,15 @@ void ParallelTopicModel::setNumThreads(int32_t n) {
   if (n < 1) raise(LDA_ERR_INVALID_ARG, "numThreads must be >= 1");
   markDirty();
   num_threads_ = n;
+}
+
+void ParallelTopicModel::setWarmStart(int32_t parts, int32_t sweeps) {
+  if (parts < 1 || parts > LDA_MAX_EXCHANGE_PARTS || sweeps < 0)
+    raise(LDA_ERR_INVALID_ARG, "warm start: parts in [1, 4], sweeps >= 0");
+  warm_parts_ = parts;
+  warm_sweeps_ = sweeps;
+  if (shards_ && !shards_dirty_)
+    for (auto c : shards_->ctx) check(lda_set_warm_start(c, warm_parts_, warm_sweeps_), "lda_set_warm_start");
 }
 
 void ParallelTopicModel::setDevices(const int32_t* devices, int32_t n) {
@@ -461,6 +481,7 @@ void ParallelTopicModel::ensureShards() {
   sg->reduce();
   sg->apply();
   sg->set_parts(exchange_parts_);
+  for (auto c : sg->ctx) check(lda_set_warm_start(c, warm_parts_, warm_sweeps_), "lda_set_warm_start");
   for (auto c : sg->ctx) check(lda_set_sweep(c, sweep_), "lda_set_sweep");
   shards_ = std::move(sg);
   shards_dirty_ = false;
@@ -573,32 +594,65 @@ void ParallelTopicModel::estimate() {
   ensureShards();
   ll_trace_.clear();
   const double total_tokens = (double)numTokens();
+  // Mallet's estimate() builds new WorkerRunnables whose alpha statistics
+  // start empty (WorkerRunnable.initializeAlphaStatistics): statistics still
+  // pending from an earlier estimate() are not carried into this one
+  std::fill(doc_len_counts_.begin(), doc_len_counts_.end(), 0);
+  std::fill(topic_doc_counts_.begin(), topic_doc_counts_.end(), 0);
+  for (auto c : shards_->ctx) check(lda_doc_topic_histograms_clear(c), "lda_doc_topic_histograms_clear");
+  // LL/token every 10 sweeps without stopping the sweeps: the kernels are
+  // enqueued behind the sweep and their sums collected (and logged) in
+  // batches, and at the end
+  std::vector<std::pair<int32_t, std::vector<int64_t>>> ll_pending;
+  auto collect_ll = [&]() {
+    for (const auto& p : ll_pending) {
+      double ll = 0.0;
+      for (size_t g = 0; g < shards_->ctx.size(); ++g) {
+        double dp = 0.0, wp = 0.0;
+        check(lda_log_likelihood_collect(shards_->ctx[g], p.second[g], &dp, &wp), "lda_log_likelihood_collect");
+        ll += dp + (g == 0 ? wp : 0.0);   // the word part is global: once
+      }
+      ll /= total_tokens;
+      ll_trace_.emplace_back(p.first, ll);
+      log("<" + std::to_string(p.first) + "> LL/token: " + java_number5(ll));
+    }
+    ll_pending.clear();
+  };
   for (int32_t it = 1; it <= num_iterations_; ++it) {
-    if (show_topics_interval_ != 0 && it % show_topics_interval_ == 0)
+    if (show_topics_interval_ != 0 && it % show_topics_interval_ == 0) {
+      collect_ll();
       log("\n" + displayTopWords(words_per_topic_, false));
+    }
     shards_->sweep();
     z_dirty_ = true;
     const bool opt = it > burnin_period_ && optimize_interval_ != 0;
     if (opt && it % save_sample_interval_ == 0)
       for (auto c : shards_->ctx)
-        check(lda_doc_topic_histograms(c, max_doc_len_, doc_len_counts_.data(),
-                                       topic_doc_counts_.data()),
-              "lda_doc_topic_histograms");
+        check(lda_doc_topic_histograms_accumulate(c, max_doc_len_), "lda_doc_topic_histograms_accumulate");
     if (opt && it % optimize_interval_ == 0) {
+      for (auto c : shards_->ctx)
+        check(lda_doc_topic_histograms_take(c, max_doc_len_, doc_len_counts_.data(), topic_doc_counts_.data()),
+              "lda_doc_topic_histograms_take");
       optimizeAlpha();
       optimizeBeta();
       for (auto c : shards_->ctx) check(lda_set_alpha_beta(c, alpha_.data(), beta_), "lda_set_alpha_beta");
     }
     if (it % 10 == 0) {
       if (print_log_likelihood_) {
-        const double ll = modelLogLikelihood() / total_tokens;
-        ll_trace_.emplace_back(it, ll);
-        log("<" + std::to_string(it) + "> LL/token: " + java_number5(ll));
+        std::vector<int64_t> tickets(shards_->ctx.size());
+        for (size_t g = 0; g < shards_->ctx.size(); ++g)
+          check(lda_log_likelihood_enqueue(shards_->ctx[g], &tickets[g]), "lda_log_likelihood_enqueue");
+        ll_pending.emplace_back(it, std::move(tickets));
+        if (ll_pending.size() >= 8) collect_ll();
       } else {
         log("<" + std::to_string(it) + ">");
       }
     }
   }
+  collect_ll();
+  // statistics gathered after the last optimisation are dropped, as Mallet's
+  // runnables are
+  for (auto c : shards_->ctx) check(lda_doc_topic_histograms_clear(c), "lda_doc_topic_histograms_clear");
   // Mallet's estimate() returns when the sweeps are done: wait for the shards'
   // streams (a kernel fault surfaces here, not in a later call)
   for (auto c : shards_->ctx) check(lda_synchronize(c), "lda_synchronize");
@@ -685,7 +739,8 @@ std::string ParallelTopicModel::displayTopWords(int32_t num_words, bool using_ne
 // run bit for bit (topics, hyperparameters, options, the statistics gathered
 // since the last optimisation, and the Philox sweep counter).
 namespace {
-constexpr char kMagic[8] = {'L', 'D', 'A', 'T', 'M', 0, 'v', '1'};
+constexpr char kMagic[8] = {'L', 'D', 'A', 'T', 'M', 0, 'v', '2'};    // v2: + warm start
+constexpr char kMagicV1[8] = {'L', 'D', 'A', 'T', 'M', 0, 'v', '1'};
 
 struct Writer {
   std::ofstream f;
@@ -762,6 +817,8 @@ void ParallelTopicModel::save(const std::string& path) {
   w.pod(max_doc_len_);
   w.vec(doc_len_counts_);
   w.vec(topic_doc_counts_);
+  w.pod(warm_parts_);
+  w.pod(warm_sweeps_);
   w.f.flush();
   if (!w.f) raise(LDA_ERR_INVALID_ARG, "write failed: " + path);
 }
@@ -771,7 +828,9 @@ std::unique_ptr<ParallelTopicModel> ParallelTopicModel::load(const std::string& 
   if (!r.f) raise(LDA_ERR_INVALID_ARG, "cannot open " + path);
   char magic[8];
   r.f.read(magic, 8);
-  if (!r.f || std::memcmp(magic, kMagic, 8) != 0) raise(LDA_ERR_INVALID_ARG, "not an lda_topic_model checkpoint");
+  const bool v1 = r.f && std::memcmp(magic, kMagicV1, 8) == 0;
+  if (!r.f || (!v1 && std::memcmp(magic, kMagic, 8) != 0))
+    raise(LDA_ERR_INVALID_ARG, "not an lda_topic_model checkpoint");
   const int32_t K = r.pod<int32_t>(), V = r.pod<int32_t>();
   const double alpha_sum = r.pod<double>(), beta = r.pod<double>();
   auto m = std::make_unique<ParallelTopicModel>(K, alpha_sum, beta);
@@ -815,6 +874,10 @@ std::unique_ptr<ParallelTopicModel> ParallelTopicModel::load(const std::string& 
       (m->max_doc_len_ >= 0 && (m->doc_len_counts_.size() != (size_t)m->max_doc_len_ + 1 ||
                                 m->topic_doc_counts_.size() != (size_t)K * (m->max_doc_len_ + 1))))
     raise(LDA_ERR_INVALID_ARG, "checkpoint corrupt (statistics)");
+  if (!v1) {
+    m->warm_parts_ = r.pod<int32_t>();
+    m->warm_sweeps_ = r.pod<int32_t>();
+  }
   m->shards_dirty_ = true;
   return m;
 }
@@ -959,6 +1022,11 @@ TM_SETTER(ldatm_set_symmetric_alpha, setSymmetricAlpha(n != 0))
 TM_SETTER(ldatm_set_num_threads, setNumThreads(n))
 TM_SETTER(ldatm_set_sampler, setSampler(n))
 TM_SETTER(ldatm_set_exchange_parts, setExchangeParts(n))
+
+lda_status ldatm_set_warm_start(ldatm* m, int32_t parts, int32_t sweeps) {
+  TM_CHECK(m);
+  return guard([&] { m->model.setWarmStart(parts, sweeps); });
+}
 
 lda_status ldatm_set_devices(ldatm* m, int32_t n, const int32_t* devices) {
   TM_CHECK(m);

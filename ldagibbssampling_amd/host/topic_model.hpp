@@ -59,6 +59,9 @@ class ParallelTopicModel {
   // to setNumThreads' plan).  Shards that share one device exchange through a
   // device-side sum instead of RCCL (the multi-shard path on one GPU).
   void setDevices(const int32_t* devices, int32_t n);
+  // warm start (lda_set_warm_start): sweeps 0..sweeps-1 in `parts` sequential
+  // parts; the default 4 x 50 (held-out perplexity at K = 20)
+  void setWarmStart(int32_t parts, int32_t sweeps);
   int32_t numShards();
   void setVerbosity(int32_t v) { verbosity_ = v; }
   // state a Java-side ParallelTopicModel already holds (GpuParallelTopicModel:
@@ -124,6 +127,7 @@ class ParallelTopicModel {
   bool symmetric_alpha_ = false, print_log_likelihood_ = true;
   uint64_t seed_ = 0;
   int32_t num_threads_ = 1, sampler_ = LDA_SAMPLER_DENSE, verbosity_ = 0, exchange_parts_ = 1;
+  int32_t warm_parts_ = 4, warm_sweeps_ = 50;
 
   std::vector<int32_t> devices_;  // setDevices (empty: plan_shards)
   std::unique_ptr<ShardGroup> shards_;

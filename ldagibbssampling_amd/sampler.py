@@ -180,6 +180,17 @@ class GibbsSampler:
                                              C.byref(n)), "lda_recount_times")
         return ms[:n.value]
 
+    def set_warm_start(self, parts: int = 4, sweeps: int = 50):
+        """lda_set_warm_start: the first `sweeps` sweeps after the counts are
+        seeded run in `parts` sequential parts (parts = 1: off)."""
+        capi.check(self._L.lda_set_warm_start(self._h, int(parts), int(sweeps)), "lda_set_warm_start")
+
+    def sweep_parts(self):
+        """(parts, sequential) of the sweep in progress or the next one."""
+        p, q = C.c_int32(), C.c_int32()
+        capi.check(self._L.lda_sweep_parts(self._h, C.byref(p), C.byref(q)), "lda_sweep_parts")
+        return p.value, bool(q.value)
+
     def set_count_update(self, mode: str = "auto", recount_sweeps: int = -1):
         """Which sweeps recount (lda_set_count_update): "auto" (the first
         `recount_sweeps` sweeps after the counts are seeded; -1 keeps the

@@ -211,9 +211,38 @@ class ExactSampler:
         n = self.V * self.Kp + self.Kp
         return np.ctypeslib.as_array(p, shape=(n,))
 
+    def set_warm_start(self, parts: int, sweeps: int):
+        """lda_set_warm_start: sweeps whose sweep counter is below `sweeps` run in
+        `parts` sequential parts (token-balanced document cuts as
+        lda_capi.cpp's make_part_ranges), each applied before the next."""
+        self._warm = (int(parts), int(sweeps) if parts > 1 else 0)
+
+    def _warm_cuts(self):
+        P = self._warm[0]
+        off = self.doc_off
+        n = int(off[-1] - off[0])
+        cuts, d0 = [0], 0
+        for i in range(P):
+            d1 = self.D
+            if i + 1 < P:
+                d1 = int(np.searchsorted(off, off[0] + n * (i + 1) // P, side="left"))
+                d1 = min(max(d1, d0), self.D)
+            cuts.append(d1)
+            d0 = d1
+        return cuts
+
     def sample(self, frozen=False):
         if self._pending:
             raise RuntimeError("sample with a pending delta: apply first (as lda_sample)")
+        warm = getattr(self, "_warm", (1, 0))
+        if not frozen and warm[0] > 1 and self.sweep_index < warm[1]:
+            cuts = self._warm_cuts()
+            for i in range(warm[0]):
+                self.sample_docs(cuts[i], cuts[i + 1])
+                if i + 1 < warm[0]:
+                    self.apply()
+            self.end_sweep()
+            return
         lib().orc_exact_sample(self._h, 1 if frozen else 0)
         self._pending = not frozen
 

@@ -86,3 +86,44 @@ def test_row_stats(K):
     nw = g.counts()[0].astype(np.float64)
     tot, nnz = nw.sum(1), (nw > 0).sum(1)
     assert abs(g.row_stats() - (tot * nnz).sum() / tot.sum()) < 1e-9
+
+
+@pytest.mark.parametrize("kind,K", [("dense", 64), ("sparse", 4096)])
+def test_device_accumulated_histograms_and_async_ll(kind, K):
+    """lda_doc_topic_histograms_accumulate over three sweeps + _take equal the
+    sum of the per-sweep histograms; lda_log_likelihood_enqueue/_collect
+    equal the blocking lda_log_likelihood_parts; a ticket is collected once."""
+    import ctypes as C
+    from ldagibbssampling_amd import capi
+    from ldagibbssampling_amd.sampler import GibbsSampler
+    c = synthetic_lda(num_docs=200, num_types=400, num_topics=30, doc_len=None, mean_len=60,
+                      min_len=0, max_len=300, seed=K)
+    g = GibbsSampler(K, c.num_types, c.doc_off, c.words, 0.1, 0.01, seed=5, sampler=kind)
+    L = g.max_doc_length()
+    lib = capi.load()
+    dl_sum = np.zeros(L + 1, np.int32)
+    td_sum = np.zeros(K * (L + 1), np.int32)
+    tickets, exp_ll = [], []
+    for _ in range(3):
+        g.sweep(1)
+        dl, td = g.doc_topic_histograms()
+        dl_sum += dl
+        td_sum += td.reshape(-1)
+        capi.check(lib.lda_doc_topic_histograms_accumulate(g._h, L), "accumulate")
+        t = C.c_int64()
+        capi.check(lib.lda_log_likelihood_enqueue(g._h, C.byref(t)), "enqueue")
+        tickets.append(t.value)
+        exp_ll.append(g.log_likelihood_parts())
+    dl_acc = np.zeros(L + 1, np.int32)
+    td_acc = np.zeros(K * (L + 1), np.int32)
+    capi.check(lib.lda_doc_topic_histograms_take(g._h, L, dl_acc, td_acc), "take")
+    np.testing.assert_array_equal(dl_acc, dl_sum)
+    np.testing.assert_array_equal(td_acc, td_sum)
+    capi.check(lib.lda_doc_topic_histograms_take(g._h, L, dl_acc, td_acc), "take")   # zeroed: adds 0
+    np.testing.assert_array_equal(dl_acc, dl_sum)
+    for t, (ed, ew) in zip(tickets, exp_ll):
+        a, b = C.c_double(), C.c_double()
+        capi.check(lib.lda_log_likelihood_collect(g._h, t, C.byref(a), C.byref(b)), "collect")
+        assert a.value == ed and b.value == ew
+    a, b = C.c_double(), C.c_double()
+    assert lib.lda_log_likelihood_collect(g._h, tickets[0], C.byref(a), C.byref(b)) == -4

@@ -76,6 +76,7 @@ def _oracle_schedule(oracle, corpus, V, K, z0, alpha, alpha_sum, beta, seed, swe
     restatement: sweeps, statistics, optimizeAlpha / optimizeBeta, LL/10)."""
     o = oracle.ExactSampler(K, V, corpus.doc_off, corpus.words, alpha, beta, seed, z_init=z0,
                             kind=kind)
+    o.set_warm_start(4, 50)       # the native model's default warm start, keyed by the sweep counter
     o.sweep_index = sweep0
     lens = np.diff(corpus.doc_off)
     L = int(lens.max())
@@ -222,3 +223,33 @@ def test_checkpoint_resume_equals_uninterrupted(oracle):
     assert resumed["sweep"] == whole["sweep"] == 40
     o, *_ = _oracle_schedule(oracle, c, V, K, z0, alpha0, 6.0, 0.02, seed, 0, 40, 0, 200, 10)
     np.testing.assert_array_equal(whole["z"], o.z())
+
+
+def test_estimate_ending_between_statistics_and_optimisation(oracle):
+    """An estimate() that ends after a statistics sweep but before the next
+    optimisation (iterations 35: statistics at 15..35 every 5, optimisation at
+    20 and 30), then a second estimate() of the same model.  Mallet 2.0.7's
+    estimate() builds new WorkerRunnables and calls initializeAlphaStatistics
+    on each, so the statistics of sweep 35 die with the first call's runnables
+    and the second call starts its schedule (iteration 1.., burn-in again)
+    with empty histograms; the oracle schedule restates exactly that."""
+    c = synthetic_lda(num_docs=220, num_types=600, num_topics=12, doc_len=None, mean_len=45,
+                      min_len=1, max_len=150, seed=19)
+    V, K, seed = c.num_types, 16, 6
+    rng = np.random.default_rng(12)
+    z0 = rng.integers(0, K, c.num_tokens).astype(np.int32)
+    alpha0 = np.full(K, 8.0 / K)
+    hyper0 = np.array([8.0, 0.05, 0.05 * V])
+    iters, interval, burnin, save = 35, 10, 10, 5
+    out1 = _run(K, V, c, z0, alpha0, hyper0, 0, [iters, burnin, interval, save, 0, 2, 0], seed)
+    o, alpha, alpha_sum, beta, ll = _oracle_schedule(oracle, c, V, K, z0, alpha0, 8.0, 0.05, seed, 0,
+                                                     iters, interval, burnin, save)
+    _check(out1, o, alpha, alpha_sum, beta, ll, K, V, iters)
+    iters2 = 20
+    out2 = _run(K, V, c, out1["z"], out1["alpha"], out1["hyper"], out1["sweep"],
+                [iters2, burnin, interval, save, 0, 2, 0], seed)
+    o2, alpha2, alpha_sum2, beta2, ll2 = _oracle_schedule(
+        oracle, c, V, K, out1["z"], out1["alpha"], out1["hyper"][0], out1["hyper"][1], seed,
+        iters, iters2, interval, burnin, save)
+    _check(out2, o2, alpha2, alpha_sum2, beta2, ll2, K, V, iters2)
+    assert out2["sweep"] == iters + iters2

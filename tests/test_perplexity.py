@@ -10,9 +10,13 @@ src/cmu_ron/TrainAndPredict.java:144), and the other half is scored:
 perplexity = exp(-sum log sum_k theta_dk phi_kw / N_scored).
 
 The posterior is multimodal: at K=20 about 30% of seeds end in a local
-optimum 5-12% worse, in cpu_mallet (28 of 96 seeds) as in the GPU kernels,
-so a few seeds measure which seeds fell in, not the sampler.  The GPU leg
-runs SEEDS = 1..96 here; cpu_mallet's 96 per-seed values are the committed
+optimum 5-12% worse (cpu_mallet: 28 of 96 seeds), so a few seeds measure
+which seeds fell in, not the sampler.  Sampling every document against one
+snapshot from the random start falls in more often (41-44 of 96 seeds for
+the full- and quarter-wave kernels, profiles/r03/ppl/stats_k20.json), so the
+GPU leg trains with the product's warm start: sweeps 0..49 in 4 sequential
+parts (lda_set_warm_start; ParallelTopicModel's default).  The GPU leg runs
+SEEDS = 1..96 here; cpu_mallet's 96 per-seed values are the committed
 fixture tests/golden/mallet_ppl_k{K}.json (tools/ppl_mallet_seeds.py: the
 restatement trained on the CPU with 4 threads, scored by cpu_exact with the
 same estimator and the GPU default kernel's inference draw).  Bars, each
@@ -60,6 +64,7 @@ def _perplexity(sampler, held_obs, held_sc, oracle):
 
 
 SEEDS = range(1, 97)
+WARM = (4, 50)        # the training loop's default warm start (ParallelTopicModel.setWarmStart)
 TRAP = 1.02
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 
@@ -90,6 +95,7 @@ def test_heldout_perplexity_within_1pct(oracle, K):
     pg = []
     for seed in SEEDS:
         g = GibbsSampler(K, c.num_types, train.doc_off, train.words, alpha, BETA, seed=seed)
+        g.set_warm_start(*WARM)
         g.sweep(1000)
         pg.append(_perplexity(g, held_obs, held_sc, oracle))
         g.close()

@@ -5,7 +5,7 @@ cd "$GRAFT_REPO_ROOT"
 O=gpurun_out/r3c; mkdir -p $O
 export TMPDIR=/tmp
 timeout -k 10 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread \
-  tests/test_recount_gpu.py tests/test_topic_model_gpu.py tests/test_distributed_gpu.py > $O/pytest.log 2>&1 || { echo "PYTEST FAILED"; tail -30 $O/pytest.log; exit 1; }
+  tests/test_recount_gpu.py tests/test_topic_model_gpu.py tests/test_distributed_gpu.py tests/test_hyper_gpu.py tests/test_parity_gpu.py tests/test_jni_harness_gpu.py > $O/pytest.log 2>&1 || { echo "PYTEST FAILED"; tail -30 $O/pytest.log; exit 1; }
 tail -2 $O/pytest.log
 for cfg in c2 c3; do
   for b in 3 7 12 17 22; do

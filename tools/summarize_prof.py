@@ -1,7 +1,11 @@
 #!/usr/bin/env python3
 """Condense rocprofv3 CSV output into small per-kernel summaries.
 
-  summarize_prof.py <prof_dir> <out.json>
+  summarize_prof.py <prof_dir> <out.json> [skip]
+
+skip: leave out each kernel's first `skip` dispatches (in dispatch order), so
+that a profile of a bench command describes the bench's own timed sweeps
+(skip = --burnin + --warmup of that command, tools/profile.sh).
 
 Reads every *_kernel_stats.csv, *_kernel_trace.csv and
 *_counter_collection.csv under prof_dir and writes, per kernel name:
@@ -33,15 +37,17 @@ def short(name: str) -> str:
     return name.split("(")[0][:80]
 
 
-def main(prof_dir, out_path):
-    out = {"kernels": {}, "counters": {}}
+def main(prof_dir, out_path, skip=0):
+    skip = int(skip)
+    out = {"kernels": {}, "counters": {}, "skipped_dispatches_per_kernel": skip}
     for path in glob.glob(os.path.join(prof_dir, "**", "*_kernel_trace.csv"), recursive=True):
         agg = defaultdict(list)
         with open(path) as f:
             for row in csv.DictReader(f):
                 dur = int(row["End_Timestamp"]) - int(row["Start_Timestamp"])
-                agg[short(row["Kernel_Name"])].append(dur)
+                agg[short(row["Kernel_Name"])].append((int(row["Start_Timestamp"]), dur))
         for k, v in agg.items():
+            v = [d for _, d in sorted(v)[skip:]] or [d for _, d in sorted(v)]
             v.sort()
             out["kernels"][k] = {
                 "calls": len(v),
@@ -65,7 +71,8 @@ def main(prof_dir, out_path):
                 per_dispatch = defaultdict(float)
                 for disp, v in vals:
                     per_dispatch[disp] += v
-                xs = list(per_dispatch.values())
+                ids = sorted(per_dispatch)
+                xs = [per_dispatch[i] for i in (ids[skip:] or ids)]
                 d[c] = {"dispatches": len(xs), "avg_per_dispatch": sum(xs) / len(xs),
                         "min": min(xs), "max": max(xs)}
     for k, ctrs in out["counters"].items():
@@ -79,4 +86,4 @@ def main(prof_dir, out_path):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1], sys.argv[2])
+    main(*sys.argv[1:4])
