@@ -167,9 +167,15 @@ lda_status lda_delta_buffer_part(lda_ctx* ctx, int32_t part, void** dev_ptr, siz
  * and is never a recount sweep.  lda_sample / lda_sweep do it by themselves;
  * a sharding driver asks lda_sweep_parts and, when sequential, runs for
  * each part: lda_sample_part(i), sum buffer 0 across ranks, lda_apply.
- * parts in [1, LDA_MAX_EXCHANGE_PARTS] (1 = off); results stay independent
- * of the number of ranks and identical to cpu_exact's same schedule. */
-lda_status lda_set_warm_start(lda_ctx* ctx, int32_t parts, int32_t sweeps);
+ * parts in [1, LDA_MAX_EXCHANGE_PARTS] (1 = off).  The parts are cut in
+ * the whole corpus, global token indices [corpus_first_token,
+ * corpus_first_token + corpus_tokens) (corpus_tokens <= 0: this shard is the
+ * whole corpus): part i is the documents starting at or after token
+ * first + tokens * i / parts (and before the next cut), so a shard samples
+ * its own documents of global part i in step i, and the result is the same
+ * for any sharding and identical to cpu_exact's same schedule. */
+lda_status lda_set_warm_start(lda_ctx* ctx, int32_t parts, int32_t sweeps, int64_t corpus_first_token,
+                              int64_t corpus_tokens);
 lda_status lda_get_warm_start(lda_ctx* ctx, int32_t* parts, int32_t* sweeps);
 /* The parts of the sweep in progress (or of the next one) and whether they
  * are sequential (a warm-start sweep) or exchange-overlapped. */

@@ -88,32 +88,50 @@ std::vector<int64_t> make_ranges(const std::vector<int64_t>& off, int64_t target
   return r;
 }
 
-// The work ranges of a split sweep: documents cut into `parts` token-balanced
-// spans, each span grouped by make_ranges on its own (its own short tail).
-// part_range[i] is the index of part i's first range.  parts == 1 gives
-// exactly make_ranges(off, target).
-std::vector<int64_t> make_part_ranges(const std::vector<int64_t>& off, int64_t target, int parts,
-                                      std::vector<int64_t>& part_range) {
+// Document cuts of `parts` token-balanced parts of a corpus whose tokens are
+// global indices [g0, g0 + gn), seen from a shard whose documents start at
+// global token base + off[d]: cut i (0 < i < parts) is the first local
+// document starting at or after g0 + gn * i / parts.  With (g0, gn) = the
+// shard itself these are the shard's own cuts; with the whole corpus every
+// shard cuts where a single context over all of it would.
+std::vector<int64_t> part_cuts(const std::vector<int64_t>& off, int parts, int64_t base, int64_t g0,
+                               int64_t gn) {
   const int64_t D = (int64_t)off.size() - 1;
+  std::vector<int64_t> cuts{0};
+  for (int i = 1; i < parts; ++i) {
+    const int64_t tgt = g0 + gn * i / parts - base;
+    int64_t d = std::lower_bound(off.begin(), off.end(), tgt) - off.begin();
+    cuts.push_back(std::min(std::max(d, cuts.back()), D));
+  }
+  cuts.push_back(D);
+  return cuts;
+}
+
+// The work ranges of documents cut into parts (cuts[0] = 0 .. cuts[P] = D),
+// each part grouped by make_ranges on its own (its own short tail).
+// part_range[i] is the index of part i's first range.
+std::vector<int64_t> make_cut_ranges(const std::vector<int64_t>& off, int64_t target,
+                                     const std::vector<int64_t>& cuts, std::vector<int64_t>& part_range) {
   std::vector<int64_t> r{0};
   part_range.assign(1, 0);
-  int64_t d_begin = 0;
-  for (int i = 0; i < parts; ++i) {
-    int64_t d_end = D;
-    if (i + 1 < parts) {
-      const int64_t tgt = off[0] + (off[D] - off[0]) * (i + 1) / parts;
-      d_end = std::lower_bound(off.begin(), off.end(), tgt) - off.begin();
-      d_end = std::min(std::max(d_end, d_begin), D);
-    }
+  for (size_t i = 0; i + 1 < cuts.size(); ++i) {
+    const int64_t d_begin = cuts[i], d_end = cuts[i + 1];
     if (d_end > d_begin) {
       const std::vector<int64_t> sub(off.begin() + d_begin, off.begin() + d_end + 1);
       const std::vector<int64_t> rr = make_ranges(sub, target);
       for (size_t j = 1; j < rr.size(); ++j) r.push_back(d_begin + rr[j]);
     }
     part_range.push_back((int64_t)r.size() - 1);
-    d_begin = d_end;
   }
   return r;
+}
+
+// A split sweep's ranges: the shard's own token-balanced cuts.  parts == 1
+// gives exactly make_ranges(off, target).
+std::vector<int64_t> make_part_ranges(const std::vector<int64_t>& off, int64_t target, int parts,
+                                      std::vector<int64_t>& part_range) {
+  const int64_t D = (int64_t)off.size() - 1;
+  return make_cut_ranges(off, target, part_cuts(off, parts, 0, off[0], off[D] - off[0]), part_range);
 }
 
 template <typename T>
@@ -927,16 +945,22 @@ lda_status lda_recount_times(lda_ctx* c, int32_t max, float* ms, int32_t* n) {
   });
 }
 
-lda_status lda_set_warm_start(lda_ctx* c, int32_t parts, int32_t sweeps) {
+lda_status lda_set_warm_start(lda_ctx* c, int32_t parts, int32_t sweeps, int64_t corpus_first_token,
+                              int64_t corpus_tokens) {
   return lda_abi::guarded([&]() -> lda_status {
   if (!c) return fail(LDA_ERR_INVALID_ARG, "null ctx");
   if (parts < 1 || parts > LDA_MAX_EXCHANGE_PARTS || sweeps < 0)
     return fail(LDA_ERR_INVALID_ARG, "parts must be in [1, LDA_MAX_EXCHANGE_PARTS], sweeps >= 0");
   if (c->next_part != 0) return fail(LDA_ERR_STATE, "inside a split sweep");
+  if (corpus_tokens <= 0) {          // this shard is the whole corpus
+    corpus_first_token = c->token_base;
+    corpus_tokens = c->N;
+  }
   HIP_TRY(hipSetDevice(c->device));
   if (parts > 1) {
     std::vector<int64_t> pr;
-    std::vector<int64_t> ranges = make_part_ranges(c->doc_off_h, c->tokens_per_range, parts, pr);
+    const std::vector<int64_t> cuts = part_cuts(c->doc_off_h, parts, c->token_base, corpus_first_token, corpus_tokens);
+    std::vector<int64_t> ranges = make_cut_ranges(c->doc_off_h, c->tokens_per_range, cuts, pr);
     int64_t* dr = nullptr;
     HIP_TRY(dalloc(&dr, ranges.size()));
     hipError_t e = hipMemcpyAsync(dr, ranges.data(), sizeof(int64_t) * ranges.size(), hipMemcpyHostToDevice, c->stream);

@@ -343,7 +343,8 @@ void ParallelTopicModel::setWarmStart(int32_t parts, int32_t sweeps) {
   warm_parts_ = parts;
   warm_sweeps_ = sweeps;
   if (shards_ && !shards_dirty_)
-    for (auto c : shards_->ctx) check(lda_set_warm_start(c, warm_parts_, warm_sweeps_), "lda_set_warm_start");
+    for (auto c : shards_->ctx)
+      check(lda_set_warm_start(c, warm_parts_, warm_sweeps_, 0, numTokens()), "lda_set_warm_start");
 }
 
 void ParallelTopicModel::setDevices(const int32_t* devices, int32_t n) {
@@ -481,7 +482,8 @@ void ParallelTopicModel::ensureShards() {
   sg->reduce();
   sg->apply();
   sg->set_parts(exchange_parts_);
-  for (auto c : sg->ctx) check(lda_set_warm_start(c, warm_parts_, warm_sweeps_), "lda_set_warm_start");
+  // warm-start parts cut in the whole corpus: the same sweeps for any shard count
+  for (auto c : sg->ctx) check(lda_set_warm_start(c, warm_parts_, warm_sweeps_, 0, N), "lda_set_warm_start");
   for (auto c : sg->ctx) check(lda_set_sweep(c, sweep_), "lda_set_sweep");
   shards_ = std::move(sg);
   shards_dirty_ = false;

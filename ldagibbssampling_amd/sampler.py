@@ -180,10 +180,13 @@ class GibbsSampler:
                                              C.byref(n)), "lda_recount_times")
         return ms[:n.value]
 
-    def set_warm_start(self, parts: int = 4, sweeps: int = 50):
-        """lda_set_warm_start: the first `sweeps` sweeps after the counts are
-        seeded run in `parts` sequential parts (parts = 1: off)."""
-        capi.check(self._L.lda_set_warm_start(self._h, int(parts), int(sweeps)), "lda_set_warm_start")
+    def set_warm_start(self, parts: int = 4, sweeps: int = 50, corpus_first_token: int = 0,
+                       corpus_tokens: int = 0):
+        """lda_set_warm_start: sweeps whose sweep counter is below `sweeps` run in
+        `parts` sequential parts (parts = 1: off), cut in the whole corpus of
+        global tokens [corpus_first_token, + corpus_tokens) (0: this shard)."""
+        capi.check(self._L.lda_set_warm_start(self._h, int(parts), int(sweeps), int(corpus_first_token),
+                                              int(corpus_tokens)), "lda_set_warm_start")
 
     def sweep_parts(self):
         """(parts, sequential) of the sweep in progress or the next one."""

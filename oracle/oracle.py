@@ -193,6 +193,7 @@ class ExactSampler:
                                          alpha, float(beta), int(seed) & (2**64 - 1), int(token_base))
         self.Kp = int(lib().orc_exact_kpad(self._h))
         self._pending = True      # create leaves the shard's counts as the pending delta
+        self.token_base = int(token_base)
         lib().orc_exact_set_kind(self._h, {"dense": 0, "dense32": 0, "sparse": 1}[kind])
         if half is None:
             half = os.environ.get("LDA_DENSE_HALF", "2")[:1]
@@ -211,24 +212,26 @@ class ExactSampler:
         n = self.V * self.Kp + self.Kp
         return np.ctypeslib.as_array(p, shape=(n,))
 
-    def set_warm_start(self, parts: int, sweeps: int):
+    def set_warm_start(self, parts: int, sweeps: int, corpus_first_token: int = 0, corpus_tokens: int = 0):
         """lda_set_warm_start: sweeps whose sweep counter is below `sweeps` run in
         `parts` sequential parts (token-balanced document cuts as
         lda_capi.cpp's make_part_ranges), each applied before the next."""
         self._warm = (int(parts), int(sweeps) if parts > 1 else 0)
+        if corpus_tokens <= 0:                      # this shard is the whole corpus
+            corpus_first_token, corpus_tokens = self.token_base, self.N
+        self._warm_corpus = (int(corpus_first_token), int(corpus_tokens))
 
     def _warm_cuts(self):
+        """lda_capi.cpp part_cuts: cut i = the first document starting at or
+        after global token g0 + gn * i // P."""
         P = self._warm[0]
-        off = self.doc_off
-        n = int(off[-1] - off[0])
-        cuts, d0 = [0], 0
-        for i in range(P):
-            d1 = self.D
-            if i + 1 < P:
-                d1 = int(np.searchsorted(off, off[0] + n * (i + 1) // P, side="left"))
-                d1 = min(max(d1, d0), self.D)
-            cuts.append(d1)
-            d0 = d1
+        g0, gn = self._warm_corpus
+        off = self.doc_off - self.doc_off[0]
+        cuts = [0]
+        for i in range(1, P):
+            d = int(np.searchsorted(off, g0 + gn * i // P - self.token_base, side="left"))
+            cuts.append(min(max(d, cuts[-1]), self.D))
+        cuts.append(self.D)
         return cuts
 
     def sample(self, frozen=False):
