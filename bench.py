@@ -487,6 +487,15 @@ def main():
                 "kernel": f"{kname}<C={sampler.Kp // 64}> avg {kern_ms:.3f} ms/launch over "
                           f"{n_local} tokens",
                 "issue": issue_roofline(rec, tok_s_kernel),
+                # what the kernel actually hits: the dense rows are
+                # a random-row gather that the 256 MB Infinity Cache largely holds
+                # (C4: 102 MB of 16-bit rows), so "hbm" names the memory path's
+                # roofline, not HBM-resident bytes; the issue fraction is the other
+                # ceiling the token's dependency chain runs into
+                "ceiling": ("random-row gather of the word rows (Infinity-Cache resident when "
+                            "they fit: 2 V Kp bytes <= 256 MB) + instruction issue / dependency "
+                            "chain; see issue.frac" if args.sampler != "sparse" else
+                            "streamed nonzero entries of long rows + scalar issue; see issue.frac"),
             },
             "collective": coll,
             "ll_per_token": ll / tokens_all,

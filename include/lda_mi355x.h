@@ -118,8 +118,9 @@ lda_status lda_count_update_mode(lda_ctx* ctx, int32_t* recount);
  *                     ones keep a delta (near init nearly every token
  *                     changes, and the delta's device atomics cost more than
  *                     the recount; later they cost less).  The default is
- *                     LDA_RECOUNT_SWEEPS_DEFAULT when the shard's z fits the
- *                     Infinity Cache (4 N <= 256 MiB), else 0.
+ *                     LDA_RECOUNT_SWEEPS_DEFAULT when K <= 128 and the
+ *                     shard's z fits the Infinity Cache (4 N <= 256 MiB),
+ *                     else 0 (measured crossover: DESIGN.md §4).
  *                     recount_sweeps < 0 keeps the current value.
  *  LDA_COUNT_RECOUNT  every sweep;  LDA_COUNT_DELTA  none.
  * Shards exchanging buffers must agree on it sweep by sweep: a distributed
@@ -128,7 +129,7 @@ lda_status lda_count_update_mode(lda_ctx* ctx, int32_t* recount);
 #define LDA_COUNT_AUTO 0
 #define LDA_COUNT_RECOUNT 1
 #define LDA_COUNT_DELTA 2
-#define LDA_RECOUNT_SWEEPS_DEFAULT 10
+#define LDA_RECOUNT_SWEEPS_DEFAULT 20
 lda_status lda_set_count_update(lda_ctx* ctx, int32_t mode, int32_t recount_sweeps);
 lda_status lda_get_count_update(lda_ctx* ctx, int32_t* mode, int32_t* recount_sweeps);
 /* nw/nwsum := buffer (recount) or += buffer (delta), buffer = 0, refresh the

@@ -568,13 +568,16 @@ lda_status lda_create(lda_ctx** out, const lda_config* cfg, const int64_t* doc_o
   c->waves_per_block = lda::sample_waves_per_block(c->C, c->sampler == LDA_SAMPLER_SPARSE, c->half);
   {
     // the dense samplers can recount (a uint32 index: < 2^32 tokens).  AUTO
-    // recounts the first LDA_RECOUNT_SWEEPS_DEFAULT sweeps when z fits the
-    // 256 MB Infinity Cache (the recount gathers z through the index: C2 near
-    // init 1.62 -> 1.43 ms per sweep; C4's 1 GB z makes the gathers cost more
-    // than the atomics they replace).  LDA_RECOUNT=0 / 1 forces
-    // the delta / recount mode (A/B runs).
+    // recounts the first LDA_RECOUNT_SWEEPS_DEFAULT sweeps of a K <= 128
+    // shard whose z fits the 256 MB Infinity Cache: C2 1.64 -> 1.46 ms per
+    // sweep at sweep 3, 1.50 -> 1.36 at sweep 17, a loss by sweep 30 (1.03 ->
+    // 1.36); at K = 1024 (C3) the atomics cost no more than the recount, and
+    // C4's 1 GB z makes its gathers cost more than the atomics they replace
+    // (profiles/r03/crossover/).  LDA_RECOUNT=0 / 1 forces the
+    // delta / recount mode (A/B runs).
     c->recount_ok = c->sampler == LDA_SAMPLER_DENSE && N < (int64_t(1) << 32);
-    c->recount_sweeps = c->recount_ok && N * 4 <= (int64_t(256) << 20) ? LDA_RECOUNT_SWEEPS_DEFAULT : 0;
+    c->recount_sweeps = c->recount_ok && c->Kp <= 128 && N * 4 <= (int64_t(256) << 20)
+                            ? LDA_RECOUNT_SWEEPS_DEFAULT : 0;
     const char* rv = std::getenv("LDA_RECOUNT");
     if (rv && rv[0] == '0') c->count_mode = LDA_COUNT_DELTA;
     if (rv && rv[0] == '1') c->count_mode = LDA_COUNT_RECOUNT;

@@ -194,6 +194,17 @@ __device__ __forceinline__ int64_t uniform_l(int64_t v) {
 // instructions of one wave already execute in order, so it costs nothing.
 __device__ __forceinline__ void wave_lds_fence() { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront"); }
 
+// The next work range of a consumer (a wave, or a 16-lane row of the
+// quarter-wave kernel): its first is static -- consumer `id` of `count`
+// takes range id -- and later ones come from the queue, offset by count.
+// A launch's first grab was a burst of same-address atomics from every
+// consumer at once; a small corpus (C1: ~1000 ranges, one per wave) now
+// takes none.  Which consumer samples which range never changes a result
+// (draws are keyed by the global token index).
+__device__ __forceinline__ int first_or_queued(bool first, int id, int count, int queued) {
+  return first ? id : count + queued;
+}
+
 template <int C>
 __device__ __forceinline__ void load_row(int32_t (&r)[C], const int32_t* __restrict__ p) {
   if constexpr (C >= 4) {
@@ -348,10 +359,12 @@ void k_sample(SampleParams p) {
   const int32_t* __restrict__ nw = p.nw;
   const float* __restrict__ inv_m1 = p.inv_m1;
 
+  bool first_range = true;
   while (true) {
     int r = 0;
-    if (lane == 0) r = atomicAdd(p.queue, 1);
-    r = uniform_i(__shfl(r, 0));
+    if (!first_range && lane == 0) r = atomicAdd(p.queue, 1);
+    r = first_or_queued(first_range, (int)blockIdx.x * 4 + wid, (int)gridDim.x * 4, uniform_i(__shfl(r, 0)));
+    first_range = false;
     if (r >= p.num_ranges) break;
     const int64_t d0 = p.range_doc[r], d1 = p.range_doc[r + 1];
     const int64_t t0 = p.doc_off[d0];
@@ -1184,6 +1197,7 @@ __global__ __launch_bounds__(256) QUARTER_ATTR void k_sample_quarter(SampleParam
   int64_t t0 = 0, doc = 0;
   int nt = 0, t = 0, cbase = 0, doc_end = 0, ev = 0, kp = 0, inc = 0;
   int active = 1, loaded = 0;
+  bool first_range = true;                           // per row (lane-varying)
   // chunk registers: row-lane i <-> token cbase + i of the quarter's range
   int cw = 0, cz = 0, cn = 0, w1 = 0, z1 = 0, w2 = 0, z2 = 0, pw = 0;
   float cu = 0.0f;
@@ -1222,8 +1236,10 @@ __global__ __launch_bounds__(256) QUARTER_ATTR void k_sample_quarter(SampleParam
             loaded = 0;
             while (true) {
               int r = 0;
-              if (ql == 0) r = atomicAdd(p.queue, 1);
-              r = row_get_i(r, rb, 0);
+              if (!first_range && ql == 0) r = atomicAdd(p.queue, 1);
+              r = first_or_queued(first_range, ((int)blockIdx.x * 4 + wid) * 4 + (lane >> 4),
+                                  (int)gridDim.x * 16, row_get_i(r, rb, 0));
+              first_range = false;
               if (r >= p.num_ranges) {
                 active = 0;
                 ev = -1;
@@ -1502,10 +1518,12 @@ __global__ __launch_bounds__(256) void k_sample_sparse(SampleParams p) {
   const int64_t* __restrict__ row_off = p.row_off;
   const int32_t* __restrict__ row_nnz = p.row_nnz;
 
+  bool first_range = true;
   while (true) {
     int r = 0;
-    if (lane == 0) r = atomicAdd(p.queue, 1);
-    r = uniform_i(__shfl(r, 0));
+    if (!first_range && lane == 0) r = atomicAdd(p.queue, 1);
+    r = first_or_queued(first_range, (int)blockIdx.x * 4 + wid, (int)gridDim.x * 4, uniform_i(__shfl(r, 0)));
+    first_range = false;
     if (r >= p.num_ranges) break;
     const int64_t d0 = p.range_doc[r], d1 = p.range_doc[r + 1];
     const int64_t t0 = p.doc_off[d0], t1 = p.doc_off[d1];
@@ -1890,10 +1908,12 @@ __global__ __launch_bounds__(64 * sb_waves<C>()) void k_sample_sparse_big(Sample
     return t;
   };
 
+  bool first_range = true;
   while (true) {
     int r = 0;
-    if (lane == 0) r = atomicAdd(p.queue, 1);
-    r = uniform_i(__shfl(r, 0));
+    if (!first_range && lane == 0) r = atomicAdd(p.queue, 1);
+    r = first_or_queued(first_range, (int)blockIdx.x * WB + wid, (int)gridDim.x * WB, uniform_i(__shfl(r, 0)));
+    first_range = false;
     if (r >= p.num_ranges) break;
     const int64_t d0 = p.range_doc[r], d1 = p.range_doc[r + 1];
     const int64_t t0 = p.doc_off[d0], t1 = p.doc_off[d1];
