@@ -36,6 +36,11 @@ CONFIGS = {
     # inverse_docs corpus; K=20, alphaSum 10 as src/cmu, 100 sweeps)
     "c1": dict(docs=2_000, doc_len=None, V=5_000, K=20, alpha_sum=10.0, steps=100,
                desc="C1: changelist-shaped corpus, 2000 docs x Poisson(8) tok, Zipf(1.1) over 5000 paths, K=20"),
+    # the same corpus at the reference's own training settings
+    "c1cmu": dict(docs=2_000, doc_len=None, V=5_000, K=100, alpha_sum=10.0, beta=0.001, steps=100,
+                  desc="C1 corpus at src/cmu/TrainAndPredict.java:259 settings: K=100, alphaSum 10, beta 0.001"),
+    "c1ron": dict(docs=2_000, doc_len=None, V=5_000, K=500, alpha_sum=100.0, beta=1.0, steps=100,
+                  desc="C1 corpus at src/cmu_ron/TrainAndPredict.java:160 settings: K=500, alphaSum 100, beta 1"),
     # the headline: the whole C4 corpus, 8 blocks of 1.25M docs split over the ranks
     "c4": dict(docs=10_000_000, blocks=8, doc_len=200, V=100_000, K=512, scaling="strong",
                desc="C4: 10M docs x 200 tok (2e9 tokens), V=100k, K=512, documents split over the GPUs"),
@@ -279,7 +284,7 @@ def main():
         args.steps = cfg.get("steps", 10)
     K, V, L = cfg["K"], cfg["V"], cfg["doc_len"]
     docs = args.docs or cfg["docs"]
-    alpha_sum, beta = cfg.get("alpha_sum", 0.1 * K), 0.01
+    alpha_sum, beta = cfg.get("alpha_sum", 0.1 * K), cfg.get("beta", 0.01)
     t_gen = time.perf_counter()
     token_base = None
     blocks_info = None
@@ -304,7 +309,7 @@ def main():
         token_base = b0 * per_block * L
         blocks_info = {"blocks": nb, "docs_per_block": per_block, "doc_seeds": "20261015 + block",
                        "rank0_blocks": [0, nb // world]}
-    elif args.config == "c1":
+    elif args.config.startswith("c1"):
         from ldagibbssampling_amd.corpus import synthetic_changelists
         corpus = synthetic_changelists(num_docs=docs, num_types=V, seed=20261015 + rank)
         V = corpus.num_types          # the alphabet: paths seen in this shard
@@ -319,7 +324,7 @@ def main():
                            seed=1, device=device,
                            # unique Philox counters per rank (c1 shards differ in size)
                            token_base=(token_base if token_base is not None else
-                                       (rank << 32) if args.config == "c1" else rank * n_local),
+                                       (rank << 32) if args.config.startswith("c1") else rank * n_local),
                            tokens_per_range=args.tokens_per_range, sampler=args.sampler)
     # one non-default stream carries the sampler kernels and (as torch's
     # current stream) orders the all-reduce behind them: no host sync per sweep.
@@ -442,7 +447,7 @@ def main():
             "vs_baseline": None,
             "dtype": "fp32 weights / int32 counts",
             "data": ("synthetic (changelist-shaped inverse_docs corpus, SURVEY.md §8d; corpus.synthetic_changelists)"
-                     if args.config == "c1" else
+                     if args.config.startswith("c1") else
                      "synthetic (LDA generative process, SURVEY.md §8d; phi~Dir(0.01), theta~Dir(0.1))"),
             "config": {
                 "workload": cfg["desc"],

@@ -1833,6 +1833,10 @@ __global__ __launch_bounds__(256) void k_sample_sparse(SampleParams p) {
 #ifndef SB_NB
 #define SB_NB 2
 #endif
+// the batch loop specialised on the row's saturation flag (0: A/B baseline)
+#ifndef SB_SAT_SPLIT
+#define SB_SAT_SPLIT 1
+#endif
 static_assert(SB_RB % SB_GRP == 0 && SB_BATCH % SB_GRP == 0, "round groups");
 template <int C>
 constexpr int sb_waves() { return 16; }
@@ -1916,27 +1920,34 @@ __global__ __launch_bounds__(64 * sb_waves<C>()) void k_sample_sparse_big(Sample
     first_range = false;
     if (r >= p.num_ranges) break;
     const int64_t d0 = p.range_doc[r], d1 = p.range_doc[r + 1];
-    const int64_t t0 = p.doc_off[d0], t1 = p.doc_off[d1];
-    if (t1 <= t0) continue;
+    const int64_t t0 = p.doc_off[d0];
+    // token positions below are 32-bit offsets from the range start (64-bit
+    // compares and adds cost two scalar instructions each, and the scalar
+    // unit binds this kernel)
+    const int t1 = (int)(p.doc_off[d1] - t0);
+    if (t1 <= 0) continue;
+    const int32_t* __restrict__ wrd = p.words + t0;
+    int32_t* __restrict__ zr = p.z + t0;
+    const uint64_t gbase = (uint64_t)(p.token_base + t0);
 
-    int64_t cbase = t0;
+    int cbase = 0;
     int cw = 0, cz = 0, w1 = 0, z1 = 0, w2 = 0, z2 = 0;
-    if (t0 + lane < t1) {
-      cw = p.words[t0 + lane];
-      cz = p.z[t0 + lane];
+    if (lane < t1) {
+      cw = wrd[lane];
+      cz = zr[lane];
     }
-    if (t0 + 64 + lane < t1) {
-      w1 = p.words[t0 + 64 + lane];
-      z1 = p.z[t0 + 64 + lane];
+    if (64 + lane < t1) {
+      w1 = wrd[64 + lane];
+      z1 = zr[64 + lane];
     }
-    if (t0 + 128 + lane < t1) {
-      w2 = p.words[t0 + 128 + lane];
-      z2 = p.z[t0 + 128 + lane];
+    if (128 + lane < t1) {
+      w2 = wrd[128 + lane];
+      z2 = zr[128 + lane];
     }
     int cmn = row_nnz[cw], m1n = row_nnz[w1];
     int64_t cmo = row_off[cw], m1o = row_off[w1];
     int cn = cz;
-    float cu = u01(draw_u32((uint64_t)(p.token_base + t0 + lane), p.c2, p.c3, p.k0, p.k1));
+    float cu = u01(draw_u32(gbase + (uint64_t)lane, p.c2, p.c3, p.k0, p.k1));
 
     // the chunk's count changes, lane i = token i: two delta and two nwsum
     // atomics when its topic changed (lanes past the range hold cz == cn)
@@ -1953,9 +1964,9 @@ __global__ __launch_bounds__(64 * sb_waves<C>()) void k_sample_sparse_big(Sample
     tg_t TG;
     // document start: every lane evaluates its own NG group trees serially
     // (the same additions as the row scan, element by element)
-    auto build_doc = [&](int64_t ts, int64_t te) {
-      for (int64_t i = ts + lane; i < te; i += 64) {
-        const int k = p.z[i];
+    auto build_doc = [&](int ts, int te) {
+      for (int i = ts + lane; i < te; i += 64) {
+        const int k = zr[i];
         atomicAdd(&nd2[k >> 1], (k & 1) ? 0x10000u : 1u);
       }
       wave_lds_fence();
@@ -1980,15 +1991,15 @@ __global__ __launch_bounds__(64 * sb_waves<C>()) void k_sample_sparse_big(Sample
 
     int64_t doc = d0;
     while (p.doc_off[doc + 1] <= t0) ++doc;
-    int64_t doc_end = p.doc_off[doc + 1];
-    build_doc(t0, doc_end);
+    int doc_end = uniform_i((int)(p.doc_off[doc + 1] - t0));
+    build_doc(0, doc_end);
 
     // ring slot of token t: t % NS; slot (t + NS - 1) % NS is refilled during t
     uint32_t ring[NS][SB_RB];
     float cinv[NS];
     // the first SB_RB rounds of token tp (< t1, at most 70 tokens past cbase)
-    auto prefetch = [&](uint32_t (&rg)[SB_RB], float& ci, int64_t tp) {
-      const int pidx = (int)(tp - cbase);
+    auto prefetch = [&](uint32_t (&rg)[SB_RB], float& ci, int tp) {
+      const int pidx = tp - cbase;
       int np, zp;
       int64_t op;
       if (pidx < 64) {
@@ -2010,17 +2021,17 @@ __global__ __launch_bounds__(64 * sb_waves<C>()) void k_sample_sparse_big(Sample
     };
 #pragma unroll
     for (int s = 0; s < NS - 1; ++s)
-      if (t0 + s < t1) prefetch(ring[s], cinv[s], t0 + s);
+      if (s < t1) prefetch(ring[s], cinv[s], s);
 
-    for (int64_t tb = t0; tb < t1; tb += NS) {
+    for (int tb = 0; tb < t1; tb += NS) {
 #pragma unroll
       for (int s = 0; s < NS; ++s) {
-        const int64_t t = tb + s;
+        const int t = tb + s;
         if (t < t1) {
-          int idx = (int)(t - cbase);
+          int idx = t - cbase;
           if (idx == 64) {
             flush_chunk();
-            p.z[cbase + lane] = cn;
+            zr[cbase + lane] = cn;
             cbase += 64;
             idx = 0;
             cw = w1;
@@ -2032,17 +2043,17 @@ __global__ __launch_bounds__(64 * sb_waves<C>()) void k_sample_sparse_big(Sample
             m1n = row_nnz[w1];
             m1o = row_off[w1];
             cn = cz;
-            cu = u01(draw_u32((uint64_t)(p.token_base + cbase + lane), p.c2, p.c3, p.k0, p.k1));
+            cu = u01(draw_u32(gbase + (uint64_t)(cbase + lane), p.c2, p.c3, p.k0, p.k1));
             if (cbase + 128 + lane < t1) {
-              w2 = p.words[cbase + 128 + lane];
-              z2 = p.z[cbase + 128 + lane];
+              w2 = wrd[cbase + 128 + lane];
+              z2 = zr[cbase + 128 + lane];
             }
           }
           if (t == doc_end) {
             clear_doc();
             ++doc;
-            while (p.doc_off[doc + 1] <= t) ++doc;
-            doc_end = p.doc_off[doc + 1];
+            while (p.doc_off[doc + 1] - t0 <= t) ++doc;
+            doc_end = uniform_i((int)(p.doc_off[doc + 1] - t0));
             build_doc(t, doc_end);
           }
 
@@ -2099,7 +2110,7 @@ __global__ __launch_bounds__(64 * sb_waves<C>()) void k_sample_sparse_big(Sample
           asm volatile("" : "+v"(acc)::"memory");
           {
             const int sp = (s + NS - 1) % NS;
-            const int64_t tp = t + NS - 1;
+            const int tp = t + NS - 1;
             if (tp < t1) prefetch(ring[sp], cinv[sp], tp);
           }
           // the rounds past SB_RB (long rows), streamed in batches; the
@@ -2108,28 +2119,42 @@ __global__ __launch_bounds__(64 * sb_waves<C>()) void k_sample_sparse_big(Sample
           float accb[SB_NB];
 #pragma unroll
           for (int i = 0; i < SB_NB; ++i) accb[i] = 0.0f;
-          int mb = 0;
-          for (int q0 = SB_RB; q0 < nr_all; q0 += SB_BATCH, ++mb) {
-            uint32_t eb[SB_BATCH];
-            const uint32_t* rp = ent + off + lane + q0 * 64;
+          // the batch loop specialised on the row's saturation flag (uniform),
+          // as the register rounds are: a runtime flag inside term_of made every
+          // batch term a divergent branch (exec-mask save/restore on the scalar
+          // unit, which binds this kernel)
+          auto batches = [&](bool sat) {
+            int mb = 0;
+            for (int q0 = SB_RB; q0 < nr_all; q0 += SB_BATCH, ++mb) {
+              uint32_t eb[SB_BATCH];
+              const uint32_t* rp = ent + off + lane + q0 * 64;
 #pragma unroll
-            for (int b = 0; b < SB_BATCH; ++b) eb[b] = (q0 + b < nr_all) ? rp[b * 64] : 0u;
+              for (int b = 0; b < SB_BATCH; ++b) eb[b] = (q0 + b < nr_all) ? rp[b * 64] : 0u;
 #pragma unroll
-            for (int b = 0; b < SB_BATCH; b += SB_GRP) {
-              if (q0 + b < nr_all) {
-                float tt[SB_GRP];
+              for (int b = 0; b < SB_BATCH; b += SB_GRP) {
+                if (q0 + b < nr_all) {
+                  float tt[SB_GRP];
 #pragma unroll
-                for (int g = 0; g < SB_GRP; ++g) tt[g] = term_of(eb[b + g], w, zc, invc, row_sat);
+                  for (int g = 0; g < SB_GRP; ++g) tt[g] = term_of(eb[b + g], w, zc, invc, sat);
 #pragma unroll
-                for (int g = 0; g < SB_GRP; ++g) {
-                  const float na = acc + tt[g];
-                  acc = (g == 0 || q0 + b + g < nr_all) ? na : acc;
+                  for (int g = 0; g < SB_GRP; ++g) {
+                    const float na = acc + tt[g];
+                    acc = (g == 0 || q0 + b + g < nr_all) ? na : acc;
+                  }
                 }
               }
-            }
 #pragma unroll
-            for (int i = 0; i < SB_NB; ++i) accb[i] = (mb == i) ? acc : accb[i];
+              for (int i = 0; i < SB_NB; ++i) accb[i] = (mb == i) ? acc : accb[i];
+            }
+          };
+#if SB_SAT_SPLIT
+          if (nr_all > SB_RB) {
+            if (!row_sat) batches(false);
+            else batches(true);
           }
+#else
+          batches(row_sat);
+#endif
           const float TB = wave_incl_scan(acc);
           const float TAs = wave_incl_scan(lane_total(TG));
           const float sumB = readlane_f(TB, 63);
@@ -2228,7 +2253,7 @@ __global__ __launch_bounds__(64 * sb_waves<C>()) void k_sample_sparse_big(Sample
       }
     }
     flush_chunk();
-    if (cbase + lane < t1) p.z[cbase + lane] = cn;
+    if (cbase + lane < t1) zr[cbase + lane] = cn;
     clear_doc();
   }
 }

@@ -145,3 +145,24 @@ def test_full_c4_single_context():
     assert np.isfinite(ll0) and np.isfinite(ll) and ll > ll0
     g.close()
     torch.cuda.empty_cache()
+
+
+@pytest.mark.parametrize("K,alpha_sum,beta", [(20, 10.0, 0.01), (500, 100.0, 1.0)])
+def test_c1_workload_bit_exact(oracle, K, alpha_sum, beta):
+    """BASELINE.json configs[0] at its size: 2000 changelist-shaped documents
+    (Poisson(8) paths, Zipf(1.1) over 5000 paths), 100 sweeps, bit-exact
+    z / nw / nwsum against cpu_exact -- at C1's K = 20 (quarter-wave kernel)
+    and at src/cmu_ron's K = 500 (full-wave k_sample<8>)."""
+    from ldagibbssampling_amd.corpus import synthetic_changelists
+    from ldagibbssampling_amd.sampler import GibbsSampler
+    c = synthetic_changelists(num_docs=2000, num_types=5000, seed=20261015)
+    alpha = np.full(K, alpha_sum / K)
+    g = GibbsSampler(K, c.num_types, c.doc_off, c.words, alpha, beta, seed=1)
+    o = oracle.ExactSampler(K, c.num_types, c.doc_off, c.words, alpha, beta, 1)
+    g.sweep(100)
+    o.sweep(100)
+    np.testing.assert_array_equal(g.z(), o.z())
+    gnw, gns, _, _ = g.counts()
+    onw, ons, _, _ = o.counts()
+    np.testing.assert_array_equal(gnw, onw)
+    np.testing.assert_array_equal(gns, ons)
