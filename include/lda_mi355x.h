@@ -119,8 +119,9 @@ lda_status lda_count_update_mode(lda_ctx* ctx, int32_t* recount);
  *                     changes, and the delta's device atomics cost more than
  *                     the recount; later they cost less).  The default is
  *                     LDA_RECOUNT_SWEEPS_DEFAULT when K <= 128 and the
- *                     shard's z fits the Infinity Cache (4 N <= 256 MiB),
- *                     else 0 (measured crossover: DESIGN.md §4).
+ *                     shard holds 2^20 <= N tokens with z fitting the
+ *                     Infinity Cache (4 N <= 256 MiB), else 0 (measured
+ *                     crossover: DESIGN.md §4).
  *                     recount_sweeps < 0 keeps the current value.
  *  LDA_COUNT_RECOUNT  every sweep;  LDA_COUNT_DELTA  none.
  * Shards exchanging buffers must agree on it sweep by sweep: a distributed

@@ -246,6 +246,10 @@ struct lda_ctx {
   // the device over sampled sweeps [doc lengths (L+1) | topics K x (L+1)]
   int32_t* stat_buf = nullptr;
   int32_t stat_len = -1;
+  // lda_count_histogram's device histogram, grow-only (an optimisation every
+  // 20 sweeps of a small corpus had paid a hipMalloc + hipFree each time)
+  int32_t* chist = nullptr;
+  size_t chist_cap = 0;
   // event pairs around the last LDA_TIME_RING sampler launches (lda_sample_times)
   static constexpr int LDA_TIME_RING = 256;
   hipEvent_t ev0[LDA_TIME_RING] = {}, ev1[LDA_TIME_RING] = {}, ev2[LDA_TIME_RING] = {};
@@ -268,6 +272,7 @@ struct lda_ctx {
       if (sl.done) (void)hipEventDestroy(sl.done);
     }
     if (stat_buf) (void)hipFree(stat_buf);
+    if (chist) (void)hipFree(chist);
     for (int i = 0; i < LDA_TIME_RING; ++i) {
       if (ev0[i]) (void)hipEventDestroy(ev0[i]);
       if (ev1[i]) (void)hipEventDestroy(ev1[i]);
@@ -576,7 +581,9 @@ lda_status lda_create(lda_ctx** out, const lda_config* cfg, const int64_t* doc_o
     // (profiles/r03/crossover/).  LDA_RECOUNT=0 / 1 forces the
     // delta / recount mode (A/B runs).
     c->recount_ok = c->sampler == LDA_SAMPLER_DENSE && N < (int64_t(1) << 32);
-    c->recount_sweeps = c->recount_ok && c->Kp <= 128 && N * 4 <= (int64_t(256) << 20)
+    // (and not for a small corpus: its few atomics cost less than a launch)
+    c->recount_sweeps = c->recount_ok && c->Kp <= 128 && N >= (int64_t(1) << 20) &&
+                                N * 4 <= (int64_t(256) << 20)
                             ? LDA_RECOUNT_SWEEPS_DEFAULT : 0;
     const char* rv = std::getenv("LDA_RECOUNT");
     if (rv && rv[0] == '0') c->count_mode = LDA_COUNT_DELTA;
@@ -1315,22 +1322,19 @@ lda_status lda_count_histogram(lda_ctx* c, int64_t max_count, int32_t* count_his
   if (c->pending) return fail(LDA_ERR_STATE, "histogram with a pending delta: call lda_apply first");
   HIP_TRY(hipSetDevice(c->device));
   const size_t n = (size_t)max_count + 1;
-  int32_t* buf = nullptr;
-  HIP_TRY(dalloc(&buf, n + 1));
-  std::vector<int32_t> h;
-  try {
-    h = host_vector<int32_t>(n + 1);
-  } catch (...) {
-    (void)hipFree(buf);
-    throw;
+  if (c->chist_cap < n + 1) {
+    if (c->chist) (void)hipFree(c->chist);
+    c->chist = nullptr;
+    c->chist_cap = 0;
+    HIP_TRY(dalloc(&c->chist, n + 1));
+    c->chist_cap = n + 1;
   }
-  hipError_t e = hipMemsetAsync(buf, 0, (n + 1) * sizeof(int32_t), c->stream);
-  if (e == hipSuccess)
-    e = lda::launch_count_hist(c->nw, c->V, c->K, c->Kp, max_count, buf, buf + n, c->stream);
-  if (e == hipSuccess) e = hipMemcpyAsync(h.data(), buf, (n + 1) * sizeof(int32_t), hipMemcpyDeviceToHost, c->stream);
-  if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
-  (void)hipFree(buf);
-  HIP_TRY(e);
+  int32_t* buf = c->chist;
+  std::vector<int32_t> h = host_vector<int32_t>(n + 1);
+  HIP_TRY(hipMemsetAsync(buf, 0, (n + 1) * sizeof(int32_t), c->stream));
+  HIP_TRY(lda::launch_count_hist(c->nw, c->V, c->K, c->Kp, max_count, buf, buf + n, c->stream));
+  HIP_TRY(hipMemcpyAsync(h.data(), buf, (n + 1) * sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
   if (h[n]) return fail(LDA_ERR_INVALID_ARG, "an nw cell exceeds max_count");
   for (size_t i = 0; i < n; ++i) count_hist[i] += h[i];
   return LDA_OK;

@@ -14,6 +14,14 @@ from oracle import oracle as O
 
 scale = float(sys.argv[1]) if len(sys.argv) > 1 else 1.0
 c = synthetic_changelists()
+# untimed: the HIP runtime and the kernels' code objects load on the process's
+# first GPU call (~2 s on a fresh box), which is not the estimate()
+w = tm.ParallelTopicModel(100, 10.0, 0.01)
+w.addInstances(tm.InstanceList.fromCorpus(c))
+w.setTopicDisplay(0, 0)
+w.setNumIterations(2)
+w.estimate()
+del w
 for name, K, asum, beta, sweeps in [("src/cmu", 100, 10.0, 0.001, 1000), ("src/cmu_ron", 500, 100.0, 1.0, 10000)]:
     sweeps = int(sweeps * scale)
     m = tm.ParallelTopicModel(K, asum, beta)
