@@ -250,6 +250,25 @@ struct lda_ctx {
   // 20 sweeps of a small corpus had paid a hipMalloc + hipFree each time)
   int32_t* chist = nullptr;
   size_t chist_cap = 0;
+  // lda_sweep's plain sweeps as hipGraphs of k x (sampler, apply), k <= 16:
+  // one launch for k sweeps instead of ~6 runtime calls per sweep (the
+  // reference's ~16k-token corpus is host-bound at ~45 us per sweep against
+  // ~32 us of kernels).  The sweep counter is read by the sampler from
+  // sweep_dev, which each apply advances; graphs are rebuilt when a captured
+  // argument changes (graph_key).
+  static constexpr int GRAPH_MAX = 16;
+  bool use_graphs = true;
+  uint32_t* sweep_dev = nullptr;
+  hipGraphExec_t graphs[GRAPH_MAX + 1] = {};
+  struct GraphKey {
+    const void* range_doc = nullptr;
+    int64_t R = -1;
+    float beta = 0.0f, vbeta = 0.0f;
+    hipStream_t stream = nullptr;
+    bool operator==(const GraphKey& o) const {
+      return range_doc == o.range_doc && R == o.R && beta == o.beta && vbeta == o.vbeta && stream == o.stream;
+    }
+  } graph_key;
   // event pairs around the last LDA_TIME_RING sampler launches (lda_sample_times)
   static constexpr int LDA_TIME_RING = 256;
   hipEvent_t ev0[LDA_TIME_RING] = {}, ev1[LDA_TIME_RING] = {}, ev2[LDA_TIME_RING] = {};
@@ -273,6 +292,9 @@ struct lda_ctx {
     }
     if (stat_buf) (void)hipFree(stat_buf);
     if (chist) (void)hipFree(chist);
+    for (auto& g : graphs)
+      if (g) (void)hipGraphExecDestroy(g);
+    if (sweep_dev) (void)hipFree(sweep_dev);
     for (int i = 0; i < LDA_TIME_RING; ++i) {
       if (ev0[i]) (void)hipEventDestroy(ev0[i]);
       if (ev1[i]) (void)hipEventDestroy(ev1[i]);
@@ -326,8 +348,9 @@ static lda_status build_row_capacity(lda_ctx* c) {
   HIP_TRY(e);
   std::vector<int64_t> off(c->V + 1);
   off[0] = 0;
-  // whole rounds of 64 entries (k_build_sparse zero-fills the padding)
-  for (int w = 0; w < c->V; ++w) off[w + 1] = off[w] + ((h[w] + 63) & ~int64_t(63));
+  // whole rounds of 64 entries, whole batches past the register rounds
+  // (lda::sparse_row_entries; k_build_sparse zero-fills the padding)
+  for (int w = 0; w < c->V; ++w) off[w + 1] = off[w] + lda::sparse_row_entries(h[w]);
   HIP_TRY(dalloc(&c->row_off, c->V + 1));
   HIP_TRY(dalloc(&c->row_nnz, c->V));
   HIP_TRY(dalloc(&c->ent, (size_t)off[c->V]));
@@ -620,6 +643,11 @@ lda_status lda_create(lda_ctx** out, const lda_config* cfg, const int64_t* doc_o
   CT(dalloc(&c->inv, c->Kp));
   CT(dalloc(&c->inv_m1, c->Kp));
   CT(dalloc(&c->partial, c->partial_blocks));
+  CT(dalloc(&c->sweep_dev, 1));
+  {
+    const char* gv = std::getenv("LDA_GRAPHS");
+    c->use_graphs = !(gv && gv[0] == '0');
+  }
   CT(dalloc(&c->nonzero, c->partial_blocks));
   for (int i = 0; i < lda_ctx::LDA_TIME_RING; ++i) {
     CT(hipEventCreate(&c->ev0[i]));
@@ -839,6 +867,7 @@ lda_status lda_set_exchange_parts(lda_ctx* c, int32_t parts, int32_t reserve_cus
   HIP_TRY(e);
   (void)hipFree(c->range_doc);
   c->range_doc = dr;
+  c->graph_key = lda_ctx::GraphKey{};   // the graphs captured the old ranges
   c->R = (int64_t)ranges.size() - 1;
   c->part_range = pr;
   c->ranges_h = ranges;
@@ -1038,6 +1067,55 @@ lda_status lda_delta_buffer(lda_ctx* c, void** dev_ptr, size_t* count) {
   });
 }
 
+// Can the next sweep run inside a graph?  A plain dense sweep: one part, not
+// a warm-start or recount sweep (and once one is, every later one is).
+static bool graph_eligible(const lda_ctx* c) {
+  return c->use_graphs && c->sampler == LDA_SAMPLER_DENSE && c->parts == 1 && c->R > 0 && !c->pending &&
+         c->next_part == 0 && !next_sweep_sequential(c) && !next_sweep_recounts(c);
+}
+
+// k x (sampler, apply) captured on the context's stream and instantiated once
+static lda_status sweep_graph(lda_ctx* c, int k, hipGraphExec_t* out) {
+  lda_ctx::GraphKey key;
+  key.range_doc = c->range_doc;
+  key.R = c->R;
+  key.beta = (float)c->beta;
+  key.vbeta = (float)((double)c->V * c->beta);
+  key.stream = c->stream;
+  if (!(key == c->graph_key)) {
+    for (auto& g : c->graphs)
+      if (g) {
+        (void)hipGraphExecDestroy(g);
+        g = nullptr;
+      }
+    c->graph_key = key;
+  }
+  if (!c->graphs[k]) {
+    lda::SampleParams p = c->params(false);
+    p.c2_dev = c->sweep_dev;
+    p.delta = c->delta;
+    p.dsum = c->delta + (int64_t)c->V * c->Kp;
+    const int64_t wpb = c->waves_per_block;
+    const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>(c->sample_blocks, (c->R + wpb - 1) / wpb));
+    lda::TopicTables t{c->nwsum, c->alpha_d, c->alpha_f, c->inv, c->inv_m1, key.vbeta, c->K, c->queue, 0,
+                       c->sweep_dev};
+    HIP_TRY(hipStreamBeginCapture(c->stream, hipStreamCaptureModeRelaxed));
+    hipError_t e = hipSuccess;
+    for (int i = 0; i < k && e == hipSuccess; ++i) {
+      e = lda::launch_sample(c->C, false, p, blocks, c->stream, c->half);
+      if (e == hipSuccess) e = lda::launch_apply_packed(c->nw, c->delta, c->V, c->Kp, c->nw16, c->wide, t, c->stream);
+    }
+    hipGraph_t g = nullptr;
+    const hipError_t e2 = hipStreamEndCapture(c->stream, &g);
+    if (e == hipSuccess) e = e2;
+    if (e == hipSuccess) e = hipGraphInstantiate(&c->graphs[k], g, nullptr, nullptr, 0);
+    if (g) (void)hipGraphDestroy(g);
+    HIP_TRY(e);
+  }
+  *out = c->graphs[k];
+  return LDA_OK;
+}
+
 lda_status lda_sweep(lda_ctx* c, int32_t n) {
   return lda_abi::guarded([&]() -> lda_status {
   if (!c) return fail(LDA_ERR_INVALID_ARG, "null ctx");
@@ -1046,11 +1124,30 @@ lda_status lda_sweep(lda_ctx* c, int32_t n) {
     lda_status s = apply_impl(c);
     if (s) return s;
   }
-  for (int32_t i = 0; i < n; ++i) {
+  for (int32_t i = 0; i < n;) {
+    if (graph_eligible(c)) {
+      // the rest as graphs of up to GRAPH_MAX sweeps
+      const int k = (int)std::min<int32_t>(n - i, lda_ctx::GRAPH_MAX);
+      hipGraphExec_t g = nullptr;
+      HIP_TRY(hipSetDevice(c->device));
+      lda_status s = sweep_graph(c, k, &g);
+      if (s) return s;
+      HIP_TRY(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(c->sweep_dev), (int)c->sweep, 1, c->stream));
+      HIP_TRY(hipGraphLaunch(g, c->stream));
+      c->sweep += (uint32_t)k;
+      c->sweeps_since_seed += k;
+      c->sweep_seq = false;
+      c->sweep_recount = false;
+      c->pending_absolute = false;
+      c->apply_gen += (uint64_t)k;
+      i += k;
+      continue;
+    }
     lda_status s = lda_sample(c);
     if (s) return s;
     s = apply_impl(c);
     if (s) return s;
+    ++i;
   }
   return LDA_OK;
   });

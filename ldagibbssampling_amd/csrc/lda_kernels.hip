@@ -200,9 +200,15 @@ __device__ __forceinline__ void wave_lds_fence() { __builtin_amdgcn_fence(__ATOM
 // A launch's first grab was a burst of same-address atomics from every
 // consumer at once; a small corpus (C1: ~1000 ranges, one per wave) now
 // takes none.  Which consumer samples which range never changes a result
-// (draws are keyed by the global token index).
+// (draws are keyed by the global token index).  The wave kernels pass the
+// result through uniform_i: the id derives from threadIdx.x, which the
+// compiler cannot tell is wave-uniform, and every branch on the range's
+// bounds downstream of it had become an exec-mask branch (scalar work).
+#ifndef LDA_STATIC_FIRST
+#define LDA_STATIC_FIRST 1
+#endif
 __device__ __forceinline__ int first_or_queued(bool first, int id, int count, int queued) {
-  return first ? id : count + queued;
+  return (LDA_STATIC_FIRST && first) ? id : (LDA_STATIC_FIRST ? count : 0) + queued;
 }
 
 template <int C>
@@ -322,6 +328,7 @@ __device__ __forceinline__ int shift_in(int a, int b, int lane) {
 template <int C, int P, bool FROZEN>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(sample_waves_per_eu<C>())))
 void k_sample(SampleParams p) {
+  if (p.c2_dev) p.c2 = *p.c2_dev;                    // a graph-launched sweep (lda_sweep)
   extern __shared__ __attribute__((aligned(16))) int32_t smem[];
   constexpr int KP = C * 64;
   constexpr int H = (C + 1) / 2;                     // dwords of a 16-bit row per lane
@@ -362,8 +369,8 @@ void k_sample(SampleParams p) {
   bool first_range = true;
   while (true) {
     int r = 0;
-    if (!first_range && lane == 0) r = atomicAdd(p.queue, 1);
-    r = first_or_queued(first_range, (int)blockIdx.x * 4 + wid, (int)gridDim.x * 4, uniform_i(__shfl(r, 0)));
+    if ((!LDA_STATIC_FIRST || !first_range) && lane == 0) r = atomicAdd(p.queue, 1);
+    r = uniform_i(first_or_queued(first_range, (int)blockIdx.x * 4 + wid, (int)gridDim.x * 4, uniform_i(__shfl(r, 0))));
     first_range = false;
     if (r >= p.num_ranges) break;
     const int64_t d0 = p.range_doc[r], d1 = p.range_doc[r + 1];
@@ -760,6 +767,7 @@ __device__ __forceinline__ float half_incl_scan(float x) {
 
 template <int CH, int P, bool FROZEN>
 __global__ __launch_bounds__(256) void k_sample_half(SampleParams p) {
+  if (p.c2_dev) p.c2 = *p.c2_dev;                    // a graph-launched sweep (lda_sweep)
   extern __shared__ __attribute__((aligned(16))) int32_t smem[];
   constexpr int KH = 32 * CH;                        // topics a half covers
   constexpr int KP = KH < 64 ? 64 : KH;              // row stride of nw / nw16
@@ -1161,6 +1169,7 @@ template <int CH, int P, bool FROZEN>
 #endif
 #define QUARTER_ATTR __attribute__((amdgpu_waves_per_eu(FROZEN ? 4 : QUARTER_WPE)))
 __global__ __launch_bounds__(256) QUARTER_ATTR void k_sample_quarter(SampleParams p) {
+  if (p.c2_dev) p.c2 = *p.c2_dev;                    // a graph-launched sweep (lda_sweep)
   extern __shared__ __attribute__((aligned(16))) int32_t smem[];
   constexpr int KQ = 16 * CH;                        // topics a quarter covers
   constexpr int KP = KQ < 64 ? 64 : KQ;              // row stride of nw / nw16
@@ -1236,7 +1245,7 @@ __global__ __launch_bounds__(256) QUARTER_ATTR void k_sample_quarter(SampleParam
             loaded = 0;
             while (true) {
               int r = 0;
-              if (!first_range && ql == 0) r = atomicAdd(p.queue, 1);
+              if ((!LDA_STATIC_FIRST || !first_range) && ql == 0) r = atomicAdd(p.queue, 1);
               r = first_or_queued(first_range, ((int)blockIdx.x * 4 + wid) * 4 + (lane >> 4),
                                   (int)gridDim.x * 16, row_get_i(r, rb, 0));
               first_range = false;
@@ -1521,8 +1530,8 @@ __global__ __launch_bounds__(256) void k_sample_sparse(SampleParams p) {
   bool first_range = true;
   while (true) {
     int r = 0;
-    if (!first_range && lane == 0) r = atomicAdd(p.queue, 1);
-    r = first_or_queued(first_range, (int)blockIdx.x * 4 + wid, (int)gridDim.x * 4, uniform_i(__shfl(r, 0)));
+    if ((!LDA_STATIC_FIRST || !first_range) && lane == 0) r = atomicAdd(p.queue, 1);
+    r = uniform_i(first_or_queued(first_range, (int)blockIdx.x * 4 + wid, (int)gridDim.x * 4, uniform_i(__shfl(r, 0))));
     first_range = false;
     if (r >= p.num_ranges) break;
     const int64_t d0 = p.range_doc[r], d1 = p.range_doc[r + 1];
@@ -1818,11 +1827,18 @@ __global__ __launch_bounds__(256) void k_sample_sparse(SampleParams p) {
 // (no re-walk); only rounds >= SB_RB of long rows are re-read, one per lane.
 // The sums and their order are those of oracle exact_draw_sparse.
 #ifndef SB_RB
-#define SB_RB 10
+#define SB_RB SPARSE_REG_ROUNDS
 #endif
 #ifndef SB_BATCH
-#define SB_BATCH 8
+#define SB_BATCH SPARSE_BATCH_ROUNDS
 #endif
+// batches loaded and summed without a per-round bound check (the rows are
+// laid out in whole batches, sparse_row_entries; entries past the row are 0)
+#ifndef SB_BPAD
+#define SB_BPAD 0
+#endif
+static_assert(!SB_BPAD || (SB_RB == SPARSE_REG_ROUNDS && SB_BATCH == SPARSE_BATCH_ROUNDS),
+              "unchecked batches need the rows' batch layout");
 #ifndef SB_NS
 #define SB_NS 3
 #endif
@@ -1837,9 +1853,27 @@ __global__ __launch_bounds__(256) void k_sample_sparse(SampleParams p) {
 #ifndef SB_SAT_SPLIT
 #define SB_SAT_SPLIT 1
 #endif
+// topic -> (lane, group) with unsigned shifts (signed / and % on the scalar
+// unit cost ~12 instructions per split)
+#ifndef SB_UDIV
+#define SB_UDIV 0
+#endif
+// the selected lane's round count as a per-lane vector count + one readlane
+// (a ballot + bit test + add per round on the scalar unit otherwise)
+#ifndef SB_VCOUNT
+#define SB_VCOUNT 0
+#endif
+// group-sum selects keyed by lane*NG + g in VGPRs (a scalar compare and
+// select per group element otherwise)
+#ifndef SB_TGKEY
+#define SB_TGKEY 0
+#endif
 static_assert(SB_RB % SB_GRP == 0 && SB_BATCH % SB_GRP == 0, "round groups");
+#ifndef SB_WAVES
+#define SB_WAVES 16
+#endif
 template <int C>
-constexpr int sb_waves() { return 16; }
+constexpr int sb_waves() { return SB_WAVES; }
 
 __device__ __forceinline__ int nd16_get(const uint32_t* nd2, int k) {
   return (int)reinterpret_cast<const uint16_t*>(nd2)[k];
@@ -1900,11 +1934,36 @@ __global__ __launch_bounds__(64 * sb_waves<C>()) void k_sample_sparse_big(Sample
   // the lane's NG group sums as one register vector: a wave-uniform group
   // index becomes an indexed register move (an array was placed in scratch)
   typedef float tg_t __attribute__((ext_vector_type(NG)));
+#if SB_TGKEY
+  // lane*NG + q per element; the asm keeps them opaque VGPRs, so the
+  // compare against a uniform key stays one VALU compare per element
+  int tkey[NG];
+#pragma unroll
+  for (int q = 0; q < NG; ++q) {
+    int v = lane * NG + q;
+    asm volatile("" : "+v"(v));
+    tkey[q] = v;
+  }
+  auto set_tg = [&](tg_t& TG, int owner, int g, float v) {
+    const int key = owner * NG + g;
+#pragma unroll
+    for (int q = 0; q < NG; ++q) TG[q] = (tkey[q] == key) ? v : TG[q];
+  };
+  // group g of lane owner, read out to every lane
+  auto tg_at = [&](const tg_t& TG, int owner, int g) -> float {
+    const int key = owner * NG + g;
+    float v = 0.0f;
+#pragma unroll
+    for (int q = 0; q < NG; ++q) v = (tkey[q] == key) ? TG[q] : v;
+    return readlane_f(v, owner);
+  };
+#else
   auto set_tg = [&](tg_t& TG, int owner, int g, float v) {
     const float cur = TG[g];
     TG[g] = (lane == owner) ? v : cur;
   };
-  auto get_tg = [&](const tg_t& TG, int g) -> float { return TG[g]; };
+  auto tg_at = [&](const tg_t& TG, int owner, int g) -> float { return readlane_f(TG[g], owner); };
+#endif
   auto lane_total = [&](const tg_t& TG) -> float {
     float t = TG[0];
 #pragma unroll
@@ -1915,8 +1974,8 @@ __global__ __launch_bounds__(64 * sb_waves<C>()) void k_sample_sparse_big(Sample
   bool first_range = true;
   while (true) {
     int r = 0;
-    if (!first_range && lane == 0) r = atomicAdd(p.queue, 1);
-    r = first_or_queued(first_range, (int)blockIdx.x * WB + wid, (int)gridDim.x * WB, uniform_i(__shfl(r, 0)));
+    if ((!LDA_STATIC_FIRST || !first_range) && lane == 0) r = atomicAdd(p.queue, 1);
+    r = uniform_i(first_or_queued(first_range, (int)blockIdx.x * WB + wid, (int)gridDim.x * WB, uniform_i(__shfl(r, 0))));
     first_range = false;
     if (r >= p.num_ranges) break;
     const int64_t d0 = p.range_doc[r], d1 = p.range_doc[r + 1];
@@ -2064,12 +2123,17 @@ __global__ __launch_bounds__(64 * sb_waves<C>()) void k_sample_sparse_big(Sample
           const bool row_sat = n_raw < 0;           // the row holds a saturated count
           const int n = n_raw & 0x7FFFFFFF;
           const int64_t off = ((int64_t)readlane_i((int)(cmo >> 32), idx) << 32) | (uint32_t)readlane_i((int)cmo, idx);
+#if SB_UDIV
+          const int lo = (int)((uint32_t)zo / (uint32_t)C);
+          const int go = (int)(((uint32_t)zo % (uint32_t)C) / 16u);
+#else
           const int lo = zo / C;
           const int go = (zo % C) / 16;
+#endif
           // while the token is out: topic zc's coefficient uses invc (inv_m1[zo])
           const int zc = FROZEN ? -1 : zo;
           const float invc = FROZEN ? 0.0f : cinv[s];
-          const float g_saved = readlane_f(get_tg(TG, go), lo);
+          const float g_saved = tg_at(TG, lo, go);
 
           // remove the token from its document; re-evaluate its group
           if (lane == 0) nd2[zo >> 1] -= (zo & 1) ? 0x10000u : 1u;
@@ -2129,10 +2193,10 @@ __global__ __launch_bounds__(64 * sb_waves<C>()) void k_sample_sparse_big(Sample
               uint32_t eb[SB_BATCH];
               const uint32_t* rp = ent + off + lane + q0 * 64;
 #pragma unroll
-              for (int b = 0; b < SB_BATCH; ++b) eb[b] = (q0 + b < nr_all) ? rp[b * 64] : 0u;
+              for (int b = 0; b < SB_BATCH; ++b) eb[b] = (SB_BPAD || q0 + b < nr_all) ? rp[b * 64] : 0u;
 #pragma unroll
               for (int b = 0; b < SB_BATCH; b += SB_GRP) {
-                if (q0 + b < nr_all) {
+                if (SB_BPAD || q0 + b < nr_all) {
                   float tt[SB_GRP];
 #pragma unroll
                   for (int g = 0; g < SB_GRP; ++g) tt[g] = term_of(eb[b + g], w, zc, invc, sat);
@@ -2170,9 +2234,16 @@ __global__ __launch_bounds__(64 * sb_waves<C>()) void k_sample_sparse_big(Sample
             // #{q : E + accq[q] <= thr} over lane lstar's register rounds; the
             // sums are monotone and constant past its last round, so a count
             // >= nr means "none exceeds" (oracle: the last round)
+#if SB_VCOUNT
+            int cv = 0;
+#pragma unroll
+            for (int q = 0; q < SB_RB; ++q) cv += (E + accq[q] <= thr) ? 1 : 0;
+            const int cnt = readlane_i(cv, lstar);
+#else
             int cnt = 0;
 #pragma unroll
             for (int q = 0; q < SB_RB; ++q) cnt = add_lane_bit(cnt, __ballot(E + accq[q] <= thr), lstar);
+#endif
             int sel;
             if (cnt < nr && cnt < SB_RB) {
               sel = cnt;
@@ -2242,7 +2313,11 @@ __global__ __launch_bounds__(64 * sb_waves<C>()) void k_sample_sparse_big(Sample
           if (kn == zo) {
             set_tg(TG, lo, go, g_saved);        // the document is as before the removal
           } else {
+#if SB_UDIV
+            const int ln = (int)((uint32_t)kn / (uint32_t)C), gn = (int)(((uint32_t)kn % (uint32_t)C) / 16u);
+#else
             const int ln = kn / C, gn = (kn % C) / 16;
+#endif
             const float x = row_pass(row == 0 ? lo : ln, row == 0 ? go : gn, -1, 0.0f);
             const float gl = readlane_f(x, 15), gk = readlane_f(x, 31);
             set_tg(TG, lo, go, gl);
@@ -2313,12 +2388,13 @@ __global__ __launch_bounds__(256) void k_build_sparse(const int32_t* __restrict_
         ++pos;
       }
     }
-    // zero entries up to the next whole round of 64 (the capacity is padded
-    // to whole rounds): the large-K sampler loads full rounds, and a zero
-    // entry adds +0 to its sums
+    // zero entries up to the row's laid-out end (whole rounds, whole batches
+    // past the register rounds; the capacity is padded the same way): the
+    // large-K sampler loads full rounds and batches, and a zero entry adds +0
+    // to its sums
     const int nnz = __shfl(incl, 63);
-    const int pad_end = (nnz + 63) & ~63;
-    if (nnz + lane < pad_end) ent[o + nnz + lane] = 0u;
+    const int pad_end = (int)sparse_row_entries(nnz);
+    for (int i = nnz + lane; i < pad_end; i += 64) ent[o + i] = 0u;
     // sign bit: the row holds a saturated count (the sampler then checks
     // entries for the escape; otherwise it skips that per-entry branch)
     if (lane == 63) row_nnz[w] = row_sat ? (int32_t)((uint32_t)incl | 0x80000000u) : incl;
@@ -2426,6 +2502,7 @@ __global__ __launch_bounds__(256) void k_apply_packed(int32_t* __restrict__ nw, 
       }
     }
     if (threadIdx.x == 0 && t.queue) *t.queue = 0;
+    if (threadIdx.x == 0 && t.sweep_dev) *t.sweep_dev += 1u;   // the next graph sweep's counter
   }
   for (int64_t w = (int64_t)blockIdx.x * 4 + wid; w < V; w += (int64_t)gridDim.x * 4) {
     int32_t c[C], d[C];

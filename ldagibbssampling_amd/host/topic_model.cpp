@@ -272,6 +272,15 @@ class ShardGroup {
   void apply() {
     for (auto c : ctx) check(lda_apply(c), "lda_apply");
   }
+  // n sweeps; one shard runs them through lda_sweep, which launches plain
+  // sweeps as graphs (the reference's small corpora are launch-bound)
+  void sweeps(int32_t n) {
+    if (ctx.size() == 1) {
+      check(lda_sweep(ctx[0], n), "lda_sweep");
+      return;
+    }
+    for (int32_t i = 0; i < n; ++i) sweep();
+  }
 };
 
 // ------------------------------------------------------------------ model
@@ -620,12 +629,23 @@ void ParallelTopicModel::estimate() {
     }
     ll_pending.clear();
   };
+  // iterations after which something besides the sweep happens (statistics,
+  // optimisation, LL), or before which the topics are shown: the sweeps in
+  // between run as one batch
+  auto work_after = [&](int32_t i) {
+    const bool opt = i > burnin_period_ && optimize_interval_ != 0;
+    return i % 10 == 0 || (opt && (i % save_sample_interval_ == 0 || i % optimize_interval_ == 0));
+  };
+  auto show_before = [&](int32_t i) { return show_topics_interval_ != 0 && i % show_topics_interval_ == 0; };
   for (int32_t it = 1; it <= num_iterations_; ++it) {
-    if (show_topics_interval_ != 0 && it % show_topics_interval_ == 0) {
+    if (show_before(it)) {
       collect_ll();
       log("\n" + displayTopWords(words_per_topic_, false));
     }
-    shards_->sweep();
+    int32_t last = it;
+    while (last < num_iterations_ && !work_after(last) && !show_before(last + 1)) ++last;
+    shards_->sweeps(last - it + 1);
+    it = last;
     z_dirty_ = true;
     const bool opt = it > burnin_period_ && optimize_interval_ != 0;
     if (opt && it % save_sample_interval_ == 0)
