@@ -271,6 +271,16 @@ lda_status lda_doc_topic_histograms_clear(lda_ctx* ctx);
  * do not sum it across ranks).  LDA_ERR_INVALID_ARG if a cell exceeds
  * max_count (the largest word total bounds every cell). */
 lda_status lda_count_histogram(lda_ctx* ctx, int64_t max_count, int32_t* count_hist);
+/* One optimisation step's statistics with a single wait on the stream (the
+ * three calls above and lda_get_counts' nwsum each wait on their own): the
+ * accumulated document histograms ADDED and zeroed as _take (when
+ * doc_len_counts / topic_doc_counts are non-null), the count histogram ADDED
+ * (count_hist non-null), nwsum[K] copied (non-null).  Each output is optional.
+ * Replaces the per-statistic round trips of ParallelTopicModel.estimate()'s
+ * optimizeAlpha / optimizeBeta (ParallelTopicModel.java 2.0.7). */
+lda_status lda_hyper_statistics(lda_ctx* ctx, int32_t max_len, int32_t* doc_len_counts,
+                                int32_t* topic_doc_counts, int64_t max_count, int32_t* count_hist,
+                                int32_t* nwsum);
 
 /* Dirichlet.learnParameters(params, observations, observationLengths, shape,
  * scale, iterations): Minka's fixed point with a Gamma(shape, scale) prior;
@@ -322,8 +332,10 @@ void lda_debug_fail_host_alloc(int32_t nth);
  * last three ints became (num_iterations, thinning, burn_in), Mallet's
  * getSampledDistribution order (was (n_iter, burn_in, thin)); 3 -- the dense
  * samplers' exchange buffer holds recounted counts (lda_count_update_mode),
- * lda_recount_times, lda_set_exchange_parts' reserve_cus < 0 = default. */
-#define LDA_ABI_VERSION 3
+ * lda_recount_times, lda_set_exchange_parts' reserve_cus < 0 = default; 4 --
+ * lda_hyper_statistics, lda_set_alpha_beta returns without waiting for the
+ * stream (its upload is asynchronous). */
+#define LDA_ABI_VERSION 4
 const char* lda_version(void);
 int32_t lda_abi_version(void);
 

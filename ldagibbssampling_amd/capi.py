@@ -96,6 +96,7 @@ SIGNATURES = {
     "lda_doc_topic_histograms_take": (C.c_int32, [_vp, C.c_int32, _i32p, _i32p]),
     "lda_doc_topic_histograms_clear": (C.c_int32, [_vp]),
     "lda_count_histogram": (C.c_int32, [_vp, C.c_int64, _i32p]),
+    "lda_hyper_statistics": (C.c_int32, [_vp, C.c_int32, _vp, _vp, C.c_int64, _vp, _vp]),
     "lda_learn_parameters": (C.c_int32, [_f64p, C.c_int32, _i32p, _i32p, C.c_int32, C.c_double,
                                          C.c_double, C.c_int32, C.POINTER(C.c_double)]),
     "lda_learn_symmetric_concentration": (C.c_int32, [_i32p, C.c_int64, _i64p, _i32p, C.c_int64,

@@ -254,19 +254,28 @@ struct lda_ctx {
   // one launch for k sweeps instead of ~6 runtime calls per sweep (the
   // reference's ~16k-token corpus is host-bound at ~45 us per sweep against
   // ~32 us of kernels).  The sweep counter is read by the sampler from
-  // sweep_dev, which each apply advances; graphs are rebuilt when a captured
-  // argument changes (graph_key).
+  // state_dev, which each apply advances, and beta from there too (the
+  // optimisation changes it every few sweeps); graphs are rebuilt when a
+  // captured argument changes (graph_key).
   static constexpr int GRAPH_MAX = 16;
   bool use_graphs = true;
-  uint32_t* sweep_dev = nullptr;
+  uint32_t* state_dev = nullptr;      // [0] sweep, [1] beta, [2] V*beta (fp32 bits)
+  int64_t state_sweep = -1;           // the sweep state_dev[0] holds (-1: unknown)
+  bool state_beta = false;            // state_dev[1..2] hold the current beta
+  // lda_set_alpha_beta's upload source (pinned, so the copy is asynchronous;
+  // the event guards its reuse) and lda_hyper_statistics' staging
+  double* alpha_pin = nullptr;
+  hipEvent_t alpha_ev = nullptr;
+  bool alpha_ev_live = false;
+  int32_t* hyper_pin = nullptr;
+  size_t hyper_pin_cap = 0;
   hipGraphExec_t graphs[GRAPH_MAX + 1] = {};
   struct GraphKey {
     const void* range_doc = nullptr;
     int64_t R = -1;
-    float beta = 0.0f, vbeta = 0.0f;
     hipStream_t stream = nullptr;
     bool operator==(const GraphKey& o) const {
-      return range_doc == o.range_doc && R == o.R && beta == o.beta && vbeta == o.vbeta && stream == o.stream;
+      return range_doc == o.range_doc && R == o.R && stream == o.stream;
     }
   } graph_key;
   // event pairs around the last LDA_TIME_RING sampler launches (lda_sample_times)
@@ -294,7 +303,10 @@ struct lda_ctx {
     if (chist) (void)hipFree(chist);
     for (auto& g : graphs)
       if (g) (void)hipGraphExecDestroy(g);
-    if (sweep_dev) (void)hipFree(sweep_dev);
+    if (state_dev) (void)hipFree(state_dev);
+    if (alpha_pin) (void)hipHostFree(alpha_pin);
+    if (alpha_ev) (void)hipEventDestroy(alpha_ev);
+    if (hyper_pin) (void)hipHostFree(hyper_pin);
     for (int i = 0; i < LDA_TIME_RING; ++i) {
       if (ev0[i]) (void)hipEventDestroy(ev0[i]);
       if (ev1[i]) (void)hipEventDestroy(ev1[i]);
@@ -348,9 +360,8 @@ static lda_status build_row_capacity(lda_ctx* c) {
   HIP_TRY(e);
   std::vector<int64_t> off(c->V + 1);
   off[0] = 0;
-  // whole rounds of 64 entries, whole batches past the register rounds
-  // (lda::sparse_row_entries; k_build_sparse zero-fills the padding)
-  for (int w = 0; w < c->V; ++w) off[w + 1] = off[w] + lda::sparse_row_entries(h[w]);
+  // whole rounds of 64 entries (k_build_sparse zero-fills the padding)
+  for (int w = 0; w < c->V; ++w) off[w + 1] = off[w] + ((h[w] + 63) & ~int64_t(63));
   HIP_TRY(dalloc(&c->row_off, c->V + 1));
   HIP_TRY(dalloc(&c->row_nnz, c->V));
   HIP_TRY(dalloc(&c->ent, (size_t)off[c->V]));
@@ -643,7 +654,7 @@ lda_status lda_create(lda_ctx** out, const lda_config* cfg, const int64_t* doc_o
   CT(dalloc(&c->inv, c->Kp));
   CT(dalloc(&c->inv_m1, c->Kp));
   CT(dalloc(&c->partial, c->partial_blocks));
-  CT(dalloc(&c->sweep_dev, 1));
+  CT(dalloc(&c->state_dev, 4));
   {
     const char* gv = std::getenv("LDA_GRAPHS");
     c->use_graphs = !(gv && gv[0] == '0');
@@ -1079,8 +1090,6 @@ static lda_status sweep_graph(lda_ctx* c, int k, hipGraphExec_t* out) {
   lda_ctx::GraphKey key;
   key.range_doc = c->range_doc;
   key.R = c->R;
-  key.beta = (float)c->beta;
-  key.vbeta = (float)((double)c->V * c->beta);
   key.stream = c->stream;
   if (!(key == c->graph_key)) {
     for (auto& g : c->graphs)
@@ -1092,13 +1101,13 @@ static lda_status sweep_graph(lda_ctx* c, int k, hipGraphExec_t* out) {
   }
   if (!c->graphs[k]) {
     lda::SampleParams p = c->params(false);
-    p.c2_dev = c->sweep_dev;
+    p.state_dev = c->state_dev;
     p.delta = c->delta;
     p.dsum = c->delta + (int64_t)c->V * c->Kp;
     const int64_t wpb = c->waves_per_block;
     const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>(c->sample_blocks, (c->R + wpb - 1) / wpb));
-    lda::TopicTables t{c->nwsum, c->alpha_d, c->alpha_f, c->inv, c->inv_m1, key.vbeta, c->K, c->queue, 0,
-                       c->sweep_dev};
+    lda::TopicTables t{c->nwsum, c->alpha_d, c->alpha_f, c->inv, c->inv_m1, 0.0f, c->K, c->queue, 0,
+                       c->state_dev};
     HIP_TRY(hipStreamBeginCapture(c->stream, hipStreamCaptureModeRelaxed));
     hipError_t e = hipSuccess;
     for (int i = 0; i < k && e == hipSuccess; ++i) {
@@ -1132,8 +1141,17 @@ lda_status lda_sweep(lda_ctx* c, int32_t n) {
       HIP_TRY(hipSetDevice(c->device));
       lda_status s = sweep_graph(c, k, &g);
       if (s) return s;
-      HIP_TRY(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(c->sweep_dev), (int)c->sweep, 1, c->stream));
+      auto word = [&](int i) { return reinterpret_cast<hipDeviceptr_t>(c->state_dev + i); };
+      if (!c->state_beta) {
+        const float b = (float)c->beta, vb = (float)((double)c->V * c->beta);
+        HIP_TRY(hipMemsetD32Async(word(1), (int)__builtin_bit_cast(uint32_t, b), 1, c->stream));
+        HIP_TRY(hipMemsetD32Async(word(2), (int)__builtin_bit_cast(uint32_t, vb), 1, c->stream));
+        c->state_beta = true;
+      }
+      if (c->state_sweep != (int64_t)c->sweep)
+        HIP_TRY(hipMemsetD32Async(word(0), (int)c->sweep, 1, c->stream));
       HIP_TRY(hipGraphLaunch(g, c->stream));
+      c->state_sweep = (int64_t)c->sweep + k;
       c->sweep += (uint32_t)k;
       c->sweeps_since_seed += k;
       c->sweep_seq = false;
@@ -1210,17 +1228,24 @@ lda_status lda_set_alpha_beta(lda_ctx* c, const double* alpha, double beta) {
   for (int k = 0; k < c->K; ++k)
     if (!(alpha[k] > 0.0)) return fail(LDA_ERR_INVALID_ARG, "alpha must be > 0");
   HIP_TRY(hipSetDevice(c->device));
+  if (!c->alpha_pin) {
+    HIP_TRY(hipHostMalloc(&c->alpha_pin, sizeof(double) * c->K, hipHostMallocDefault));
+    HIP_TRY(hipEventCreateWithFlags(&c->alpha_ev, hipEventDisableTiming));
+  }
+  if (c->alpha_ev_live) HIP_TRY(hipEventSynchronize(c->alpha_ev));   // the previous upload has left
   c->alpha.assign(alpha, alpha + c->K);
   c->beta = beta;
-  HIP_TRY(hipMemcpyAsync(c->alpha_d, c->alpha.data(), sizeof(double) * c->K, hipMemcpyHostToDevice, c->stream));
+  c->state_beta = false;
+  std::copy(alpha, alpha + c->K, c->alpha_pin);
+  HIP_TRY(hipMemcpyAsync(c->alpha_d, c->alpha_pin, sizeof(double) * c->K, hipMemcpyHostToDevice, c->stream));
+  HIP_TRY(hipEventRecord(c->alpha_ev, c->stream));
+  c->alpha_ev_live = true;
   // refresh the fp32 tables (the nwsum delta part is zero unless pending)
   if (!c->pending) {
     HIP_TRY(lda::launch_prepare_topics(c->nwsum, c->delta + (int64_t)c->V * c->Kp, c->alpha_d,
                                        c->beta, (double)c->V * c->beta, c->K, c->Kp, c->alpha_f,
                                        c->inv, c->inv_m1, c->stream));
-
   }
-  HIP_TRY(hipStreamSynchronize(c->stream));
   return LDA_OK;
   });
 }
@@ -1434,6 +1459,58 @@ lda_status lda_count_histogram(lda_ctx* c, int64_t max_count, int32_t* count_his
   HIP_TRY(hipStreamSynchronize(c->stream));
   if (h[n]) return fail(LDA_ERR_INVALID_ARG, "an nw cell exceeds max_count");
   for (size_t i = 0; i < n; ++i) count_hist[i] += h[i];
+  return LDA_OK;
+  });
+}
+
+lda_status lda_hyper_statistics(lda_ctx* c, int32_t max_len, int32_t* doc_len_counts, int32_t* topic_doc_counts,
+                                int64_t max_count, int32_t* count_hist, int32_t* nwsum) {
+  return lda_abi::guarded([&]() -> lda_status {
+  if (!c) return fail(LDA_ERR_INVALID_ARG, "null ctx");
+  if ((doc_len_counts == nullptr) != (topic_doc_counts == nullptr))
+    return fail(LDA_ERR_INVALID_ARG, "doc_len_counts and topic_doc_counts go together");
+  if (count_hist && max_count < 0) return fail(LDA_ERR_INVALID_ARG, "max_count must be >= 0");
+  if (c->pending && (count_hist || nwsum)) return fail(LDA_ERR_STATE, "statistics with a pending delta: call lda_apply first");
+  const bool docs = doc_len_counts && c->stat_buf;
+  if (docs && c->stat_len != max_len) return fail(LDA_ERR_INVALID_ARG, "max_len differs from the accumulated histograms'");
+  HIP_TRY(hipSetDevice(c->device));
+  const size_t L1 = (size_t)max_len + 1;
+  const size_t n_doc = docs ? L1 + (size_t)c->K * L1 : 0;
+  const size_t n_cnt = count_hist ? (size_t)max_count + 2 : 0;   // + the overflow cell
+  const size_t n_sum = nwsum ? (size_t)c->K : 0;
+  const size_t need = n_doc + n_cnt + n_sum;
+  if (need == 0) return LDA_OK;
+  if (c->hyper_pin_cap < need) {
+    if (c->hyper_pin) (void)hipHostFree(c->hyper_pin);
+    c->hyper_pin = nullptr;
+    c->hyper_pin_cap = 0;
+    HIP_TRY(hipHostMalloc(&c->hyper_pin, sizeof(int32_t) * need, hipHostMallocDefault));
+    c->hyper_pin_cap = need;
+  }
+  int32_t* h = c->hyper_pin;
+  if (docs) {
+    HIP_TRY(hipMemcpyAsync(h, c->stat_buf, n_doc * sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipMemsetAsync(c->stat_buf, 0, n_doc * sizeof(int32_t), c->stream));
+  }
+  if (count_hist) {
+    if (c->chist_cap < n_cnt) {
+      if (c->chist) (void)hipFree(c->chist);
+      c->chist = nullptr;
+      c->chist_cap = 0;
+      HIP_TRY(dalloc(&c->chist, n_cnt));
+      c->chist_cap = n_cnt;
+    }
+    HIP_TRY(hipMemsetAsync(c->chist, 0, n_cnt * sizeof(int32_t), c->stream));
+    HIP_TRY(lda::launch_count_hist(c->nw, c->V, c->K, c->Kp, max_count, c->chist, c->chist + n_cnt - 1, c->stream));
+    HIP_TRY(hipMemcpyAsync(h + n_doc, c->chist, n_cnt * sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
+  }
+  if (nwsum)
+    HIP_TRY(hipMemcpyAsync(h + n_doc + n_cnt, c->nwsum, n_sum * sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));   // the one wait
+  if (count_hist && h[n_doc + n_cnt - 1]) return fail(LDA_ERR_INVALID_ARG, "an nw cell exceeds max_count");
+  for (size_t i = 0; i < n_doc; ++i) (i < L1 ? doc_len_counts[i] : topic_doc_counts[i - L1]) += h[i];
+  for (size_t i = 0; i + 1 < n_cnt; ++i) count_hist[i] += h[n_doc + i];
+  for (size_t i = 0; i < n_sum; ++i) nwsum[i] = h[n_doc + n_cnt + i];
   return LDA_OK;
   });
 }

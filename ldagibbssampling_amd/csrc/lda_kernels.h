@@ -71,9 +71,10 @@ struct SampleParams {
   // 16-bit copy of the snapshot rows (k_sample)
   const uint16_t* nw16;     // [V*Kp] counts, clamped at 65535
   const uint8_t* wide;      // [V] 1 when the row holds a count > 65535 (read nw)
-  // graph-launched sweeps (lda_sweep): the sweep counter (Philox word 2) read
-  // from device memory, which each sweep's apply advances (dense kernels)
-  const uint32_t* c2_dev;
+  // graph-launched sweeps (lda_sweep), dense kernels: [0] the sweep counter
+  // (Philox word 2), which each sweep's apply advances, [1] beta's fp32 bits,
+  // read from device memory in place of c2 / beta
+  const uint32_t* state_dev;
 };
 
 // Tokens [tok[i], tok[i+1]) of a shard belong to exchange part i.
@@ -90,19 +91,6 @@ constexpr int32_t RECOUNT_ITEM_TOKENS = 1024;
 constexpr uint32_t ENT_TOPIC_BITS = 12;
 constexpr uint32_t ENT_TOPIC_MASK = (1u << ENT_TOPIC_BITS) - 1;
 constexpr uint32_t ENT_COUNT_SAT = (1u << (32 - ENT_TOPIC_BITS)) - 1;
-// Entries a sparse row is laid out with for n nonzeros: whole 64-entry rounds
-// and, past the large-K sampler's SPARSE_REG_ROUNDS register rounds, whole
-// batches of SPARSE_BATCH_ROUNDS rounds, zero-filled (k_build_sparse), so the
-// sampler loads a long row's batches without a per-round bound check.
-constexpr int SPARSE_REG_ROUNDS = 10;
-constexpr int SPARSE_BATCH_ROUNDS = 8;
-__host__ __device__ constexpr int64_t sparse_row_entries(int64_t n) {
-  const int64_t r = (n + 63) >> 6;
-  return 64 * (r <= SPARSE_REG_ROUNDS
-                   ? r
-                   : SPARSE_REG_ROUNDS + (r - SPARSE_REG_ROUNDS + SPARSE_BATCH_ROUNDS - 1) / SPARSE_BATCH_ROUNDS *
-                                             SPARSE_BATCH_ROUNDS);
-}
 
 // half: 1 = the half-wave variant k_sample_half, 2 = the quarter-wave
 // k_sample_quarter (C <= 2 only; lda_capi.cpp: LDA_DENSE_HALF), 0 = k_sample<C>
@@ -131,7 +119,7 @@ struct TopicTables {
   int32_t K;
   int32_t* queue;           // work-queue counter zeroed for the next sample (nullable)
   int32_t absolute;         // 1: the buffer holds recounted counts that replace nw / nwsum
-  uint32_t* sweep_dev;      // advanced by one when non-null (graph-launched sweeps)
+  uint32_t* state_dev;      // graph-launched sweeps: [0] advanced by one, [2] vbeta's fp32 bits read in place of vbeta
 };
 // dense sampler's apply: nw += delta, delta = 0, 16-bit rows + wide flags,
 // nwsum/tables (k_apply + k_build_packed + k_prepare_topics in one launch)

@@ -328,7 +328,10 @@ __device__ __forceinline__ int shift_in(int a, int b, int lane) {
 template <int C, int P, bool FROZEN>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(sample_waves_per_eu<C>())))
 void k_sample(SampleParams p) {
-  if (p.c2_dev) p.c2 = *p.c2_dev;                    // a graph-launched sweep (lda_sweep)
+  if (p.state_dev) {                                  // a graph-launched sweep (lda_sweep)
+    p.c2 = p.state_dev[0];
+    p.beta = __uint_as_float(p.state_dev[1]);
+  }
   extern __shared__ __attribute__((aligned(16))) int32_t smem[];
   constexpr int KP = C * 64;
   constexpr int H = (C + 1) / 2;                     // dwords of a 16-bit row per lane
@@ -767,7 +770,10 @@ __device__ __forceinline__ float half_incl_scan(float x) {
 
 template <int CH, int P, bool FROZEN>
 __global__ __launch_bounds__(256) void k_sample_half(SampleParams p) {
-  if (p.c2_dev) p.c2 = *p.c2_dev;                    // a graph-launched sweep (lda_sweep)
+  if (p.state_dev) {                                  // a graph-launched sweep (lda_sweep)
+    p.c2 = p.state_dev[0];
+    p.beta = __uint_as_float(p.state_dev[1]);
+  }
   extern __shared__ __attribute__((aligned(16))) int32_t smem[];
   constexpr int KH = 32 * CH;                        // topics a half covers
   constexpr int KP = KH < 64 ? 64 : KH;              // row stride of nw / nw16
@@ -1169,7 +1175,10 @@ template <int CH, int P, bool FROZEN>
 #endif
 #define QUARTER_ATTR __attribute__((amdgpu_waves_per_eu(FROZEN ? 4 : QUARTER_WPE)))
 __global__ __launch_bounds__(256) QUARTER_ATTR void k_sample_quarter(SampleParams p) {
-  if (p.c2_dev) p.c2 = *p.c2_dev;                    // a graph-launched sweep (lda_sweep)
+  if (p.state_dev) {                                  // a graph-launched sweep (lda_sweep)
+    p.c2 = p.state_dev[0];
+    p.beta = __uint_as_float(p.state_dev[1]);
+  }
   extern __shared__ __attribute__((aligned(16))) int32_t smem[];
   constexpr int KQ = 16 * CH;                        // topics a quarter covers
   constexpr int KP = KQ < 64 ? 64 : KQ;              // row stride of nw / nw16
@@ -1827,18 +1836,11 @@ __global__ __launch_bounds__(256) void k_sample_sparse(SampleParams p) {
 // (no re-walk); only rounds >= SB_RB of long rows are re-read, one per lane.
 // The sums and their order are those of oracle exact_draw_sparse.
 #ifndef SB_RB
-#define SB_RB SPARSE_REG_ROUNDS
+#define SB_RB 10
 #endif
 #ifndef SB_BATCH
-#define SB_BATCH SPARSE_BATCH_ROUNDS
+#define SB_BATCH 8
 #endif
-// batches loaded and summed without a per-round bound check (the rows are
-// laid out in whole batches, sparse_row_entries; entries past the row are 0)
-#ifndef SB_BPAD
-#define SB_BPAD 0
-#endif
-static_assert(!SB_BPAD || (SB_RB == SPARSE_REG_ROUNDS && SB_BATCH == SPARSE_BATCH_ROUNDS),
-              "unchecked batches need the rows' batch layout");
 #ifndef SB_NS
 #define SB_NS 3
 #endif
@@ -1856,17 +1858,17 @@ static_assert(!SB_BPAD || (SB_RB == SPARSE_REG_ROUNDS && SB_BATCH == SPARSE_BATC
 // topic -> (lane, group) with unsigned shifts (signed / and % on the scalar
 // unit cost ~12 instructions per split)
 #ifndef SB_UDIV
-#define SB_UDIV 0
+#define SB_UDIV 1
 #endif
 // the selected lane's round count as a per-lane vector count + one readlane
 // (a ballot + bit test + add per round on the scalar unit otherwise)
 #ifndef SB_VCOUNT
-#define SB_VCOUNT 0
+#define SB_VCOUNT 1
 #endif
 // group-sum selects keyed by lane*NG + g in VGPRs (a scalar compare and
 // select per group element otherwise)
 #ifndef SB_TGKEY
-#define SB_TGKEY 0
+#define SB_TGKEY 1
 #endif
 static_assert(SB_RB % SB_GRP == 0 && SB_BATCH % SB_GRP == 0, "round groups");
 #ifndef SB_WAVES
@@ -2193,10 +2195,10 @@ __global__ __launch_bounds__(64 * sb_waves<C>()) void k_sample_sparse_big(Sample
               uint32_t eb[SB_BATCH];
               const uint32_t* rp = ent + off + lane + q0 * 64;
 #pragma unroll
-              for (int b = 0; b < SB_BATCH; ++b) eb[b] = (SB_BPAD || q0 + b < nr_all) ? rp[b * 64] : 0u;
+              for (int b = 0; b < SB_BATCH; ++b) eb[b] = (q0 + b < nr_all) ? rp[b * 64] : 0u;
 #pragma unroll
               for (int b = 0; b < SB_BATCH; b += SB_GRP) {
-                if (SB_BPAD || q0 + b < nr_all) {
+                if (q0 + b < nr_all) {
                   float tt[SB_GRP];
 #pragma unroll
                   for (int g = 0; g < SB_GRP; ++g) tt[g] = term_of(eb[b + g], w, zc, invc, sat);
@@ -2388,13 +2390,12 @@ __global__ __launch_bounds__(256) void k_build_sparse(const int32_t* __restrict_
         ++pos;
       }
     }
-    // zero entries up to the row's laid-out end (whole rounds, whole batches
-    // past the register rounds; the capacity is padded the same way): the
-    // large-K sampler loads full rounds and batches, and a zero entry adds +0
-    // to its sums
+    // zero entries up to the next whole round of 64 (the capacity is padded
+    // to whole rounds): the large-K sampler loads full rounds, and a zero
+    // entry adds +0 to its sums
     const int nnz = __shfl(incl, 63);
-    const int pad_end = (int)sparse_row_entries(nnz);
-    for (int i = nnz + lane; i < pad_end; i += 64) ent[o + i] = 0u;
+    const int pad_end = (nnz + 63) & ~63;
+    if (nnz + lane < pad_end) ent[o + nnz + lane] = 0u;
     // sign bit: the row holds a saturated count (the sampler then checks
     // entries for the escape; otherwise it skips that per-entry branch)
     if (lane == 63) row_nnz[w] = row_sat ? (int32_t)((uint32_t)incl | 0x80000000u) : incl;
@@ -2492,9 +2493,10 @@ __global__ __launch_bounds__(256) void k_apply_packed(int32_t* __restrict__ nw, 
       t.nwsum[k] = s;
       dsum[k] = 0;
       if (k < t.K) {
+        const float vb = t.state_dev ? __uint_as_float(t.state_dev[2]) : t.vbeta;
         t.alpha_f[k] = (float)t.alpha[k];
-        t.inv[k] = 1.0f / ((float)s + t.vbeta);
-        t.inv_m1[k] = 1.0f / ((float)(s - 1) + t.vbeta);
+        t.inv[k] = 1.0f / ((float)s + vb);
+        t.inv_m1[k] = 1.0f / ((float)(s - 1) + vb);
       } else {
         t.alpha_f[k] = 0.0f;
         t.inv[k] = 0.0f;
@@ -2502,7 +2504,7 @@ __global__ __launch_bounds__(256) void k_apply_packed(int32_t* __restrict__ nw, 
       }
     }
     if (threadIdx.x == 0 && t.queue) *t.queue = 0;
-    if (threadIdx.x == 0 && t.sweep_dev) *t.sweep_dev += 1u;   // the next graph sweep's counter
+    if (threadIdx.x == 0 && t.state_dev) t.state_dev[0] += 1u;   // the next graph sweep's counter
   }
   for (int64_t w = (int64_t)blockIdx.x * 4 + wid; w < V; w += (int64_t)gridDim.x * 4) {
     int32_t c[C], d[C];

@@ -574,14 +574,10 @@ void ParallelTopicModel::optimizeAlpha() {
   std::fill(topic_doc_counts_.begin(), topic_doc_counts_.end(), 0);
 }
 
-void ParallelTopicModel::optimizeBeta() {
-  // countHistogram: nw cells by count, up to the largest word total
-  const int64_t max_count = max_word_total_;
-  std::vector<int32_t> hist((size_t)max_count + 1, 0);
-  check(lda_count_histogram(shards_->ctx[0], max_count, hist.data()), "lda_count_histogram");
+void ParallelTopicModel::optimizeBeta(const std::vector<int32_t>& hist, const std::vector<int32_t>& nwsum) {
+  // countHistogram: nw cells by count, up to the largest word total (hist);
   // topicSizeHistogram, sparse: (tokens in topic, number of topics)
-  std::vector<int32_t> nwsum((size_t)K_);
-  check(lda_get_counts(shards_->ctx[0], nullptr, nwsum.data(), nullptr, nullptr), "lda_get_counts");
+  const int64_t max_count = max_word_total_;
   std::vector<int64_t> sizes(nwsum.begin(), nwsum.end());
   std::sort(sizes.begin(), sizes.end());
   std::vector<int64_t> lens;
@@ -652,11 +648,16 @@ void ParallelTopicModel::estimate() {
       for (auto c : shards_->ctx)
         check(lda_doc_topic_histograms_accumulate(c, max_doc_len_), "lda_doc_topic_histograms_accumulate");
     if (opt && it % optimize_interval_ == 0) {
-      for (auto c : shards_->ctx)
-        check(lda_doc_topic_histograms_take(c, max_doc_len_, doc_len_counts_.data(), topic_doc_counts_.data()),
-              "lda_doc_topic_histograms_take");
+      // every shard's alpha statistics (summed); the count histogram and
+      // nwsum of the global counts from shard 0; one wait per shard
+      std::vector<int32_t> hist((size_t)max_word_total_ + 1, 0), nwsum((size_t)K_);
+      for (size_t g = 0; g < shards_->ctx.size(); ++g)
+        check(lda_hyper_statistics(shards_->ctx[g], max_doc_len_, doc_len_counts_.data(), topic_doc_counts_.data(),
+                                   max_word_total_, g == 0 ? hist.data() : nullptr,
+                                   g == 0 ? nwsum.data() : nullptr),
+              "lda_hyper_statistics");
       optimizeAlpha();
-      optimizeBeta();
+      optimizeBeta(hist, nwsum);
       for (auto c : shards_->ctx) check(lda_set_alpha_beta(c, alpha_.data(), beta_), "lda_set_alpha_beta");
     }
     if (it % 10 == 0) {

@@ -107,7 +107,9 @@ class ParallelTopicModel {
   void ensureShards();
   void markDirty();
   void optimizeAlpha();
-  void optimizeBeta();
+  // count histogram (max_word_total_ + 1 cells) and nwsum, fetched with the
+  // alpha statistics in one lda_hyper_statistics call
+  void optimizeBeta(const std::vector<int32_t>& count_hist, const std::vector<int32_t>& nwsum);
   void log(const std::string& line) const;
 
   int32_t K_;

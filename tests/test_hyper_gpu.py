@@ -127,3 +127,42 @@ def test_device_accumulated_histograms_and_async_ll(kind, K):
         assert a.value == ed and b.value == ew
     a, b = C.c_double(), C.c_double()
     assert lib.lda_log_likelihood_collect(g._h, tickets[0], C.byref(a), C.byref(b)) == -4
+
+
+@pytest.mark.parametrize("kind,K", [("dense", 100), ("sparse", 2048)])
+def test_hyper_statistics_in_one_call(kind, K):
+    """lda_hyper_statistics (one wait) equals _take + lda_count_histogram +
+    lda_get_counts' nwsum, each output optional; the accumulated histograms
+    are zeroed by it as by _take."""
+    import ctypes as C
+    from ldagibbssampling_amd import capi
+    from ldagibbssampling_amd.sampler import GibbsSampler
+    c = synthetic_lda(num_docs=150, num_types=300, num_topics=20, doc_len=None, mean_len=50,
+                      min_len=0, max_len=200, seed=K + 1)
+    mk = lambda: GibbsSampler(K, c.num_types, c.doc_off, c.words, 0.1, 0.01, seed=9, sampler=kind)
+    a, b = mk(), mk()
+    L = a.max_doc_length()
+    M = int(np.bincount(c.words, minlength=c.num_types).max())
+    lib = capi.load()
+    for g in (a, b):
+        for _ in range(2):
+            g.sweep(1)
+            capi.check(lib.lda_doc_topic_histograms_accumulate(g._h, L), "accumulate")
+    dl, td = np.zeros(L + 1, np.int32), np.zeros(K * (L + 1), np.int32)
+    capi.check(lib.lda_doc_topic_histograms_take(a._h, L, dl, td), "take")
+    hist = a.count_histogram(M)
+    nws = a.counts(with_nd=False)[1]
+    dl2, td2 = np.zeros(L + 1, np.int32), np.zeros(K * (L + 1), np.int32)
+    hist2, nws2 = np.zeros(M + 1, np.int32), np.zeros(K, np.int32)
+    ptr = lambda x: x.ctypes.data_as(C.c_void_p)
+    capi.check(lib.lda_hyper_statistics(b._h, L, ptr(dl2), ptr(td2), M, ptr(hist2), ptr(nws2)), "hyper")
+    np.testing.assert_array_equal(dl2, dl)
+    np.testing.assert_array_equal(td2, td)
+    np.testing.assert_array_equal(hist2, hist)
+    np.testing.assert_array_equal(nws2, nws[:K])
+    # zeroed like _take; outputs optional
+    capi.check(lib.lda_hyper_statistics(b._h, L, ptr(dl2), ptr(td2), 0, None, None), "hyper")
+    np.testing.assert_array_equal(dl2, dl)
+    capi.check(lib.lda_hyper_statistics(b._h, L, None, None, M, None, ptr(nws2)), "hyper")
+    np.testing.assert_array_equal(nws2, nws[:K])
+    assert lib.lda_hyper_statistics(b._h, L, ptr(dl2), None, 0, None, None) == -1
