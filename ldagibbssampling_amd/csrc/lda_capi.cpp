@@ -281,6 +281,7 @@ struct lda_ctx {
   // event pairs around the last LDA_TIME_RING sampler launches (lda_sample_times)
   static constexpr int LDA_TIME_RING = 256;
   hipEvent_t ev0[LDA_TIME_RING] = {}, ev1[LDA_TIME_RING] = {}, ev2[LDA_TIME_RING] = {};
+  bool recounted[LDA_TIME_RING] = {};   // the launch in this slot ran the recount (ev1 -> ev2)
   int64_t launches = 0;
 
   ~lda_ctx() {
@@ -808,6 +809,7 @@ static lda_status sample_part_impl(lda_ctx* c, int part) {
                                   c->stream));
     }
     HIP_TRY(hipEventRecord(c->ev2[slot], c->stream));
+    c->recounted[slot] = c->sweep_recount;
     c->launches++;
   }
   c->pending = true;  // the part buffers hold this sweep's changes
@@ -988,6 +990,8 @@ lda_status lda_recount_times(lda_ctx* c, int32_t max, float* ms, int32_t* n) {
   *n = k;
   for (int32_t i = 0; i < k; ++i) {
     const int slot = (int)((c->launches - k + i) % lda_ctx::LDA_TIME_RING);
+    ms[i] = 0.0f;                      // a delta-mode launch runs no recount
+    if (!c->recounted[slot]) continue;
     HIP_TRY(hipEventSynchronize(c->ev2[slot]));
     HIP_TRY(hipEventElapsedTime(&ms[i], c->ev1[slot], c->ev2[slot]));
   }

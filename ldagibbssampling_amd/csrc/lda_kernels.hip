@@ -1870,6 +1870,19 @@ __global__ __launch_bounds__(256) void k_sample_sparse(SampleParams p) {
 #ifndef SB_TGKEY
 #define SB_TGKEY 1
 #endif
+// word-row loads as buffer loads bounded by the row (a load past it returns
+// 0 without a memory access): the ring prefetch is issued for every token
+// slot without a per-round branch, so every path round the loop issues the
+// same loads and the first round's wait need not drain the next token's
+// prefetch; the batches past the register rounds are double-buffered
+#ifndef SB_BUF
+#define SB_BUF 0
+#endif
+#ifndef SB_DBUF
+#define SB_DBUF SB_BUF
+#endif
+// gfx9 buffer resource word 3 (raw 32-bit loads, bounds checked)
+constexpr int kBufWord3 = 0x00020000;
 static_assert(SB_RB % SB_GRP == 0 && SB_BATCH % SB_GRP == 0, "round groups");
 #ifndef SB_WAVES
 #define SB_WAVES 16
@@ -2073,16 +2086,25 @@ __global__ __launch_bounds__(64 * sb_waves<C>()) void k_sample_sparse_big(Sample
              (uint32_t)readlane_i((int)m1o, pidx - 64);
         zp = readlane_i(z1, pidx - 64);
       }
+#if SB_BUF
+      // past the range end: an empty row (every load returns 0)
+      const int nrp = tp < t1 ? ((np & 0x7FFFFFFF) + 63) >> 6 : 0;
+      const __amdgpu_buffer_rsrc_t rs =
+          __builtin_amdgcn_make_buffer_rsrc((void*)(ent + op), (short)0, nrp * 256, kBufWord3);
+#pragma unroll
+      for (int q = 0; q < SB_RB; ++q) rg[q] = __builtin_amdgcn_raw_buffer_load_b32(rs, lane * 4 + q * 256, 0, 0);
+#else
       const int nrp = ((np & 0x7FFFFFFF) + 63) >> 6;
       const uint32_t* rp = ent + op + lane;
 #pragma unroll
       for (int q = 0; q < SB_RB; ++q)
         if (q < nrp) rg[q] = rp[q * 64];
+#endif
       if (!FROZEN) ci = inv_m1[zp];
     };
 #pragma unroll
     for (int s = 0; s < NS - 1; ++s)
-      if (s < t1) prefetch(ring[s], cinv[s], s);
+      if (SB_BUF || s < t1) prefetch(ring[s], cinv[s], s);
 
     for (int tb = 0; tb < t1; tb += NS) {
 #pragma unroll
@@ -2177,7 +2199,7 @@ __global__ __launch_bounds__(64 * sb_waves<C>()) void k_sample_sparse_big(Sample
           {
             const int sp = (s + NS - 1) % NS;
             const int tp = t + NS - 1;
-            if (tp < t1) prefetch(ring[sp], cinv[sp], tp);
+            if (SB_BUF || tp < t1) prefetch(ring[sp], cinv[sp], tp);
           }
           // the rounds past SB_RB (long rows), streamed in batches; the
           // lane's running sum after each of the first SB_NB batches is kept
@@ -2189,6 +2211,31 @@ __global__ __launch_bounds__(64 * sb_waves<C>()) void k_sample_sparse_big(Sample
           // as the register rounds are: a runtime flag inside term_of made every
           // batch term a divergent branch (exec-mask save/restore on the scalar
           // unit, which binds this kernel)
+#if SB_DBUF
+          // double-buffered: batch b+1's loads are in flight while batch b is
+          // summed; loads past the row return 0, and a 0 entry adds +0
+          auto batches = [&](bool sat) {
+            const __amdgpu_buffer_rsrc_t rb =
+                __builtin_amdgcn_make_buffer_rsrc((void*)(ent + off), (short)0, nr_all * 256, kBufWord3);
+            uint32_t ea[SB_BATCH];
+#pragma unroll
+            for (int b = 0; b < SB_BATCH; ++b)
+              ea[b] = __builtin_amdgcn_raw_buffer_load_b32(rb, lane * 4 + (SB_RB + b) * 256, 0, 0);
+            int mb = 0;
+            for (int q0 = SB_RB; q0 < nr_all; q0 += SB_BATCH, ++mb) {
+              uint32_t en[SB_BATCH];
+              const int vo = lane * 4 + (q0 + SB_BATCH) * 256;
+#pragma unroll
+              for (int b = 0; b < SB_BATCH; ++b) en[b] = __builtin_amdgcn_raw_buffer_load_b32(rb, vo + b * 256, 0, 0);
+#pragma unroll
+              for (int b = 0; b < SB_BATCH; ++b) acc = acc + term_of(ea[b], w, zc, invc, sat);
+#pragma unroll
+              for (int i = 0; i < SB_NB; ++i) accb[i] = (mb == i) ? acc : accb[i];
+#pragma unroll
+              for (int b = 0; b < SB_BATCH; ++b) ea[b] = en[b];
+            }
+          };
+#else
           auto batches = [&](bool sat) {
             int mb = 0;
             for (int q0 = SB_RB; q0 < nr_all; q0 += SB_BATCH, ++mb) {
@@ -2213,6 +2260,7 @@ __global__ __launch_bounds__(64 * sb_waves<C>()) void k_sample_sparse_big(Sample
               for (int i = 0; i < SB_NB; ++i) accb[i] = (mb == i) ? acc : accb[i];
             }
           };
+#endif
 #if SB_SAT_SPLIT
           if (nr_all > SB_RB) {
             if (!row_sat) batches(false);
