@@ -1839,7 +1839,7 @@ __global__ __launch_bounds__(256) void k_sample_sparse(SampleParams p) {
 #define SB_RB 10
 #endif
 #ifndef SB_BATCH
-#define SB_BATCH 8
+#define SB_BATCH 4
 #endif
 #ifndef SB_NS
 #define SB_NS 3
@@ -1876,13 +1876,13 @@ __global__ __launch_bounds__(256) void k_sample_sparse(SampleParams p) {
 // same loads and the first round's wait need not drain the next token's
 // prefetch; the batches past the register rounds are double-buffered
 #ifndef SB_BUF
-#define SB_BUF 0
+#define SB_BUF 1
 #endif
 #ifndef SB_DBUF
 #define SB_DBUF SB_BUF
 #endif
 // gfx9 buffer resource word 3 (raw 32-bit loads, bounds checked)
-constexpr int kBufWord3 = 0x00020000;
+[[maybe_unused]] constexpr int kBufWord3 = 0x00020000;
 static_assert(SB_RB % SB_GRP == 0 && SB_BATCH % SB_GRP == 0, "round groups");
 #ifndef SB_WAVES
 #define SB_WAVES 16

@@ -1,19 +1,19 @@
-# Round 3, step M: large-K sampler word-row loads as bounded buffer loads
-# (the ring prefetch without per-round branches; double-buffered batches),
-# with 6-10 register rounds and 2-3 ring slots: parity of each (the large-K
+# Round 3, step N: the bounded-load prefetch with double-buffered batches
+# of 2-4 rounds (fewer registers than 8), and 4-round single batches,
+# against the in-tree kernel: parity of each (the large-K
 # tests), then C5 at burn-in 0 / 30.
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
-O=gpurun_out/r3m; mkdir -p $O
+O=gpurun_out/r3n; mkdir -p $O
 export TMPDIR=/tmp
 line() { python3 -c "import json;d=json.loads(open('$1').read());r=d['roofline'];print('$2', round(d['value']/1e9,4),'Gtok/s', round(d['ms_per_step'],4), 'ms/step kernel',round(r['kernel_ms_timed_region'],4),'ms')"; }
-for v in c5bufp c5bufprb8 c5buf c5bufrb6 c5bufns2 c5bufns2rb8; do
+for v in c5bufp c5bufd4 c5bufd4rb8 c5bufd2 c5bufp4; do
   LDA_MI355X_LIB=$PWD/variants/$v/liblda_mi355x.so timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread \
     tests/test_parity_gpu.py -k "sparse or large_k" > $O/parity_$v.log 2>&1 || { echo "PARITY $v FAILED"; tail -20 $O/parity_$v.log; exit 1; }
   echo "$v $(tail -1 $O/parity_$v.log)"
 done
 for b in 0 30; do
-  for v in intree c5bufp c5bufprb8 c5buf c5bufrb6 c5bufns2 c5bufns2rb8; do
+  for v in intree c5bufp c5bufd4 c5bufd4rb8 c5bufd2 c5bufp4; do
     L=""; [ $v != intree ] && L=$PWD/variants/$v/liblda_mi355x.so
     LDA_MI355X_LIB=$L timeout -k 10 600 python bench.py --no-cpu-baseline --config c5 --burnin $b > $O/bench_${v}_b$b.log 2>&1 || { echo "BENCH $v $b FAILED"; tail -5 $O/bench_${v}_b$b.log; exit 1; }
     tail -1 $O/bench_${v}_b$b.log > $O/bench_${v}_b$b.jsonl
