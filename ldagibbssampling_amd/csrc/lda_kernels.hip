@@ -1883,7 +1883,7 @@ __global__ __launch_bounds__(256) void k_sample_sparse(SampleParams p) {
 #endif
 // gfx9 buffer resource word 3 (raw 32-bit loads, bounds checked)
 [[maybe_unused]] constexpr int kBufWord3 = 0x00020000;
-static_assert(SB_RB % SB_GRP == 0 && SB_BATCH % SB_GRP == 0, "round groups");
+static_assert(SB_RB % SB_GRP == 0 && (SB_DBUF || SB_BATCH % SB_GRP == 0), "round groups");
 #ifndef SB_WAVES
 #define SB_WAVES 16
 #endif
