@@ -196,6 +196,15 @@ struct lda_ctx {
   int32_t recount_sweeps = 0;
   int64_t sweeps_since_seed = 0;
   bool sweep_recount = false;      // the sweep being sampled recounts
+  // the word-ordered copy of z for the quarter-wave sampler's recount sweeps
+  // (zw[zpos[i]] = z[i] in the recount index's order; the sampler updates it,
+  // the recount streams it).  Valid while every sweep since it was built kept
+  // it current; rebuilt from z at a recount sweep otherwise.
+  int32_t* zw = nullptr;
+  uint32_t* zpos = nullptr;
+  bool zw_valid = false;
+  bool sweep_zw = false;           // the sweep being sampled keeps zw current
+  bool use_zw = true;              // LDA_ZW=0: the recount gathers z through perm (A/B)
   bool pending_absolute = false;   // the pending buffer holds counts (recount) rather than a delta
   bool recount_ok = false;         // dense sampler, N < 2^32
   // warm start (lda_set_warm_start): sweeps with a sweep counter below
@@ -305,6 +314,8 @@ struct lda_ctx {
     for (auto& g : graphs)
       if (g) (void)hipGraphExecDestroy(g);
     if (state_dev) (void)hipFree(state_dev);
+    if (zw) (void)hipFree(zw);
+    if (zpos) (void)hipFree(zpos);
     if (alpha_pin) (void)hipHostFree(alpha_pin);
     if (alpha_ev) (void)hipEventDestroy(alpha_ev);
     if (hyper_pin) (void)hipHostFree(hyper_pin);
@@ -384,6 +395,7 @@ static lda_status build_recount_index(lda_ctx* c) {
   c->perm = nullptr;
   c->items = nullptr;
   c->part_item.assign((size_t)c->parts + 1, 0);
+  c->zw_valid = false;             // zw follows perm's order
   if (!c->recount_ok || c->N == 0) return LDA_OK;
   lda::PartSpans ps{};
   ps.parts = c->parts;
@@ -503,6 +515,7 @@ static lda_status reseed_counts(lda_ctx* c) {
   c->pending = true;
   c->pending_absolute = false;   // nw is zero: adding the local counts sets them
   c->sweeps_since_seed = 0;
+  c->zw_valid = false;           // z may have been replaced
   return LDA_OK;
 }
 
@@ -659,6 +672,8 @@ lda_status lda_create(lda_ctx** out, const lda_config* cfg, const int64_t* doc_o
   {
     const char* gv = std::getenv("LDA_GRAPHS");
     c->use_graphs = !(gv && gv[0] == '0');
+    const char* zv = std::getenv("LDA_ZW");
+    c->use_zw = !(zv && zv[0] == '0');
   }
   CT(dalloc(&c->nonzero, c->partial_blocks));
   for (int i = 0; i < lda_ctx::LDA_TIME_RING; ++i) {
@@ -770,6 +785,15 @@ static lda_status sample_part_impl(lda_ctx* c, int part) {
       lda_status s = build_recount_index(c);
       if (s) return s;
     }
+    // the quarter-wave sampler keeps the word-ordered z copy current on a
+    // recount sweep (the others leave it stale); built from z when stale
+    c->sweep_zw = c->sweep_recount && c->use_zw && c->sampler == LDA_SAMPLER_DENSE && c->half == 2 && c->perm;
+    if (c->sweep_zw && !c->zw_valid) {
+      if (!c->zw) HIP_TRY(dalloc(&c->zw, (size_t)c->N));
+      if (!c->zpos) HIP_TRY(dalloc(&c->zpos, (size_t)c->N));
+      HIP_TRY(lda::launch_zw_build(c->perm, c->N, c->z, c->zpos, c->zw, c->stream));
+    }
+    c->zw_valid = c->sweep_zw;
   }
   const bool seq = c->sweep_seq;
   const int nparts = seq ? c->warm_parts : c->parts;
@@ -785,6 +809,8 @@ static lda_status sample_part_impl(lda_ctx* c, int part) {
     p.num_ranges = r1 - r0;
     p.queue = c->queue + part;
     p.delta = c->sweep_recount ? nullptr : buf;   // recount: the sampler writes z only
+    p.zw = c->sweep_zw ? c->zw : nullptr;
+    p.zpos = c->sweep_zw ? c->zpos : nullptr;
     p.dsum = c->sweep_recount ? nullptr : buf + (int64_t)c->V * c->Kp;
     const int64_t wpb = c->waves_per_block;
     // a split sweep leaves reserve_cus CUs' worth of sampler blocks free, so
@@ -804,7 +830,8 @@ static lda_status sample_part_impl(lda_ctx* c, int part) {
       // this part's rows recounted into its exchange buffer (the apply left
       // it zero)
       const int64_t i0 = c->part_item[(size_t)part], i1 = c->part_item[(size_t)part + 1];
-      HIP_TRY(lda::launch_recount(c->Kp, c->perm, c->items + 4 * i0, (int32_t)(i1 - i0), c->z, c->delta_part[part],
+      HIP_TRY(lda::launch_recount(c->Kp, c->perm, c->sweep_zw ? c->zw : nullptr, c->items + 4 * i0,
+                                  (int32_t)(i1 - i0), c->z, c->delta_part[part],
                                   c->delta_part[part] + (int64_t)c->V * c->Kp, c->recount_blocks,
                                   c->stream));
     }
@@ -1160,6 +1187,7 @@ lda_status lda_sweep(lda_ctx* c, int32_t n) {
       c->sweeps_since_seed += k;
       c->sweep_seq = false;
       c->sweep_recount = false;
+      c->zw_valid = false;
       c->pending_absolute = false;
       c->apply_gen += (uint64_t)k;
       i += k;

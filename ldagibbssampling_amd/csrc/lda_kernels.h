@@ -75,6 +75,11 @@ struct SampleParams {
   // (Philox word 2), which each sweep's apply advances, [1] beta's fp32 bits,
   // read from device memory in place of c2 / beta
   const uint32_t* state_dev;
+  // recount sweeps of the quarter-wave sampler: the word-ordered copy of z
+  // (zw[zpos[i]] = z[i], the recount index's order) kept current by the
+  // sampler, so the recount streams it instead of gathering z through perm
+  int32_t* zw;
+  const uint32_t* zpos;
 };
 
 // Tokens [tok[i], tok[i+1]) of a shard belong to exchange part i.
@@ -130,7 +135,11 @@ hipError_t launch_word_hist(const int32_t* words, int64_t n, const PartSpans& ps
                             uint32_t* cnt, hipStream_t st);
 hipError_t launch_word_scatter(const int32_t* words, int64_t n, const PartSpans& ps, int64_t V,
                                uint32_t* cursor, uint32_t* perm, hipStream_t st);
-hipError_t launch_recount(int32_t Kp, const uint32_t* perm, const int32_t* items, int32_t n_items,
+// zpos[perm[j]] = j; zw[j] = z[perm[j]] (the word-ordered copy of z)
+hipError_t launch_zw_build(const uint32_t* perm, int64_t n, const int32_t* z, uint32_t* zpos, int32_t* zw,
+                           hipStream_t st);
+// zw non-null: the topics are read from zw[perm index] (streamed) instead of z[perm[.]]
+hipError_t launch_recount(int32_t Kp, const uint32_t* perm, const int32_t* zw, const int32_t* items, int32_t n_items,
                           const int32_t* z, int32_t* buf, int32_t* bufsum, int blocks, hipStream_t st);
 hipError_t launch_philox_draws(const int64_t* gtok, int64_t n, uint32_t c2, uint32_t c3, uint64_t seed,
                                uint32_t* out, hipStream_t st);

@@ -1218,6 +1218,7 @@ __global__ __launch_bounds__(256) QUARTER_ATTR void k_sample_quarter(SampleParam
   bool first_range = true;                           // per row (lane-varying)
   // chunk registers: row-lane i <-> token cbase + i of the quarter's range
   int cw = 0, cz = 0, cn = 0, w1 = 0, z1 = 0, w2 = 0, z2 = 0, pw = 0;
+  uint32_t cpos = 0;                                 // zw position of the chunk's token (recount sweeps)
   float cu = 0.0f;
   uint32_t rows[P][HD];
 #pragma unroll
@@ -1241,6 +1242,7 @@ __global__ __launch_bounds__(256) QUARTER_ATTR void k_sample_quarter(SampleParam
             // the range is done (or none loaded yet): publish, clear, next range
             if (loaded) {
               if (ql < nt - cbase) p.z[t0 + cbase + ql] = cn;
+              if (!FROZEN && p.zw && cn != cz && ql < nt - cbase) p.zw[cpos] = cn;
               if (!FROZEN && p.delta && cn != cz) {
                 const uint32_t row = (uint32_t)cw * (uint32_t)KP;
                 atomicAdd(p.delta + (row + (uint32_t)cz), -1);
@@ -1290,6 +1292,7 @@ __global__ __launch_bounds__(256) QUARTER_ATTR void k_sample_quarter(SampleParam
               w2 = 32 + ql < n ? wrd[32 + ql] : 0;
               z2 = 32 + ql < n ? zr[32 + ql] : 0;
               cn = cz;
+              if (!FROZEN && p.zw && ql < n) cpos = p.zpos[s0 + ql];   // used at the chunk's publish
               cu = u01(draw_u32((uint64_t)(p.token_base + s0 + ql), p.c2, p.c3, p.k0, p.k1));
               int64_t dd = d0;
               while (p.doc_off[dd + 1] <= s0) ++dd;
@@ -1317,6 +1320,7 @@ __global__ __launch_bounds__(256) QUARTER_ATTR void k_sample_quarter(SampleParam
             if (t - cbase == 16) {
               // chunk switch: publish the finished chunk, shift
               p.z[t0 + cbase + ql] = cn;
+              if (!FROZEN && p.zw && cn != cz) p.zw[cpos] = cn;
               if (!FROZEN && p.delta && cn != cz) {
                 const uint32_t row = (uint32_t)cw * (uint32_t)KP;
                 atomicAdd(p.delta + (row + (uint32_t)cz), -1);
@@ -1330,6 +1334,7 @@ __global__ __launch_bounds__(256) QUARTER_ATTR void k_sample_quarter(SampleParam
               w1 = w2;
               z1 = z2;
               cn = cz;
+              if (!FROZEN && p.zw && cbase + ql < nt) cpos = p.zpos[t0 + cbase + ql];
               cu = u01(draw_u32((uint64_t)(p.token_base + t0 + cbase + ql), p.c2, p.c3, p.k0, p.k1));
               if (cbase + 32 + ql < nt) {
                 w2 = p.words[t0 + cbase + 32 + ql];
@@ -2900,6 +2905,7 @@ __global__ __launch_bounds__(256) void k_word_scatter(const int32_t* __restrict_
 // kernel at ~60M items/s (C2: 0.81 ms for 50k items).
 template <int C>
 __global__ __launch_bounds__(256) void k_recount(const uint32_t* __restrict__ perm,
+                                                 const int32_t* __restrict__ zw,
                                                  const int4* __restrict__ items, int32_t n_items,
                                                  const int32_t* __restrict__ z,
                                                  int32_t* __restrict__ buf,
@@ -2916,12 +2922,18 @@ __global__ __launch_bounds__(256) void k_recount(const uint32_t* __restrict__ pe
     const uint32_t b = (uint32_t)m.y;
     const int len = m.z;
     for (int i = lane; i < len; i += 256) {
-      uint32_t tk[4];
-#pragma unroll
-      for (int u = 0; u < 4; ++u) tk[u] = (i + 64 * u < len) ? perm[b + (uint32_t)(i + 64 * u)] : 0xFFFFFFFFu;
       int k[4];
+      if (zw) {
+        // the word-ordered copy: the item's topics are contiguous
 #pragma unroll
-      for (int u = 0; u < 4; ++u) k[u] = tk[u] != 0xFFFFFFFFu ? z[tk[u]] : -1;
+        for (int u = 0; u < 4; ++u) k[u] = (i + 64 * u < len) ? zw[b + (uint32_t)(i + 64 * u)] : -1;
+      } else {
+        uint32_t tk[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) tk[u] = (i + 64 * u < len) ? perm[b + (uint32_t)(i + 64 * u)] : 0xFFFFFFFFu;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) k[u] = tk[u] != 0xFFFFFFFFu ? z[tk[u]] : -1;
+      }
 #pragma unroll
       for (int u = 0; u < 4; ++u)
         if (k[u] >= 0) atomicAdd(&hist[k[u]], 1);
@@ -3335,17 +3347,35 @@ hipError_t launch_word_scatter(const int32_t* words, int64_t n, const PartSpans&
   return hipGetLastError();
 }
 
-hipError_t launch_recount(int32_t Kp, const uint32_t* perm, const int32_t* items, int32_t n_items,
+__global__ __launch_bounds__(256) void k_zw_build(const uint32_t* __restrict__ perm, int64_t n,
+                                                  const int32_t* __restrict__ z, uint32_t* __restrict__ zpos,
+                                                  int32_t* __restrict__ zw) {
+  for (int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x; j < n; j += (int64_t)gridDim.x * 256) {
+    const uint32_t i = perm[j];
+    zpos[i] = (uint32_t)j;
+    zw[j] = z[i];
+  }
+}
+
+hipError_t launch_zw_build(const uint32_t* perm, int64_t n, const int32_t* z, uint32_t* zpos, int32_t* zw,
+                           hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  const int blocks = (int)std::min<int64_t>((n + 255) / 256, 16384);
+  hipLaunchKernelGGL(k_zw_build, dim3(blocks), dim3(256), 0, st, perm, n, z, zpos, zw);
+  return hipGetLastError();
+}
+
+hipError_t launch_recount(int32_t Kp, const uint32_t* perm, const int32_t* zw, const int32_t* items, int32_t n_items,
                           const int32_t* z, int32_t* buf, int32_t* bufsum, int blocks, hipStream_t st) {
   if (n_items <= 0) return hipSuccess;
   blocks = std::max(1, std::min(blocks, (n_items + 3) / 4));
   const int4* it = reinterpret_cast<const int4*>(items);
   switch (Kp / 64) {
-    case 1: hipLaunchKernelGGL(k_recount<1>, dim3(blocks), dim3(256), 0, st, perm, it, n_items, z, buf, bufsum); break;
-    case 2: hipLaunchKernelGGL(k_recount<2>, dim3(blocks), dim3(256), 0, st, perm, it, n_items, z, buf, bufsum); break;
-    case 4: hipLaunchKernelGGL(k_recount<4>, dim3(blocks), dim3(256), 0, st, perm, it, n_items, z, buf, bufsum); break;
-    case 8: hipLaunchKernelGGL(k_recount<8>, dim3(blocks), dim3(256), 0, st, perm, it, n_items, z, buf, bufsum); break;
-    case 16: hipLaunchKernelGGL(k_recount<16>, dim3(blocks), dim3(256), 0, st, perm, it, n_items, z, buf, bufsum); break;
+    case 1: hipLaunchKernelGGL(k_recount<1>, dim3(blocks), dim3(256), 0, st, perm, zw, it, n_items, z, buf, bufsum); break;
+    case 2: hipLaunchKernelGGL(k_recount<2>, dim3(blocks), dim3(256), 0, st, perm, zw, it, n_items, z, buf, bufsum); break;
+    case 4: hipLaunchKernelGGL(k_recount<4>, dim3(blocks), dim3(256), 0, st, perm, zw, it, n_items, z, buf, bufsum); break;
+    case 8: hipLaunchKernelGGL(k_recount<8>, dim3(blocks), dim3(256), 0, st, perm, zw, it, n_items, z, buf, bufsum); break;
+    case 16: hipLaunchKernelGGL(k_recount<16>, dim3(blocks), dim3(256), 0, st, perm, zw, it, n_items, z, buf, bufsum); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();
