@@ -92,7 +92,13 @@ void lda_destroy(lda_ctx* ctx);
 
 /* Run n full sweeps on a single (unsharded) context: apply any pending delta,
  * then n x (sample + apply).  Replaces ParallelTopicModel.estimate() with
- * setNumIterations(n) and optimizeInterval 0 [src/cmu_ron/TrainAndPredict.java:165-166]. */
+ * setNumIterations(n) and optimizeInterval 0 [src/cmu_ron/TrainAndPredict.java:165-166].
+ * Plain dense sweeps (one part, not warm-start or recount sweeps) are
+ * launched as hipGraphs of up to 16 sweeps, captured once per length on the
+ * context's stream; the results are those of n lda_sample + lda_apply calls
+ * (the sweep counter and beta are read from device memory).  No event timing
+ * is recorded for them (lda_sample_times covers lda_sample launches).  The
+ * environment variable LDA_GRAPHS=0 at lda_create turns the graphs off. */
 lda_status lda_sweep(lda_ctx* ctx, int32_t n);
 
 /* One sampling pass over the shard against the current nw/nwsum snapshot
@@ -126,7 +132,11 @@ lda_status lda_count_update_mode(lda_ctx* ctx, int32_t* recount);
  *  LDA_COUNT_RECOUNT  every sweep;  LDA_COUNT_DELTA  none.
  * Shards exchanging buffers must agree on it sweep by sweep: a distributed
  * driver sets the same mode and count on every rank (ADLDATrainer: the
- * minimum over ranks).  Results are identical in every mode. */
+ * minimum over ranks).  Results are identical in every mode.  On recount
+ * sweeps the K <= 128 default sampler also keeps a copy of z in the
+ * recount's word order (N int32 + N uint32 of device memory, allocated at
+ * the first recount sweep) so that the recount streams it instead of
+ * gathering z; LDA_ZW=0 at lda_create turns the copy off. */
 #define LDA_COUNT_AUTO 0
 #define LDA_COUNT_RECOUNT 1
 #define LDA_COUNT_DELTA 2
