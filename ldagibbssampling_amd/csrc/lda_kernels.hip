@@ -1886,6 +1886,13 @@ __global__ __launch_bounds__(256) void k_sample_sparse(SampleParams p) {
 #ifndef SB_DBUF
 #define SB_DBUF SB_BUF
 #endif
+// the add-back of a token's new topic deferred to the next token of its
+// document and folded into that token's removal: one LDS update block and one
+// row pass per token (rows: the previous token's old and new groups, this
+// token's group) instead of two
+#ifndef SB_DEFER
+#define SB_DEFER 1
+#endif
 // gfx9 buffer resource word 3 (raw 32-bit loads, bounds checked)
 [[maybe_unused]] constexpr int kBufWord3 = 0x00020000;
 static_assert(SB_RB % SB_GRP == 0 && (SB_DBUF || SB_BATCH % SB_GRP == 0), "round groups");
@@ -1969,8 +1976,8 @@ __global__ __launch_bounds__(64 * sb_waves<C>()) void k_sample_sparse_big(Sample
 #pragma unroll
     for (int q = 0; q < NG; ++q) TG[q] = (tkey[q] == key) ? v : TG[q];
   };
-  // group g of lane owner, read out to every lane
-  auto tg_at = [&](const tg_t& TG, int owner, int g) -> float {
+  // group g of lane owner, read out to every lane (the non-deferred path)
+  [[maybe_unused]] auto tg_at = [&](const tg_t& TG, int owner, int g) -> float {
     const int key = owner * NG + g;
     float v = 0.0f;
 #pragma unroll
@@ -1982,7 +1989,7 @@ __global__ __launch_bounds__(64 * sb_waves<C>()) void k_sample_sparse_big(Sample
     const float cur = TG[g];
     TG[g] = (lane == owner) ? v : cur;
   };
-  auto tg_at = [&](const tg_t& TG, int owner, int g) -> float { return readlane_f(TG[g], owner); };
+  [[maybe_unused]] auto tg_at = [&](const tg_t& TG, int owner, int g) -> float { return readlane_f(TG[g], owner); };
 #endif
   auto lane_total = [&](const tg_t& TG) -> float {
     float t = TG[0];
@@ -2111,6 +2118,10 @@ __global__ __launch_bounds__(64 * sb_waves<C>()) void k_sample_sparse_big(Sample
     for (int s = 0; s < NS - 1; ++s)
       if (SB_BUF || s < t1) prefetch(ring[s], cinv[s], s);
 
+    // the previous token of this document: its new topic still to add back
+    // (pk < 0: none) and its old / new groups, whose sums are refreshed with
+    // this token's removal (SB_DEFER)
+    int pk = -1, plo = 0, pgo = 0, pln = 0, pgn = 0;
     for (int tb = 0; tb < t1; tb += NS) {
 #pragma unroll
       for (int s = 0; s < NS; ++s) {
@@ -2143,6 +2154,7 @@ __global__ __launch_bounds__(64 * sb_waves<C>()) void k_sample_sparse_big(Sample
             while (p.doc_off[doc + 1] - t0 <= t) ++doc;
             doc_end = uniform_i((int)(p.doc_off[doc + 1] - t0));
             build_doc(t, doc_end);
+            pk = -1;                       // the last document's add-back is moot
           }
 
           const int w = readlane_i(cw, idx);
@@ -2162,12 +2174,34 @@ __global__ __launch_bounds__(64 * sb_waves<C>()) void k_sample_sparse_big(Sample
           // while the token is out: topic zc's coefficient uses invc (inv_m1[zo])
           const int zc = FROZEN ? -1 : zo;
           const float invc = FROZEN ? 0.0f : cinv[s];
+#if SB_DEFER
+          // add the previous token back under its new topic and remove this
+          // one, then one pass: row 0 / 1 the previous token's old / new
+          // group, rows 2-3 this token's (set last: it may be one of them)
+          if (lane == 0) {
+            if (pk >= 0) nd2[pk >> 1] += (pk & 1) ? 0x10000u : 1u;
+            nd2[zo >> 1] -= (zo & 1) ? 0x10000u : 1u;
+          }
+          wave_lds_fence();
+          {
+            const bool own_row = row >= 2;
+            const int ow = row == 0 ? plo : (row == 1 ? pln : lo);
+            const int og = row == 0 ? pgo : (row == 1 ? pgn : go);
+            const float x = row_scan16(coef_at(ow * C + og * 16 + col, own_row ? zc : -1, own_row ? invc : 0.0f) * beta);
+            if (pk >= 0) {
+              set_tg(TG, plo, pgo, readlane_f(x, 15));
+              set_tg(TG, pln, pgn, readlane_f(x, 31));
+            }
+            set_tg(TG, lo, go, readlane_f(x, 47));
+          }
+#else
           const float g_saved = tg_at(TG, lo, go);
 
           // remove the token from its document; re-evaluate its group
           if (lane == 0) nd2[zo >> 1] -= (zo & 1) ? 0x10000u : 1u;
           wave_lds_fence();
           set_tg(TG, lo, go, readlane_f(row_pass(lo, go, zc, invc), 15));
+#endif
 
           // word part, register rounds: lane l holds entry l + 64 q; accq[q]
           // = the lane's running sum after round q
@@ -2362,6 +2396,14 @@ __global__ __launch_bounds__(64 * sb_waves<C>()) void k_sample_sparse_big(Sample
             kn = lstar * C + (cnt < C ? cnt : last_j);
           }
 
+#if SB_DEFER
+          // the add-back waits for the document's next token
+          pk = kn;
+          plo = lo;
+          pgo = go;
+          pln = (int)((uint32_t)kn / (uint32_t)C);
+          pgn = (int)(((uint32_t)kn % (uint32_t)C) / 16u);
+#else
           // add the token back under its new topic
           if (lane == 0) nd2[kn >> 1] += (kn & 1) ? 0x10000u : 1u;
           wave_lds_fence();
@@ -2378,6 +2420,7 @@ __global__ __launch_bounds__(64 * sb_waves<C>()) void k_sample_sparse_big(Sample
             set_tg(TG, lo, go, gl);
             set_tg(TG, ln, gn, gk);
           }
+#endif
           cn = (lane == idx) ? kn : cn;
         }
       }
