@@ -295,6 +295,9 @@ struct lda_ctx {
 
   ~lda_ctx() {
     if (device >= 0) (void)hipSetDevice(device);
+    // work still queued (graph sweeps, asynchronous uploads and read-backs)
+    // finishes before its buffers, graphs and pinned staging are released
+    if (device >= 0) (void)hipDeviceSynchronize();
     for (void* p : {(void*)words, (void*)z, (void*)doc_off, (void*)range_doc, (void*)queue,
                     (void*)nw, (void*)nwsum, (void*)delta, (void*)alpha_d, (void*)alpha_f,
                     (void*)inv, (void*)inv_m1, (void*)partial, (void*)nonzero, (void*)ent,
