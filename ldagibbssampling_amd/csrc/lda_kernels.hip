@@ -2788,6 +2788,13 @@ __global__ __launch_bounds__(256) void k_ll_words(const int32_t* __restrict__ nw
 // Mallet's alpha statistics (WorkerRunnable, shouldSaveState): per document
 // docLengthCounts[len]++ and topicDocCounts[k][n_dk]++ for every n_dk > 0;
 // one wavefront per document, the document's counts in LDS.
+// The block's counts of document lengths up to DOC_HIST_LEN and of (topic,
+// count) pairs with count <= DOC_HIST_SMALL are summed in LDS and added to the
+// device histograms once per block: the same few cells (common lengths, a
+// topic held once) took every document's device atomic and serialised on it
+// (25 us a launch at the reference's 2000 documents).
+#define DOC_HIST_LEN 1024
+#define DOC_HIST_SMALL 4
 __global__ __launch_bounds__(256) void k_doc_hist(const int32_t* __restrict__ z,
                                                   const int64_t* __restrict__ doc_off, int64_t D,
                                                   int32_t K, int32_t Kp, int32_t L,
@@ -2796,22 +2803,35 @@ __global__ __launch_bounds__(256) void k_doc_hist(const int32_t* __restrict__ z,
   extern __shared__ __attribute__((aligned(16))) int32_t h[];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   int32_t* hist = h + wid * Kp;
-  for (int i = lane; i < Kp; i += 64) hist[i] = 0;
-  wave_lds_fence();
+  int32_t* len_l = h + 4 * Kp;                       // [DOC_HIST_LEN]
+  int32_t* small = len_l + DOC_HIST_LEN;              // [K][DOC_HIST_SMALL], count c at c - 1
+  for (int i = threadIdx.x; i < 4 * Kp + DOC_HIST_LEN + K * DOC_HIST_SMALL; i += 256) h[i] = 0;
+  __syncthreads();
   for (int64_t d = (int64_t)blockIdx.x * 4 + wid; d < D; d += (int64_t)gridDim.x * 4) {
     const int64_t t0 = doc_off[d], t1 = doc_off[d + 1];
     for (int64_t i = t0 + lane; i < t1; i += 64) atomicAdd(&hist[z[i]], 1);
     wave_lds_fence();
-    if (lane == 0) atomicAdd(&len_hist[t1 - t0], 1);
+    if (lane == 0) {
+      const int64_t n = t1 - t0;
+      if (n < DOC_HIST_LEN) atomicAdd(&len_l[n], 1);
+      else atomicAdd(&len_hist[n], 1);
+    }
     // each of the document's topics taken once through its tokens (as k_ll_docs)
     for (int64_t i = t0 + lane; i < t1; i += 64) {
       const int k = z[i];
       const int32_t c = atomicExch(&hist[k], 0);
-      if (c > 0) atomicAdd(&topic_hist[(int64_t)k * (L + 1) + c], 1);
+      if (c > 0 && c <= DOC_HIST_SMALL) atomicAdd(&small[k * DOC_HIST_SMALL + c - 1], 1);
+      else if (c > 0) atomicAdd(&topic_hist[(int64_t)k * (L + 1) + c], 1);
     }
     wave_lds_fence();
   }
-  (void)K;
+  __syncthreads();
+  for (int i = threadIdx.x; i < DOC_HIST_LEN && i <= L; i += 256)
+    if (len_l[i]) atomicAdd(&len_hist[i], len_l[i]);
+  for (int i = threadIdx.x; i < K * DOC_HIST_SMALL; i += 256) {
+    const int c = i % DOC_HIST_SMALL + 1;
+    if (small[i] && c <= L) atomicAdd(&topic_hist[(int64_t)(i / DOC_HIST_SMALL) * (L + 1) + c], small[i]);
+  }
 }
 
 // optimizeBeta's countHistogram: cells of nw (k < K) holding each count > 0.
@@ -3343,8 +3363,15 @@ hipError_t launch_ll_words(const int32_t* nw, int64_t V, int32_t K, int32_t Kp, 
 hipError_t launch_doc_hist(const int32_t* z, const int64_t* doc_off, int64_t D, int32_t K, int32_t Kp,
                            int32_t L, int32_t* len_hist, int32_t* topic_hist, hipStream_t st) {
   if (D <= 0) return hipSuccess;
-  const int blocks = (int)std::min<int64_t>((D + 3) / 4, 4096);
-  hipLaunchKernelGGL(k_doc_hist, dim3(blocks), dim3(256), 4 * Kp * sizeof(int32_t), st, z, doc_off, D,
+  // >= 8 documents per wave, so the per-block flush is amortised
+  const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>((D + 31) / 32, 1024));
+  const size_t lds = (4 * (size_t)Kp + DOC_HIST_LEN + (size_t)K * DOC_HIST_SMALL) * sizeof(int32_t);
+  if (lds > 65536) {   // K > 1024: past the default dynamic LDS limit (160 KB per CU)
+    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_doc_hist),
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return e;
+  }
+  hipLaunchKernelGGL(k_doc_hist, dim3(blocks), dim3(256), lds, st, z, doc_off, D,
                      K, Kp, L, len_hist, topic_hist);
   return hipGetLastError();
 }
@@ -3352,7 +3379,10 @@ hipError_t launch_doc_hist(const int32_t* z, const int64_t* doc_off, int64_t D, 
 hipError_t launch_count_hist(const int32_t* nw, int64_t V, int32_t K, int32_t Kp, int64_t max_count,
                              int32_t* hist, int32_t* overflow, hipStream_t st) {
   if (V <= 0) return hipSuccess;
-  const int blocks = (int)std::min<int64_t>((V * Kp + 255) / 256, 4096);
+  // each block clears and flushes a 16 KB LDS histogram: >= 16 cells per
+  // thread keep that off the small models' launch (4096 blocks of ~2 cells
+  // each had taken 28 us at V = 5000, K = 500)
+  const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>((V * Kp + 4095) / 4096, 1024));
   hipLaunchKernelGGL(k_count_hist, dim3(blocks), dim3(256), 0, st, nw, V, K, Kp, max_count, hist,
                      overflow);
   return hipGetLastError();
