@@ -79,3 +79,30 @@ def test_graph_sweeps_across_parts_warm_start_and_recount(oracle, monkeypatch):
     o.set_warm_start(3, 6, 0, c.num_tokens)
     o.sweep(9 + 20 + 3 + 21)
     _same(g, o)
+
+
+def test_graph_sweeps_follow_sweep_counter_and_stream(monkeypatch):
+    """The sweep counter set between graph launches (lda_set_sweep, as a
+    resumed checkpoint does) and a change of stream (lda_set_stream: the
+    graphs are rebuilt for it) give the one-by-one path's state."""
+    import torch
+    c = synthetic_changelists(num_docs=500, num_types=800, seed=9)
+    K = 48
+    g = _make(c, K, 21, True, monkeypatch)
+    n = _make(c, K, 21, False, monkeypatch)
+    for s in (g, n):
+        s.sweep(5)
+        s.sweep_index = 2            # rewind the Philox sweep word
+        s.sweep(7)
+    assert g.sweep_index == n.sweep_index == 9
+    _same(g, n)
+    st = torch.cuda.Stream()
+    for s in (g, n):
+        s.set_stream(st.cuda_stream)
+        s.sweep(19)
+        s.synchronize()
+    _same(g, n)
+    for s in (g, n):
+        s.set_stream(None)
+        s.sweep(3)
+    _same(g, n)
