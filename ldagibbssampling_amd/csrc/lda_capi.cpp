@@ -170,6 +170,7 @@ struct lda_ctx {
   uint32_t* ent = nullptr;
   int64_t* row_off = nullptr;
   int32_t* row_nnz = nullptr;
+  uint32_t* row_rnd = nullptr;   // row_off / 64: the large-K sampler's 32-bit row starts
   bool rows_ready = false;
   int half = 0;    // dense K <= 128: 1 = the half-wave variant, 2 = the quarter-wave one (LDA_DENSE_HALF)
   // lda_infer: word totals of the snapshot (TopicInferencer's empty-row test),
@@ -301,7 +302,7 @@ struct lda_ctx {
     for (void* p : {(void*)words, (void*)z, (void*)doc_off, (void*)range_doc, (void*)queue,
                     (void*)nw, (void*)nwsum, (void*)delta, (void*)alpha_d, (void*)alpha_f,
                     (void*)inv, (void*)inv_m1, (void*)partial, (void*)nonzero, (void*)ent,
-                    (void*)row_off, (void*)row_nnz, (void*)nw16, (void*)wide, (void*)inf_words,
+                    (void*)row_off, (void*)row_nnz, (void*)row_rnd, (void*)nw16, (void*)wide, (void*)inf_words,
                     (void*)inf_z, (void*)inf_acc, (void*)inf_q, (void*)inf_doff, (void*)inf_range,
                     (void*)perm, (void*)items, (void*)warm_range_doc})
       if (p) (void)hipFree(p);
@@ -354,6 +355,7 @@ struct lda_ctx {
     p.ent = ent;
     p.row_off = row_off;
     p.row_nnz = row_nnz;
+    p.row_rnd = row_rnd;
     p.nw16 = nw16;
     p.wide = wide;
     (void)frozen;
@@ -377,10 +379,16 @@ static lda_status build_row_capacity(lda_ctx* c) {
   off[0] = 0;
   // whole rounds of 64 entries (k_build_sparse zero-fills the padding)
   for (int w = 0; w < c->V; ++w) off[w + 1] = off[w] + ((h[w] + 63) & ~int64_t(63));
+  // the large-K sampler reads a row's start as a 32-bit count of whole
+  // rounds: 2^32 rounds are 2^38 entries (1 TiB), beyond any device memory
+  std::vector<uint32_t> rnd(c->V);
+  for (int w = 0; w < c->V; ++w) rnd[w] = (uint32_t)(off[w] >> 6);
   HIP_TRY(dalloc(&c->row_off, c->V + 1));
   HIP_TRY(dalloc(&c->row_nnz, c->V));
+  HIP_TRY(dalloc(&c->row_rnd, c->V));
   HIP_TRY(dalloc(&c->ent, (size_t)off[c->V]));
   HIP_TRY(hipMemcpyAsync(c->row_off, off.data(), sizeof(int64_t) * (c->V + 1), hipMemcpyHostToDevice, c->stream));
+  HIP_TRY(hipMemcpyAsync(c->row_rnd, rnd.data(), sizeof(uint32_t) * c->V, hipMemcpyHostToDevice, c->stream));
   HIP_TRY(hipStreamSynchronize(c->stream));
   c->rows_ready = true;
   return LDA_OK;

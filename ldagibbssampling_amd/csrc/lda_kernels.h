@@ -67,6 +67,7 @@ struct SampleParams {
   const uint32_t* ent;      // packed (count << 12) | topic, count saturated at 0xFFFFF
   const int64_t* row_off;   // [V+1] capacity offsets (min(Kp, word total) per row)
   const int32_t* row_nnz;   // [V] live entries per row; sign bit: the row has a saturated count
+  const uint32_t* row_rnd;  // [V] row_off / 64 (rows start on whole 64-entry rounds)
   float* trace;             // debug only: 8 floats per token when non-null
   // 16-bit copy of the snapshot rows (k_sample)
   const uint16_t* nw16;     // [V*Kp] counts, clamped at 65535

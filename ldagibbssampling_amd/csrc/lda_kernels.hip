@@ -1886,6 +1886,15 @@ __global__ __launch_bounds__(256) void k_sample_sparse(SampleParams p) {
 #ifndef SB_DBUF
 #define SB_DBUF SB_BUF
 #endif
+// the double-buffered batch loop runs whole batches only and sums the row's
+// last partial batch round by round (no zero rounds past the row's end)
+#ifndef SB_REM
+#define SB_REM 0
+#endif
+// row starts read as 32-bit round counts (row_rnd) instead of 64-bit offsets
+#ifndef SB_OFF32
+#define SB_OFF32 1
+#endif
 // the add-back of a token's new topic deferred to the next token of its
 // document and folded into that token's removal: one LDS update block and one
 // row pass per token (rows: the previous token's old and new groups, this
@@ -1936,7 +1945,21 @@ __global__ __launch_bounds__(64 * sb_waves<C>()) void k_sample_sparse_big(Sample
   const int last_lane = (p.K - 1) / C;
   const int32_t* __restrict__ nw = p.nw;
   const uint32_t* __restrict__ ent = p.ent;
+#if SB_OFF32
+  // a row's start as a 32-bit count of whole 64-entry rounds: one VGPR and one
+  // readlane per row offset instead of two
+  const uint32_t* __restrict__ row_off = p.row_rnd;
+  typedef uint32_t roff_t;
+  auto row_ptr = [&](roff_t o) -> const uint32_t* { return ent + ((uint64_t)o << 6); };
+  auto readlane_o = [&](roff_t v, int l) -> roff_t { return (roff_t)readlane_i((int)v, l); };
+#else
   const int64_t* __restrict__ row_off = p.row_off;
+  typedef int64_t roff_t;
+  auto row_ptr = [&](roff_t o) -> const uint32_t* { return ent + o; };
+  auto readlane_o = [&](roff_t v, int l) -> roff_t {
+    return ((int64_t)readlane_i((int)(v >> 32), l) << 32) | (uint32_t)readlane_i((int)v, l);
+  };
+#endif
   const int32_t* __restrict__ row_nnz = p.row_nnz;
   const float* __restrict__ inv_m1 = p.inv_m1;
 
@@ -2031,7 +2054,7 @@ __global__ __launch_bounds__(64 * sb_waves<C>()) void k_sample_sparse_big(Sample
       z2 = zr[128 + lane];
     }
     int cmn = row_nnz[cw], m1n = row_nnz[w1];
-    int64_t cmo = row_off[cw], m1o = row_off[w1];
+    roff_t cmo = row_off[cw], m1o = row_off[w1];
     int cn = cz;
     float cu = u01(draw_u32(gbase + (uint64_t)lane, p.c2, p.c3, p.k0, p.k1));
 
@@ -2087,27 +2110,26 @@ __global__ __launch_bounds__(64 * sb_waves<C>()) void k_sample_sparse_big(Sample
     auto prefetch = [&](uint32_t (&rg)[SB_RB], float& ci, int tp) {
       const int pidx = tp - cbase;
       int np, zp;
-      int64_t op;
+      roff_t op;
       if (pidx < 64) {
         np = readlane_i(cmn, pidx);
-        op = ((int64_t)readlane_i((int)(cmo >> 32), pidx) << 32) | (uint32_t)readlane_i((int)cmo, pidx);
+        op = readlane_o(cmo, pidx);
         zp = readlane_i(cz, pidx);
       } else {
         np = readlane_i(m1n, pidx - 64);
-        op = ((int64_t)readlane_i((int)(m1o >> 32), pidx - 64) << 32) |
-             (uint32_t)readlane_i((int)m1o, pidx - 64);
+        op = readlane_o(m1o, pidx - 64);
         zp = readlane_i(z1, pidx - 64);
       }
 #if SB_BUF
       // past the range end: an empty row (every load returns 0)
       const int nrp = tp < t1 ? ((np & 0x7FFFFFFF) + 63) >> 6 : 0;
       const __amdgpu_buffer_rsrc_t rs =
-          __builtin_amdgcn_make_buffer_rsrc((void*)(ent + op), (short)0, nrp * 256, kBufWord3);
+          __builtin_amdgcn_make_buffer_rsrc((void*)row_ptr(op), (short)0, nrp * 256, kBufWord3);
 #pragma unroll
       for (int q = 0; q < SB_RB; ++q) rg[q] = __builtin_amdgcn_raw_buffer_load_b32(rs, lane * 4 + q * 256, 0, 0);
 #else
       const int nrp = ((np & 0x7FFFFFFF) + 63) >> 6;
-      const uint32_t* rp = ent + op + lane;
+      const uint32_t* rp = row_ptr(op) + lane;
 #pragma unroll
       for (int q = 0; q < SB_RB; ++q)
         if (q < nrp) rg[q] = rp[q * 64];
@@ -2163,7 +2185,8 @@ __global__ __launch_bounds__(64 * sb_waves<C>()) void k_sample_sparse_big(Sample
           const int n_raw = readlane_i(cmn, idx);
           const bool row_sat = n_raw < 0;           // the row holds a saturated count
           const int n = n_raw & 0x7FFFFFFF;
-          const int64_t off = ((int64_t)readlane_i((int)(cmo >> 32), idx) << 32) | (uint32_t)readlane_i((int)cmo, idx);
+          const roff_t off = readlane_o(cmo, idx);
+          const uint32_t* __restrict__ erow = row_ptr(off);
 #if SB_UDIV
           const int lo = (int)((uint32_t)zo / (uint32_t)C);
           const int go = (int)(((uint32_t)zo % (uint32_t)C) / 16u);
@@ -2255,13 +2278,21 @@ __global__ __launch_bounds__(64 * sb_waves<C>()) void k_sample_sparse_big(Sample
           // summed; loads past the row return 0, and a 0 entry adds +0
           auto batches = [&](bool sat) {
             const __amdgpu_buffer_rsrc_t rb =
-                __builtin_amdgcn_make_buffer_rsrc((void*)(ent + off), (short)0, nr_all * 256, kBufWord3);
+                __builtin_amdgcn_make_buffer_rsrc((void*)erow, (short)0, nr_all * 256, kBufWord3);
             uint32_t ea[SB_BATCH];
 #pragma unroll
             for (int b = 0; b < SB_BATCH; ++b)
               ea[b] = __builtin_amdgcn_raw_buffer_load_b32(rb, lane * 4 + (SB_RB + b) * 256, 0, 0);
             int mb = 0;
+#if SB_REM
+            // whole batches only; the row's last 1..SB_BATCH-1 rounds below,
+            // without the zero rounds that pad them to a batch (a +0 term
+            // leaves the sum unchanged, so skipping it keeps the order)
+            int q0 = SB_RB;
+            for (; q0 + SB_BATCH <= nr_all; q0 += SB_BATCH, ++mb) {
+#else
             for (int q0 = SB_RB; q0 < nr_all; q0 += SB_BATCH, ++mb) {
+#endif
               uint32_t en[SB_BATCH];
               const int vo = lane * 4 + (q0 + SB_BATCH) * 256;
 #pragma unroll
@@ -2273,13 +2304,23 @@ __global__ __launch_bounds__(64 * sb_waves<C>()) void k_sample_sparse_big(Sample
 #pragma unroll
               for (int b = 0; b < SB_BATCH; ++b) ea[b] = en[b];
             }
+#if SB_REM
+            const int rem = nr_all - q0;   // uniform, 0 .. SB_BATCH-1
+            if (rem > 0) {
+#pragma unroll
+              for (int b = 0; b < SB_BATCH - 1; ++b)
+                if (b < rem) acc = acc + term_of(ea[b], w, zc, invc, sat);
+#pragma unroll
+              for (int i = 0; i < SB_NB; ++i) accb[i] = (mb == i) ? acc : accb[i];
+            }
+#endif
           };
 #else
           auto batches = [&](bool sat) {
             int mb = 0;
             for (int q0 = SB_RB; q0 < nr_all; q0 += SB_BATCH, ++mb) {
               uint32_t eb[SB_BATCH];
-              const uint32_t* rp = ent + off + lane + q0 * 64;
+              const uint32_t* rp = erow + lane + q0 * 64;
 #pragma unroll
               for (int b = 0; b < SB_BATCH; ++b) eb[b] = (q0 + b < nr_all) ? rp[b * 64] : 0u;
 #pragma unroll
@@ -2350,14 +2391,14 @@ __global__ __launch_bounds__(64 * sb_waves<C>()) void k_sample_sparse_big(Sample
                 if (i < nbl && cb == i && E + readlane_f(accb[i], lstar) <= thr) cb = i + 1;
               if (cb == nbl) {
                 sel = -1;                 // none exceeds: the lane's last round
-                const uint32_t e = (uint32_t)ent[off + lstar + 64 * (nr - 1)];
+                const uint32_t e = erow[lstar + 64 * (nr - 1)];
                 kn = (int)(e & ENT_TOPIC_MASK);
               } else {
                 // rounds r0.. of lane lstar (one batch, or all the rest past the
                 // kept batches), one per lane, continuing its serial sum
                 const int r0 = SB_RB + SB_BATCH * cb;
                 const int nx = (cb < SB_NB ? min(nr, r0 + SB_BATCH) : nr) - r0;
-                const uint32_t e = lane < nx ? ent[off + lstar + 64 * (r0 + lane)] : 0u;
+                const uint32_t e = lane < nx ? erow[lstar + 64 * (r0 + lane)] : 0u;
                 const float term = term_of(e, w, zc, invc, row_sat);
                 float a = readlane_f(accq[SB_RB - 1], lstar);
 #pragma unroll

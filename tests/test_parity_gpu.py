@@ -113,6 +113,36 @@ def test_large_k_sparse_long_rows_and_inference(oracle):
     np.testing.assert_allclose(tg, to, rtol=0, atol=1e-12)
 
 
+@pytest.mark.parametrize("K", [1500, 4096])
+def test_large_k_symmetric_and_asymmetric_alpha(oracle, K):
+    """The large-K sampler has a symmetric-alpha instantiation (alpha in a
+    register, an inv-only LDS table) and the general one; a run that switches
+    symmetric -> asymmetric -> symmetric alpha (as the optimisation does after
+    its burn-in) stays bit-exact through both, and so does inference."""
+    corpus = _ragged_corpus(D=80, V=600, seed=K + 3)
+    train = corpus.subset(range(0, 64))
+    held = corpus.subset(range(64, 80))
+    alpha = np.full(K, 20.0 / K)
+    g, o = _pair(oracle, train, K, alpha, 0.01, seed=K + 5, tokens_per_range=300, kind="sparse")
+    g.sweep(2)
+    o.sweep(2)
+    _assert_same_state(g, o)
+    rng = np.random.default_rng(K)
+    alpha2 = rng.uniform(0.5, 2.0, size=K) * (20.0 / K)
+    # one topic differing in its fp32 value is enough to leave the symmetric path
+    alpha3 = alpha.copy()
+    alpha3[K - 1] *= 1.25
+    for a in (alpha2, alpha3, np.full(K, 30.0 / K)):
+        g.set_alpha_beta(a, 0.02)
+        o.set_alpha_beta(a, 0.02)
+        g.sweep(2)
+        o.sweep(2)
+        _assert_same_state(g, o)
+        tg = g.infer(held.doc_off, held.words, n_iter=4, burn_in=1, thin=1, seed=3)
+        to = o.infer(held.doc_off, held.words, n_iter=4, burn_in=1, thin=1, seed=3)
+        np.testing.assert_allclose(tg, to, rtol=0, atol=1e-12)
+
+
 def test_large_k_limits():
     from ldagibbssampling_amd.sampler import GibbsSampler
     from ldagibbssampling_amd.capi import LdaError
