@@ -1895,6 +1895,10 @@ __global__ __launch_bounds__(256) void k_sample_sparse(SampleParams p) {
 #ifndef SB_OFF32
 #define SB_OFF32 1
 #endif
+// the per-token document-count updates as no-return LDS atomics
+#ifndef SB_NDATOM
+#define SB_NDATOM 1
+#endif
 // the add-back of a token's new topic deferred to the next token of its
 // document and folded into that token's removal: one LDS update block and one
 // row pass per token (rows: the previous token's old and new groups, this
@@ -2202,8 +2206,18 @@ __global__ __launch_bounds__(64 * sb_waves<C>()) void k_sample_sparse_big(Sample
           // one, then one pass: row 0 / 1 the previous token's old / new
           // group, rows 2-3 this token's (set last: it may be one of them)
           if (lane == 0) {
+#if SB_NDATOM
+            // no-return LDS atomics: both updates in flight at once (a plain
+            // += / -= is a read, a wait and a write each, one after the other)
+            if (pk >= 0)
+              __hip_atomic_fetch_add(&nd2[pk >> 1], (pk & 1) ? 0x10000u : 1u, __ATOMIC_RELAXED,
+                                     __HIP_MEMORY_SCOPE_WAVEFRONT);
+            __hip_atomic_fetch_add(&nd2[zo >> 1], (zo & 1) ? 0xFFFF0000u : 0xFFFFFFFFu, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_WAVEFRONT);
+#else
             if (pk >= 0) nd2[pk >> 1] += (pk & 1) ? 0x10000u : 1u;
             nd2[zo >> 1] -= (zo & 1) ? 0x10000u : 1u;
+#endif
           }
           wave_lds_fence();
           {
