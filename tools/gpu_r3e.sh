@@ -22,10 +22,15 @@ line() {  # name, bench args
   python3 -c "import json;d=json.loads(open('$O/bench_$N.jsonl').read());r=d['roofline'];print('$N', round(d['value']/1e9,4),'Gtok/s', round(d['ms_per_step'],3),'ms kernel',round(r['kernel_ms_timed_region'],3),'frac',round(r['frac'],3),'traffic',r.get('traffic'),'traffic_frac',r.get('traffic_frac'))"
 }
 # two calls (each under gpurun's 20-minute limit): "prof" then "lines"
+# ("profc4c2": the C4 and C2 profiles alone, after a large-K-only change)
 case ${1:-all} in
   prof|all) prof c4 "k_sample<8, 3, false>" 2000000000 512 --config c4 && \
             prof c2 "k_sample_quarter<8, 4, false>" 20000000 128 --config c2 && \
             prof c5 "k_sample_sparse_big<64, 3, false>" 250000000 4096 --config c5 || exit 1 ;;
+esac
+case ${1:-all} in
+  profc4c2) prof c4 "k_sample<8, 3, false>" 2000000000 512 --config c4 && \
+            prof c2 "k_sample_quarter<8, 4, false>" 20000000 128 --config c2 || exit 1 ;;
 esac
 case ${1:-all} in
   lines|all) line c4 && line c2 --config c2 --no-cpu-baseline && line c3 --config c3 --no-cpu-baseline && \
