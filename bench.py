@@ -72,12 +72,14 @@ def _newest(pattern):
     return sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", pattern)))[::-1]
 
 
-def pmc_record(tokens_per_launch: int, kernel_prefix: str, K: int):
+def pmc_record(tokens_per_launch: int, kernel_prefix: str, K: int, burnin: int = 0):
     """The newest committed rocprofv3 summary (profiles/rNN/traffic_*.json,
     tools/make_traffic.py over separate FETCH_SIZE / WRITE_SIZE / SQ passes of
     this same command) measured on the kernel code loaded now (the library's
     sha256, or the sha256 of the kernel sources it is built from), for this
-    workload and kernel; (None, None) otherwise."""
+    workload, kernel and burn-in (a file without "burnin" profiled the
+    command without one: rows, change rates and bytes per token move with the
+    sweep window); (None, None) otherwise."""
     import hashlib
     from ldagibbssampling_amd import capi
     lib = os.environ.get("LDA_MI355X_LIB") or capi.LIB_PATH
@@ -97,7 +99,7 @@ def pmc_record(tokens_per_launch: int, kernel_prefix: str, K: int):
             src_sha is not None and t.get("kernel_src_sha256") == src_sha)
         if (t.get("tokens_per_launch") == tokens_per_launch and same_code
                 and t.get("kernel", "").startswith(kernel_prefix)
-                and t.get("num_topics", K) == K):
+                and t.get("num_topics", K) == K and t.get("burnin", 0) == burnin):
             return t, os.path.relpath(path, ROOT)
     return None, None
 
@@ -414,7 +416,7 @@ def main():
             enc_model = (f"16-bit row over Kp={sampler.Kp} topics (2 Kp) + word + z read + z write "
                          f"+ amortised delta (4 each)")
         achieved = n_local * enc / (kern_ms * 1e-3) / 1e9          # GB/s, shipped encoding
-        rec, rec_src = pmc_record(n_local, kname + "<", K)
+        rec, rec_src = pmc_record(n_local, kname + "<", K, args.burnin)
         traffic_gb = rec["hbm_bytes_per_launch"] / 1e9 if rec else None
         tok_s_kernel = n_local / (kern_ms * 1e-3)
         coll = None

@@ -100,3 +100,21 @@ def test_no_cpu_fallback_without_library(tmp_path):
             capi.load(str(tmp_path / "missing.so"))
     finally:
         capi._lib = saved
+
+
+def test_bench_traffic_record_matches_its_sweep_window():
+    """bench.py prices a line's PMC traffic only with a profile of the same
+    window: the committed C5 profile (the bench command near init) is found
+    for burn-in 0 on the kernel sources in the tree, and not for an
+    after-burn-in line, whose rows are shorter."""
+    import importlib.util
+    import os
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(root, "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    rec, src = bench.pmc_record(250_000_000, "k_sample_sparse_big<", 4096, 0)
+    if rec is None:
+        pytest.skip("no C5 profile of the kernel sources in the tree")
+    assert src.endswith("traffic_c5.json")
+    assert bench.pmc_record(250_000_000, "k_sample_sparse_big<", 4096, 30) == (None, None)
