@@ -74,7 +74,7 @@ def fetch_factor(pattern):
     return 0.5, "MI355X_MICROARCH.md §HBM (16 B/lane stream)"
 
 
-def main(d, kernel, tokens, workload, out, K=None):
+def main(d, kernel, tokens, workload, out, K=None, burnin=None):
     kt = json.load(open(os.path.join(d, "summary_kt.json")))
     fe = json.load(open(os.path.join(d, "summary_fetch.json")))["counters"][kernel]["FETCH_SIZE"]
     wr = json.load(open(os.path.join(d, "summary_write.json")))["counters"][kernel]["WRITE_SIZE"]
@@ -105,6 +105,9 @@ def main(d, kernel, tokens, workload, out, K=None):
     t["bytes_per_token"] = t["hbm_bytes_per_launch"] / t["tokens_per_launch"]
     if K is not None:
         t["num_topics"] = int(K)
+    if burnin is not None and int(burnin) > 0:
+        # the profiled command's --burnin (bench.py matches a line's window on it)
+        t["burnin"] = int(burnin)
     # instruction mix per token (wave-instructions: SQ_INSTS_* sum over all waves)
     mix = {}
     for name, counter in (("sq", "SQ_INSTS_VALU"), ("lds", "SQ_INSTS_SALU"), ("lds", "SQ_INSTS_LDS"),
@@ -131,4 +134,4 @@ def main(d, kernel, tokens, workload, out, K=None):
 
 
 if __name__ == "__main__":
-    main(*sys.argv[1:7])
+    main(*sys.argv[1:8])
