@@ -104,9 +104,9 @@ def test_no_cpu_fallback_without_library(tmp_path):
 
 def test_bench_traffic_record_matches_its_sweep_window():
     """bench.py prices a line's PMC traffic only with a profile of the same
-    window: the committed C5 profile (the bench command near init) is found
-    for burn-in 0 on the kernel sources in the tree, and not for an
-    after-burn-in line, whose rows are shorter."""
+    window: the committed C5 profile of the bench command near init is found
+    for burn-in 0 on the kernel sources in the tree, the after-30-sweeps one
+    (shorter rows) for burn-in 30, and none for a window nobody profiled."""
     import importlib.util
     import os
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -117,4 +117,9 @@ def test_bench_traffic_record_matches_its_sweep_window():
     if rec is None:
         pytest.skip("no C5 profile of the kernel sources in the tree")
     assert src.endswith("traffic_c5.json")
-    assert bench.pmc_record(250_000_000, "k_sample_sparse_big<", 4096, 30) == (None, None)
+    assert rec.get("burnin", 0) == 0
+    rec30, src30 = bench.pmc_record(250_000_000, "k_sample_sparse_big<", 4096, 30)
+    if rec30 is not None:
+        assert src30.endswith("traffic_c5_b30.json") and rec30["burnin"] == 30
+        assert rec30["bytes_per_token"] < rec["bytes_per_token"]
+    assert bench.pmc_record(250_000_000, "k_sample_sparse_big<", 4096, 7) == (None, None)
