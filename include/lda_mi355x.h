@@ -129,6 +129,13 @@ lda_status lda_count_update_mode(lda_ctx* ctx, int32_t* recount);
  *                     Infinity Cache (4 N <= 256 MiB), else 0 (measured
  *                     crossover: DESIGN.md §4).
  *                     recount_sweeps < 0 keeps the current value.
+ *                     Warm-start sweeps (lda_set_warm_start) never recount
+ *                     but do count toward the window: with the native
+ *                     ParallelTopicModel's default 4 x 50 warm start the
+ *                     window has passed before the first plain sweep, which
+ *                     is right, since after ~20 sweeps the delta is the
+ *                     faster update.  AUTO recount therefore
+ *                     acts when the warm start is off (lda_sweep, bench).
  *  LDA_COUNT_RECOUNT  every sweep;  LDA_COUNT_DELTA  none.
  * Shards exchanging buffers must agree on it sweep by sweep: a distributed
  * driver sets the same mode and count on every rank (ADLDATrainer: the
@@ -182,10 +189,20 @@ lda_status lda_delta_buffer_part(lda_ctx* ctx, int32_t part, void** dev_ptr, siz
  * parts in [1, LDA_MAX_EXCHANGE_PARTS] (1 = off).  The parts are cut in
  * the whole corpus, global token indices [corpus_first_token,
  * corpus_first_token + corpus_tokens) (corpus_tokens <= 0: this shard is the
- * whole corpus): part i is the documents starting at or after token
- * first + tokens * i / parts (and before the next cut), so a shard samples
- * its own documents of global part i in step i, and the result is the same
- * for any sharding and identical to cpu_exact's same schedule. */
+ * whole corpus), into S = parts * LDA_WARM_BLOCKS token-balanced segments:
+ * cut j is the first document starting at or after token
+ * first + tokens * j / S, and segment j belongs to part j % parts.  A shard
+ * samples its own documents of global part i in step i, so the result is the
+ * same for any sharding and identical to cpu_exact's same schedule, and every
+ * shard of a token-balanced sharding into <= LDA_WARM_BLOCKS shards has work
+ * in every step. */
+#define LDA_WARM_BLOCKS 64
+/* Host-only (no device call): the tokens a shard (documents doc_off[0..D],
+ * global token base + doc_off[d] - doc_off[0]) samples in each warm-start
+ * part of the corpus [corpus_first_token, + corpus_tokens), as
+ * lda_set_warm_start cuts them; tokens_out[parts]. */
+lda_status lda_warm_part_tokens(const int64_t* doc_off, int64_t num_docs, int32_t parts, int64_t token_base,
+                                int64_t corpus_first_token, int64_t corpus_tokens, int64_t* tokens_out);
 lda_status lda_set_warm_start(lda_ctx* ctx, int32_t parts, int32_t sweeps, int64_t corpus_first_token,
                               int64_t corpus_tokens);
 lda_status lda_get_warm_start(lda_ctx* ctx, int32_t* parts, int32_t* sweeps);
@@ -194,7 +211,8 @@ lda_status lda_get_warm_start(lda_ctx* ctx, int32_t* parts, int32_t* sweeps);
 lda_status lda_sweep_parts(lda_ctx* ctx, int32_t* parts, int32_t* sequential);
 
 /* The HIP stream every call of this context is ordered on (hipStream_t;
- * NULL = the context's own stream). */
+ * NULL = the context's own stream).  Work already queued on the previous
+ * stream is ordered before the new stream's (an event, no host wait). */
 lda_status lda_set_stream(lda_ctx* ctx, void* hip_stream);
 lda_status lda_get_stream(lda_ctx* ctx, void** hip_stream);
 lda_status lda_synchronize(lda_ctx* ctx);
@@ -344,8 +362,9 @@ void lda_debug_fail_host_alloc(int32_t nth);
  * samplers' exchange buffer holds recounted counts (lda_count_update_mode),
  * lda_recount_times, lda_set_exchange_parts' reserve_cus < 0 = default; 4 --
  * lda_hyper_statistics, lda_set_alpha_beta returns without waiting for the
- * stream (its upload is asynchronous). */
-#define LDA_ABI_VERSION 4
+ * stream (its upload is asynchronous); 5 -- warm-start parts are interleaved
+ * segments of the corpus (LDA_WARM_BLOCKS), lda_warm_part_tokens. */
+#define LDA_ABI_VERSION 5
 const char* lda_version(void);
 int32_t lda_abi_version(void);
 

@@ -63,6 +63,9 @@ public class GpuParallelTopicModel extends ParallelTopicModel {
   /** 1: the native side prints Mallet's INFO lines on stderr as well. */
   public void setNativeVerbosity(int level) { verbosity = level; }
 
+  /** Largest corpus (tokens) the flat int[] hand-over supports: Integer.MAX_VALUE - 8. */
+  public static final long MAX_TOKENS = Integer.MAX_VALUE - 8L;
+
   // --- JNI (integration/jni/lda_jni.c) -------------------------------------
   private static native int nativeEstimate(int K, int V, long[] docOff, int[] words, int[] z,
                                            double[] alpha, double[] hyper, long[] sweep,
@@ -77,6 +80,13 @@ public class GpuParallelTopicModel extends ParallelTopicModel {
       FeatureSequence fs = (FeatureSequence) data.get(d).instance.getData();
       docOff[d + 1] = docOff[d] + fs.getLength();
     }
+    // Java arrays are int-indexed: the flat token arrays hold at most
+    // MAX_TOKENS (the JVM's largest safe array length); a larger corpus
+    // needs the native ParallelTopicModel (include/lda_topic_model.h) fed in
+    // pieces, not this drop-in (INTEGRATION.md "Limits")
+    if (docOff[D] > MAX_TOKENS)
+      throw new IllegalArgumentException("corpus has " + docOff[D] + " tokens; GpuParallelTopicModel "
+          + "passes them as one Java int[] and supports at most " + MAX_TOKENS);
     final int N = (int) docOff[D];
     int[] words = new int[N];
     int[] z = new int[N];
@@ -92,6 +102,9 @@ public class GpuParallelTopicModel extends ParallelTopicModel {
     // typeTopicCounts rows as addInstances allocated them: min(K, typeTotal)
     long[] rowOff = new long[numTypes + 1];
     for (int w = 0; w < numTypes; w++) rowOff[w + 1] = rowOff[w] + typeTopicCounts[w].length;
+    if (rowOff[numTypes] > MAX_TOKENS)
+      throw new IllegalArgumentException("typeTopicCounts hold " + rowOff[numTypes] + " cells; at most "
+          + MAX_TOKENS + " fit one Java int[]");
     int[] rows = new int[(int) rowOff[numTypes]];
     double[] hyper = {alphaSum, beta, betaSum};
     long[] sweep = {gpuSweep};

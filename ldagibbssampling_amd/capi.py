@@ -112,6 +112,7 @@ SIGNATURES = {
     "lda_set_count_update": (C.c_int32, [_vp, C.c_int32, C.c_int32]),
     "lda_set_warm_start": (C.c_int32, [_vp, C.c_int32, C.c_int32, C.c_int64, C.c_int64]),
     "lda_get_warm_start": (C.c_int32, [_vp, C.POINTER(C.c_int32), C.POINTER(C.c_int32)]),
+    "lda_warm_part_tokens": (C.c_int32, [_vp, C.c_int64, C.c_int32, C.c_int64, C.c_int64, C.c_int64, _vp]),
     "lda_sweep_parts": (C.c_int32, [_vp, C.POINTER(C.c_int32), C.POINTER(C.c_int32)]),
     "lda_get_count_update": (C.c_int32, [_vp, C.POINTER(C.c_int32), C.POINTER(C.c_int32)]),
     "lda_abi_version": (C.c_int32, []),

@@ -126,6 +126,67 @@ std::vector<int64_t> make_cut_ranges(const std::vector<int64_t>& off, int64_t ta
   return r;
 }
 
+// Warm-start parts (lda_set_warm_start), seen from a shard whose documents
+// start at global token base + off[d]: the corpus [g0, g0 + gn) is cut into
+// S = parts * LDA_WARM_BLOCKS token-balanced segments (cut j = the first
+// document starting at or after g0 + gn * j / S) and segment j belongs to
+// part j % parts.  Every shard of a token-balanced sharding into up to
+// LDA_WARM_BLOCKS shards therefore holds documents of every part (round 3
+// had cut P contiguous parts, so at G = 8, P = 4 only 2 of 8 GPUs sampled in
+// each step).  runs[i] = part i's local document runs [d0, d1), in order.
+std::vector<std::vector<std::pair<int64_t, int64_t>>> warm_part_runs(const std::vector<int64_t>& off,
+                                                                     int parts, int64_t base,
+                                                                     int64_t g0, int64_t gn) {
+  const int64_t D = (int64_t)off.size() - 1;
+  const int64_t S = (int64_t)parts * LDA_WARM_BLOCKS;
+  std::vector<std::vector<std::pair<int64_t, int64_t>>> runs((size_t)parts);
+  int64_t prev = 0;
+  for (int64_t j = 0; j < S; ++j) {
+    int64_t next = D;
+    if (j + 1 < S) {
+      const int64_t tgt = g0 + gn * (j + 1) / S - base;
+      next = std::lower_bound(off.begin(), off.end(), tgt) - off.begin();
+      next = std::min(std::max(next, prev), D);
+    }
+    if (next > prev) runs[(size_t)(j % parts)].push_back({prev, next});
+    prev = next;
+  }
+  return runs;
+}
+
+// The work ranges of each part's document runs: ranges never cross a run
+// end, and the last ~1/8 of a part's tokens go in quarter-size ranges (its
+// launch tail).  Range r is documents [start[r], end[r]); part_range[i] is
+// part i's first range.
+void make_run_ranges(const std::vector<int64_t>& off, int64_t target,
+                     const std::vector<std::vector<std::pair<int64_t, int64_t>>>& runs,
+                     std::vector<int64_t>& start, std::vector<int64_t>& end,
+                     std::vector<int64_t>& part_range) {
+  start.clear();
+  end.clear();
+  part_range.assign(1, 0);
+  const int64_t tail_target = std::max<int64_t>(16, target / 4);
+  for (const auto& pr : runs) {
+    int64_t total = 0;
+    for (const auto& r : pr) total += off[r.second] - off[r.first];
+    const int64_t tail_from = total / 8 * 7;
+    int64_t seen = 0;
+    for (const auto& r : pr) {
+      int64_t s = r.first;
+      for (int64_t d = r.first; d < r.second; ++d) {
+        const int64_t tgt = seen >= tail_from ? tail_target : target;
+        if (off[d + 1] - off[s] >= tgt || d + 1 == r.second) {
+          seen += off[d + 1] - off[s];
+          start.push_back(s);
+          end.push_back(d + 1);
+          s = d + 1;
+        }
+      }
+    }
+    part_range.push_back((int64_t)start.size());
+  }
+}
+
 // A split sweep's ranges: the shard's own token-balanced cuts.  parts == 1
 // gives exactly make_ranges(off, target).
 std::vector<int64_t> make_part_ranges(const std::vector<int64_t>& off, int64_t target, int parts,
@@ -213,7 +274,8 @@ struct lda_ctx {
   // the next part samples; all through buffer 0), over their own ranges
   int warm_parts = 1;
   int32_t warm_sweeps = 0;
-  int64_t* warm_range_doc = nullptr;
+  int64_t* warm_range_doc = nullptr;   // range starts [R_warm], then the ends (warm_range_end)
+  int64_t* warm_range_end = nullptr;
   std::vector<int64_t> warm_part_range{0, 0};
   bool sweep_seq = false;          // the sweep being sampled is a warm-start sweep
   uint32_t* perm = nullptr;        // [N] token indices grouped by (part, word)
@@ -280,6 +342,9 @@ struct lda_ctx {
   int32_t* hyper_pin = nullptr;
   size_t hyper_pin_cap = 0;
   hipGraphExec_t graphs[GRAPH_MAX + 1] = {};
+  hipEvent_t graph_ev = nullptr;      // recorded after each graph launch
+  hipEvent_t switch_ev = nullptr;     // lda_set_stream: orders the new stream after the old
+  bool graph_ev_live = false;
   struct GraphKey {
     const void* range_doc = nullptr;
     int64_t R = -1;
@@ -317,6 +382,8 @@ struct lda_ctx {
     if (chist) (void)hipFree(chist);
     for (auto& g : graphs)
       if (g) (void)hipGraphExecDestroy(g);
+    if (graph_ev) (void)hipEventDestroy(graph_ev);
+    if (switch_ev) (void)hipEventDestroy(switch_ev);
     if (state_dev) (void)hipFree(state_dev);
     if (zw) (void)hipFree(zw);
     if (zpos) (void)hipFree(zpos);
@@ -337,6 +404,7 @@ struct lda_ctx {
     p.z = z;
     p.doc_off = doc_off;
     p.range_doc = range_doc;
+    p.range_end = range_doc + 1;     // contiguous ranges: range r ends where r + 1 starts
     p.num_ranges = R;
     p.queue = queue;
     p.nw = nw;
@@ -534,7 +602,10 @@ extern "C" {
 
 const char* lda_last_error(void) { return g_last_error.c_str(); }
 void lda_debug_fail_host_alloc(int32_t nth) { g_fail_alloc = nth > 0 ? nth : 0; }
-const char* lda_version(void) { return "lda_mi355x 0.3.0 (gfx950; ABI 3)"; }
+#define LDA_STR2(x) #x
+#define LDA_STR(x) LDA_STR2(x)
+// the version string carries the header's ABI number (they had drifted apart)
+const char* lda_version(void) { return "lda_mi355x 0.4.0 (gfx950; ABI " LDA_STR(LDA_ABI_VERSION) ")"; }
 int32_t lda_abi_version(void) { return LDA_ABI_VERSION; }
 int32_t lda_padded_topics(int32_t num_topics) { return pad_topics(num_topics); }
 
@@ -724,7 +795,16 @@ void lda_destroy(lda_ctx* ctx) { delete ctx; }
 lda_status lda_set_stream(lda_ctx* c, void* s) {
   return lda_abi::guarded([&]() -> lda_status {
   if (!c) return fail(LDA_ERR_INVALID_ARG, "null ctx");
-  c->stream = s ? (hipStream_t)s : c->own_stream;
+  hipStream_t ns = s ? (hipStream_t)s : c->own_stream;
+  if (ns != c->stream) {
+    // work already queued on the old stream comes first on the new one,
+    // without a host wait (the caller need not synchronize to switch)
+    HIP_TRY(hipSetDevice(c->device));
+    if (!c->switch_ev) HIP_TRY(hipEventCreateWithFlags(&c->switch_ev, hipEventDisableTiming));
+    HIP_TRY(hipEventRecord(c->switch_ev, c->stream));
+    HIP_TRY(hipStreamWaitEvent(ns, c->switch_ev, 0));
+  }
+  c->stream = ns;
   return LDA_OK;
   });
 }
@@ -817,6 +897,7 @@ static lda_status sample_part_impl(lda_ctx* c, int part) {
       HIP_TRY(hipMemsetAsync(c->queue + part, 0, sizeof(int32_t), c->stream));
     lda::SampleParams p = c->params(false);
     p.range_doc = (seq ? c->warm_range_doc : c->range_doc) + r0;
+    p.range_end = (seq ? c->warm_range_end : c->range_doc + 1) + r0;
     p.num_ranges = r1 - r0;
     p.queue = c->queue + part;
     p.delta = c->sweep_recount ? nullptr : buf;   // recount: the sampler writes z only
@@ -1050,21 +1131,43 @@ lda_status lda_set_warm_start(lda_ctx* c, int32_t parts, int32_t sweeps, int64_t
   }
   HIP_TRY(hipSetDevice(c->device));
   if (parts > 1) {
-    std::vector<int64_t> pr;
-    const std::vector<int64_t> cuts = part_cuts(c->doc_off_h, parts, c->token_base, corpus_first_token, corpus_tokens);
-    std::vector<int64_t> ranges = make_cut_ranges(c->doc_off_h, c->tokens_per_range, cuts, pr);
+    std::vector<int64_t> pr, st, en;
+    make_run_ranges(c->doc_off_h, c->tokens_per_range,
+                    warm_part_runs(c->doc_off_h, parts, c->token_base, corpus_first_token, corpus_tokens),
+                    st, en, pr);
+    // one device buffer: starts [R] then ends [R]
+    const size_t R = st.size();
+    st.insert(st.end(), en.begin(), en.end());
     int64_t* dr = nullptr;
-    HIP_TRY(dalloc(&dr, ranges.size()));
-    hipError_t e = hipMemcpyAsync(dr, ranges.data(), sizeof(int64_t) * ranges.size(), hipMemcpyHostToDevice, c->stream);
+    HIP_TRY(dalloc(&dr, st.size()));
+    hipError_t e = hipMemcpyAsync(dr, st.data(), sizeof(int64_t) * st.size(), hipMemcpyHostToDevice, c->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
     if (e != hipSuccess) (void)hipFree(dr);
     HIP_TRY(e);
     if (c->warm_range_doc) (void)hipFree(c->warm_range_doc);
     c->warm_range_doc = dr;
+    c->warm_range_end = dr + R;
     c->warm_part_range = pr;
   }
   c->warm_parts = parts;
   c->warm_sweeps = parts > 1 ? sweeps : 0;
+  return LDA_OK;
+  });
+}
+
+lda_status lda_warm_part_tokens(const int64_t* doc_off, int64_t num_docs, int32_t parts, int64_t token_base,
+                                int64_t corpus_first_token, int64_t corpus_tokens, int64_t* tokens_out) {
+  return lda_abi::guarded([&]() -> lda_status {
+  if (!doc_off || !tokens_out || num_docs < 0 || parts < 1 || parts > LDA_MAX_EXCHANGE_PARTS || corpus_tokens <= 0)
+    return fail(LDA_ERR_INVALID_ARG, "null pointer, num_docs < 0, parts outside [1, LDA_MAX_EXCHANGE_PARTS] or corpus_tokens <= 0");
+  std::vector<int64_t> off(doc_off, doc_off + num_docs + 1);
+  for (auto& o : off) o -= doc_off[0];
+  const auto runs = warm_part_runs(off, parts, token_base, corpus_first_token, corpus_tokens);
+  for (int i = 0; i < parts; ++i) {
+    int64_t n = 0;
+    for (const auto& r : runs[(size_t)i]) n += off[(size_t)r.second] - off[(size_t)r.first];
+    tokens_out[i] = n;
+  }
   return LDA_OK;
   });
 }
@@ -1134,6 +1237,10 @@ static lda_status sweep_graph(lda_ctx* c, int k, hipGraphExec_t* out) {
   key.R = c->R;
   key.stream = c->stream;
   if (!(key == c->graph_key)) {
+    // a graph launched earlier (perhaps on another stream: lda_set_stream does
+    // not synchronize) may still run; it finishes before it is destroyed
+    if (c->graph_ev_live) HIP_TRY(hipEventSynchronize(c->graph_ev));
+    c->graph_ev_live = false;
     for (auto& g : c->graphs)
       if (g) {
         (void)hipGraphExecDestroy(g);
@@ -1193,6 +1300,9 @@ lda_status lda_sweep(lda_ctx* c, int32_t n) {
       if (c->state_sweep != (int64_t)c->sweep)
         HIP_TRY(hipMemsetD32Async(word(0), (int)c->sweep, 1, c->stream));
       HIP_TRY(hipGraphLaunch(g, c->stream));
+      if (!c->graph_ev) HIP_TRY(hipEventCreateWithFlags(&c->graph_ev, hipEventDisableTiming));
+      HIP_TRY(hipEventRecord(c->graph_ev, c->stream));
+      c->graph_ev_live = true;
       c->state_sweep = (int64_t)c->sweep + k;
       c->sweep += (uint32_t)k;
       c->sweeps_since_seed += k;
@@ -1655,6 +1765,7 @@ lda_status lda_infer(lda_ctx* c, int64_t Dh, const int64_t* doc_off, const int32
   p.z = dz;
   p.doc_off = doff;
   p.range_doc = drange;
+  p.range_end = drange + 1;
   p.num_ranges = R;
   p.delta = nullptr;
   p.dsum = nullptr;

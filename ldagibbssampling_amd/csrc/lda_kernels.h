@@ -49,7 +49,8 @@ struct SampleParams {
   const int32_t* words;     // [N] token stream (doc-contiguous)
   int32_t* z;               // [N] topic of each token (read old, write new)
   const int64_t* doc_off;   // [D+1]
-  const int64_t* range_doc; // [R+1] work ranges as doc boundaries
+  const int64_t* range_doc; // [R] work range r starts at document range_doc[r]
+  const int64_t* range_end; // [R] ... and ends before range_end[r] (range_doc + 1: contiguous ranges)
   int64_t num_ranges;
   int32_t* queue;           // range counter, zeroed before each launch
   const int32_t* nw;        // [V*Kp] snapshot

@@ -376,7 +376,7 @@ void k_sample(SampleParams p) {
     r = uniform_i(first_or_queued(first_range, (int)blockIdx.x * 4 + wid, (int)gridDim.x * 4, uniform_i(__shfl(r, 0))));
     first_range = false;
     if (r >= p.num_ranges) break;
-    const int64_t d0 = p.range_doc[r], d1 = p.range_doc[r + 1];
+    const int64_t d0 = p.range_doc[r], d1 = p.range_end[r];
     const int64_t t0 = p.doc_off[d0];
     // token positions below are 32-bit offsets from the range start
     const int nt = (int)(p.doc_off[d1] - t0);
@@ -899,7 +899,7 @@ __global__ __launch_bounds__(256) void k_sample_half(SampleParams p) {
         }
         return;
       }
-      const int64_t d0 = p.range_doc[r], d1 = p.range_doc[r + 1];
+      const int64_t d0 = p.range_doc[r], d1 = p.range_end[r];
       const int64_t s = p.doc_off[d0];
       const int n = (int)(p.doc_off[d1] - s);
       if (n <= 0) continue;
@@ -1274,7 +1274,7 @@ __global__ __launch_bounds__(256) QUARTER_ATTR void k_sample_quarter(SampleParam
                 pw = 0;
                 break;
               }
-              const int64_t d0 = p.range_doc[r], d1 = p.range_doc[r + 1];
+              const int64_t d0 = p.range_doc[r], d1 = p.range_end[r];
               const int64_t s0 = p.doc_off[d0];
               const int n = (int)(p.doc_off[d1] - s0);
               if (n <= 0) continue;
@@ -1548,7 +1548,7 @@ __global__ __launch_bounds__(256) void k_sample_sparse(SampleParams p) {
     r = uniform_i(first_or_queued(first_range, (int)blockIdx.x * 4 + wid, (int)gridDim.x * 4, uniform_i(__shfl(r, 0))));
     first_range = false;
     if (r >= p.num_ranges) break;
-    const int64_t d0 = p.range_doc[r], d1 = p.range_doc[r + 1];
+    const int64_t d0 = p.range_doc[r], d1 = p.range_end[r];
     const int64_t t0 = p.doc_off[d0], t1 = p.doc_off[d1];
     if (t1 <= t0) continue;
 
@@ -2032,7 +2032,7 @@ __global__ __launch_bounds__(64 * sb_waves<C>()) void k_sample_sparse_big(Sample
     r = uniform_i(first_or_queued(first_range, (int)blockIdx.x * WB + wid, (int)gridDim.x * WB, uniform_i(__shfl(r, 0))));
     first_range = false;
     if (r >= p.num_ranges) break;
-    const int64_t d0 = p.range_doc[r], d1 = p.range_doc[r + 1];
+    const int64_t d0 = p.range_doc[r], d1 = p.range_end[r];
     const int64_t t0 = p.doc_off[d0];
     // token positions below are 32-bit offsets from the range start (64-bit
     // compares and adds cost two scalar instructions each, and the scalar

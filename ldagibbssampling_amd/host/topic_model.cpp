@@ -759,8 +759,11 @@ std::string ParallelTopicModel::displayTopWords(int32_t num_words, bool using_ne
 }
 
 // ---- checkpoint: little-endian binary, every field needed to continue the
-// run bit for bit (topics, hyperparameters, options, the statistics gathered
-// since the last optimisation, and the Philox sweep counter).
+// run bit for bit (topics, hyperparameters, options and the Philox sweep
+// counter).  The alpha statistics arrays are still written (format v2) but
+// carry nothing across: estimate() clears them at its start and end, as
+// Mallet 2.0.7's new WorkerRunnables drop theirs, so a resumed model starts
+// its statistics empty whatever the file holds.
 namespace {
 constexpr char kMagic[8] = {'L', 'D', 'A', 'T', 'M', 0, 'v', '2'};    // v2: + warm start
 constexpr char kMagicV1[8] = {'L', 'D', 'A', 'T', 'M', 0, 'v', '1'};

@@ -214,34 +214,45 @@ class ExactSampler:
 
     def set_warm_start(self, parts: int, sweeps: int, corpus_first_token: int = 0, corpus_tokens: int = 0):
         """lda_set_warm_start: sweeps whose sweep counter is below `sweeps` run in
-        `parts` sequential parts (token-balanced document cuts as
-        lda_capi.cpp's make_part_ranges), each applied before the next."""
+        `parts` sequential parts (interleaved token-balanced segments of the
+        corpus, _warm_runs), each applied before the next."""
         self._warm = (int(parts), int(sweeps) if parts > 1 else 0)
         if corpus_tokens <= 0:                      # this shard is the whole corpus
             corpus_first_token, corpus_tokens = self.token_base, self.N
         self._warm_corpus = (int(corpus_first_token), int(corpus_tokens))
 
-    def _warm_cuts(self):
-        """lda_capi.cpp part_cuts: cut i = the first document starting at or
-        after global token g0 + gn * i // P."""
+    WARM_BLOCKS = 64      # include/lda_mi355x.h LDA_WARM_BLOCKS
+
+    def _warm_runs(self):
+        """lda_capi.cpp warm_part_runs: the corpus [g0, g0 + gn) is cut into
+        S = P * WARM_BLOCKS token-balanced segments (cut j = the first
+        document starting at or after g0 + gn * j // S) and segment j belongs
+        to part j % P; returns part i's local document runs [(d0, d1), ...]."""
         P = self._warm[0]
+        S = P * self.WARM_BLOCKS
         g0, gn = self._warm_corpus
         off = self.doc_off - self.doc_off[0]
-        cuts = [0]
-        for i in range(1, P):
-            d = int(np.searchsorted(off, g0 + gn * i // P - self.token_base, side="left"))
-            cuts.append(min(max(d, cuts[-1]), self.D))
-        cuts.append(self.D)
-        return cuts
+        runs = [[] for _ in range(P)]
+        prev = 0
+        for j in range(S):
+            nxt = self.D
+            if j + 1 < S:
+                d = int(np.searchsorted(off, g0 + gn * (j + 1) // S - self.token_base, side="left"))
+                nxt = min(max(d, prev), self.D)
+            if nxt > prev:
+                runs[j % P].append((prev, nxt))
+            prev = nxt
+        return runs
 
     def sample(self, frozen=False):
         if self._pending:
             raise RuntimeError("sample with a pending delta: apply first (as lda_sample)")
         warm = getattr(self, "_warm", (1, 0))
         if not frozen and warm[0] > 1 and self.sweep_index < warm[1]:
-            cuts = self._warm_cuts()
+            runs = self._warm_runs()
             for i in range(warm[0]):
-                self.sample_docs(cuts[i], cuts[i + 1])
+                for d0, d1 in runs[i]:
+                    self.sample_docs(d0, d1)
                 if i + 1 < warm[0]:
                     self.apply()
             self.end_sweep()

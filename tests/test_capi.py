@@ -123,3 +123,51 @@ def test_bench_traffic_record_matches_its_sweep_window():
         assert src30.endswith("traffic_c5_b30.json") and rec30["burnin"] == 30
         assert rec30["bytes_per_token"] < rec["bytes_per_token"]
     assert bench.pmc_record(250_000_000, "k_sample_sparse_big<", 4096, 7) == (None, None)
+
+
+def test_version_string_carries_the_abi_number(lib):
+    """lda_version() had said "ABI 3" while the header said 4."""
+    v = lib.lda_version().decode()
+    assert v.endswith(f"; ABI {lib.lda_abi_version()})"), v
+
+
+def _warm_tokens(lib, doc_off, parts, token_base, g0, gn):
+    import numpy as np
+    off = np.ascontiguousarray(doc_off, dtype=np.int64)
+    out = np.zeros(parts, dtype=np.int64)
+    capi.check(lib.lda_warm_part_tokens(off.ctypes.data, len(off) - 1, parts, int(token_base),
+                                        int(g0), int(gn), out.ctypes.data), "lda_warm_part_tokens")
+    return out
+
+
+def test_warm_start_parts_keep_every_shard_busy(lib):
+    """the warm start's parts are interleaved segments of
+    the corpus, so at G = 8 shards and P = 4 parts every shard samples in
+    every step (round 3's contiguous parts left 6 of 8 GPUs idle per step),
+    and the product's cuts equal the oracle's (cpu_exact _warm_runs)."""
+    import numpy as np
+    from ldagibbssampling_amd.distributed import shard_corpus
+    from oracle import oracle as O
+    rng = np.random.default_rng(5)
+    lens = rng.integers(20, 400, size=40_000)
+    doc_off = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
+    words = np.zeros(int(doc_off[-1]), dtype=np.int32)
+    N = int(doc_off[-1])
+    for G, P in [(8, 4), (8, 2), (3, 4), (1, 3)]:
+        tot = np.zeros(P, dtype=np.int64)
+        for r in range(G):
+            sh = shard_corpus(doc_off, words, G, r)
+            t = _warm_tokens(lib, sh.doc_off, P, sh.token_base, 0, N)
+            assert t.sum() == len(sh.words)
+            # every shard has ~1/P of its tokens in each part
+            assert (t > 0).all() and t.min() >= 0.15 * len(sh.words), (G, P, r, t)
+            o = O.ExactSampler(4, 1, sh.doc_off, sh.words, 0.1, 0.01, 1, token_base=sh.token_base)
+            o.set_warm_start(P, 1, 0, N)
+            off = sh.doc_off - sh.doc_off[0]
+            ot = [sum(int(off[b] - off[a]) for a, b in runs) for runs in o._warm_runs()]
+            assert list(t) == ot
+            tot += t
+        # the global parts do not depend on the sharding
+        one = _warm_tokens(lib, doc_off, P, 0, 0, N)
+        np.testing.assert_array_equal(tot, one)
+        assert (abs(one - N / P) < 0.02 * N).all()

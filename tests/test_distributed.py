@@ -90,9 +90,10 @@ class WarmOracleEngine(OracleEngine):
         return (P, True) if P > 1 and self.s.sweep_index < S else (1, False)
 
     def sample_part(self, i):
-        cuts = self.s._warm_cuts()
-        self.s.sample_docs(cuts[i], cuts[i + 1])
-        if i + 1 == len(cuts) - 1:
+        runs = self.s._warm_runs()
+        for d0, d1 in runs[i]:
+            self.s.sample_docs(d0, d1)
+        if i + 1 == len(runs):
             self.s.end_sweep()
 
 

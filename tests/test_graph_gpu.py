@@ -106,3 +106,24 @@ def test_graph_sweeps_follow_sweep_counter_and_stream(monkeypatch):
         s.set_stream(None)
         s.sweep(3)
     _same(g, n)
+
+
+def test_graph_sweeps_stream_switch_without_synchronize(monkeypatch):
+    """lda_set_stream between two lda_sweep calls with graph sweeps
+    still in flight on the old stream.  The graphs captured for the old stream
+    are destroyed only after their last launch has finished, and the new
+    stream is ordered after the old one, so no caller synchronize is needed."""
+    import torch
+    c = synthetic_changelists(num_docs=500, num_types=800, seed=19)
+    K = 100
+    g = _make(c, K, 31, True, monkeypatch)
+    n = _make(c, K, 31, False, monkeypatch)
+    streams = [torch.cuda.Stream() for _ in range(3)]
+    for s in (g, n):
+        for i in range(6):
+            s.set_stream(streams[i % 3].cuda_stream)     # no synchronize in between
+            s.sweep(17)
+        s.set_stream(None)
+        s.sweep(2)
+        s.synchronize()
+    _same(g, n)

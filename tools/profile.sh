@@ -11,11 +11,12 @@ mkdir -p $P
 STEPS=${STEPS:-10}; WARMUP=${WARMUP:-3}; BURNIN=${BURNIN:-0}
 B="python3 bench.py --steps $STEPS --warmup $WARMUP --burnin $BURNIN --no-cpu-baseline ${BENCH_ARGS:-}"
 SKIP=$((WARMUP + BURNIN))
+PER_SWEEP=${PER_SWEEP:-1}   # sampler launches per sweep (--exchange-parts P: P)
 SEL='--kernel-include-regex k_sample|k_apply|k_prepare|k_count|k_build|k_recount'
 run() {  # name, rocprof args...
   local name=$1; shift
   timeout -k 10 600 rocprofv3 "$@" -d $P/$name -o $name --output-format csv -- $B > $P/$name.log 2>&1 || { echo "$name FAILED"; tail -20 $P/$name.log; return 1; }
-  python3 tools/summarize_prof.py $P/$name $P/summary_$name.json $SKIP && cp $P/$name/*kernel_stats.csv $P/ 2>/dev/null; rm -rf $P/$name
+  python3 tools/summarize_prof.py $P/$name $P/summary_$name.json $SKIP $PER_SWEEP && cp $P/$name/*kernel_stats.csv $P/ 2>/dev/null; rm -rf $P/$name
   echo "$name ok"
 }
 PASSES=${PASSES:-"kt fetch write sq lat tcc ea lds"}

@@ -1,11 +1,15 @@
 #!/usr/bin/env python3
 """Condense rocprofv3 CSV output into small per-kernel summaries.
 
-  summarize_prof.py <prof_dir> <out.json> [skip]
+  summarize_prof.py <prof_dir> <out.json> [skip_sweeps] [dispatches_per_sweep]
 
-skip: leave out each kernel's first `skip` dispatches (in dispatch order), so
-that a profile of a bench command describes the bench's own timed sweeps
-(skip = --burnin + --warmup of that command, tools/profile.sh).
+skip_sweeps: leave out each kernel's dispatches of the first `skip_sweeps`
+sweeps (in dispatch order), so that a profile of a bench command describes
+the bench's own timed sweeps (skip_sweeps = --burnin + --warmup of that
+command, tools/profile.sh).  dispatches_per_sweep (default 1): how many
+launches of a kernel one sweep makes -- the sampler launches once per part
+with --exchange-parts P (the skip had not been scaled, so split
+profiles kept near-init launches).  The summary records both.
 
 Reads every *_kernel_stats.csv, *_kernel_trace.csv and
 *_counter_collection.csv under prof_dir and writes, per kernel name:
@@ -37,9 +41,11 @@ def short(name: str) -> str:
     return name.split("(")[0][:80]
 
 
-def main(prof_dir, out_path, skip=0):
-    skip = int(skip)
-    out = {"kernels": {}, "counters": {}, "skipped_dispatches_per_kernel": skip}
+def main(prof_dir, out_path, skip=0, per_sweep=1):
+    skip_sweeps, per_sweep = int(skip), max(1, int(per_sweep))
+    skip = skip_sweeps * per_sweep
+    out = {"kernels": {}, "counters": {}, "skipped_sweeps": skip_sweeps,
+           "dispatches_per_sweep": per_sweep, "skipped_dispatches_per_kernel": skip}
     for path in glob.glob(os.path.join(prof_dir, "**", "*_kernel_trace.csv"), recursive=True):
         agg = defaultdict(list)
         with open(path) as f:
@@ -86,4 +92,4 @@ def main(prof_dir, out_path, skip=0):
 
 
 if __name__ == "__main__":
-    main(*sys.argv[1:4])
+    main(*sys.argv[1:5])
