@@ -544,7 +544,12 @@ static lda_status apply_impl(lda_ctx* c) {
     c->pending = false;
     return LDA_OK;
   }
-  HIP_TRY(lda::launch_apply(c->nw, c->delta, (int64_t)c->V * c->Kp, c->stream));
+  // the sparse samplers write no nwsum delta: k_apply_cols derives it from the
+  // (summed) nw delta's column sums.  Whatever the nwsum cells hold (the
+  // initial counts of k_count, an exchange's sum) is the same column sum, so
+  // it is dropped and recomputed
+  HIP_TRY(hipMemsetAsync(c->delta + (int64_t)c->V * c->Kp, 0, sizeof(int32_t) * c->Kp, c->stream));
+  HIP_TRY(lda::launch_apply_cols(c->nw, c->delta, c->V, c->Kp, c->delta + (int64_t)c->V * c->Kp, c->stream));
   HIP_TRY(lda::launch_prepare_topics(c->nwsum, c->delta + (int64_t)c->V * c->Kp, c->alpha_d,
                                      c->beta, (double)c->V * c->beta, c->K, c->Kp, c->alpha_f,
                                      c->inv, c->inv_m1, c->stream));
@@ -903,7 +908,8 @@ static lda_status sample_part_impl(lda_ctx* c, int part) {
     p.delta = c->sweep_recount ? nullptr : buf;   // recount: the sampler writes z only
     p.zw = c->sweep_zw ? c->zw : nullptr;
     p.zpos = c->sweep_zw ? c->zpos : nullptr;
-    p.dsum = c->sweep_recount ? nullptr : buf + (int64_t)c->V * c->Kp;
+    // the sparse samplers leave the nwsum delta to k_apply_cols
+    p.dsum = c->sweep_recount || c->sampler == LDA_SAMPLER_SPARSE ? nullptr : buf + (int64_t)c->V * c->Kp;
     const int64_t wpb = c->waves_per_block;
     // a split sweep leaves reserve_cus CUs' worth of sampler blocks free, so
     // the collective of the part before this one finds CUs to run on

@@ -151,6 +151,10 @@ hipError_t launch_count(const int32_t* words, const int32_t* z, int64_t n, int32
                         int32_t* delta, int32_t* dsum, hipStream_t st);
 hipError_t launch_apply(int32_t* nw, int32_t* delta, int64_t n, hipStream_t st);
 // dst += src; src = 0 over n int32 (n a multiple of 4): a split sweep's parts
+// sparse samplers' apply: nw += delta, delta = 0, dsum += the delta's column
+// sums (dsum must hold only what is to be added: the caller zeroes it)
+hipError_t launch_apply_cols(int32_t* nw, int32_t* delta, int64_t V, int32_t Kp, int32_t* dsum,
+                             hipStream_t st);
 hipError_t launch_fold_delta(int32_t* dst, int32_t* src, int64_t n, hipStream_t st);
 hipError_t launch_prepare_topics(int32_t* nwsum, int32_t* dsum, const double* alpha, double beta,
                                  double vbeta, int32_t K, int32_t Kp, float* alpha_f, float* inv,

@@ -2062,15 +2062,17 @@ __global__ __launch_bounds__(64 * sb_waves<C>()) void k_sample_sparse_big(Sample
     int cn = cz;
     float cu = u01(draw_u32(gbase + (uint64_t)lane, p.c2, p.c3, p.k0, p.k1));
 
-    // the chunk's count changes, lane i = token i: two delta and two nwsum
-    // atomics when its topic changed (lanes past the range hold cz == cn)
+    // the chunk's count changes, lane i = token i: two delta atomics when its
+    // topic changed (lanes past the range hold cz == cn).  No nwsum atomics:
+    // the sparse apply derives the nwsum delta from the nw delta's column sums
+    // (k_apply_cols); two more device atomics per changed token into one
+    // Kp-cell array that every wave of the chip hits had cost ~64 of the
+    // kernel's 127 written B/token
     auto flush_chunk = [&]() {
       if (!FROZEN && cn != cz) {
         const uint64_t rb = (uint64_t)(uint32_t)cw * (uint64_t)KP;
         atomicAdd(p.delta + (rb + (uint32_t)cz), -1);
         atomicAdd(p.delta + (rb + (uint32_t)cn), 1);
-        atomicAdd(p.dsum + cz, -1);
-        atomicAdd(p.dsum + cn, 1);
       }
     };
 
@@ -2604,6 +2606,42 @@ __global__ __launch_bounds__(256) void k_apply(int4* __restrict__ nw, int4* __re
       delta[i] = make_int4(0, 0, 0, 0);
     }
   }
+}
+
+// The sparse samplers' apply: nw += delta; delta = 0 over the V*Kp cells
+// (int4 groups that are zero in delta are not rewritten), and dsum += the
+// column sums of the delta -- the nwsum delta, which the sparse samplers do
+// not write (their per-token nwsum atomics all hit one Kp-cell array).  The
+// grid is a multiple of kp4 = Kp/4 threads, so thread t owns int4 column
+// group t % kp4 of every row it visits and keeps its partial sums in four
+// registers: one device atomic per nonzero partial at the end (~Kp per 256
+// blocks) instead of two per changed token.
+__global__ __launch_bounds__(256) void k_apply_cols(int4* __restrict__ nw, int4* __restrict__ delta,
+                                                    int64_t n4, int32_t* __restrict__ dsum, int32_t kp4) {
+  const int64_t gid = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t T = (int64_t)gridDim.x * 256;
+  int4 acc = make_int4(0, 0, 0, 0);
+  for (int64_t i = gid; i < n4; i += T) {
+    const int4 d = delta[i];
+    if (d.x | d.y | d.z | d.w) {
+      int4 a = nw[i];
+      a.x += d.x;
+      a.y += d.y;
+      a.z += d.z;
+      a.w += d.w;
+      nw[i] = a;
+      delta[i] = make_int4(0, 0, 0, 0);
+      acc.x += d.x;
+      acc.y += d.y;
+      acc.z += d.z;
+      acc.w += d.w;
+    }
+  }
+  int32_t* ds = dsum + (gid % kp4) * 4;
+  if (acc.x) atomicAdd(ds + 0, acc.x);
+  if (acc.y) atomicAdd(ds + 1, acc.y);
+  if (acc.z) atomicAdd(ds + 2, acc.z);
+  if (acc.w) atomicAdd(ds + 3, acc.w);
 }
 
 // Split sweep (lda_set_exchange_parts): dst += src; src = 0 over the whole
@@ -3370,6 +3408,21 @@ hipError_t launch_apply(int32_t* nw, int32_t* delta, int64_t n, hipStream_t st) 
   const int blocks = (int)std::min<int64_t>((n4 + 255) / 256, 8192);
   hipLaunchKernelGGL(k_apply, dim3(blocks), dim3(256), 0, st, reinterpret_cast<int4*>(nw),
                      reinterpret_cast<int4*>(delta), n4);
+  return hipGetLastError();
+}
+
+hipError_t launch_apply_cols(int32_t* nw, int32_t* delta, int64_t V, int32_t Kp, int32_t* dsum,
+                             hipStream_t st) {
+  const int64_t n4 = V * Kp / 4;
+  if (n4 <= 0) return hipSuccess;
+  const int kp4 = Kp / 4;                     // a power of two >= 16
+  // the grid a multiple of kp4 threads (kp4 <= 1024: a multiple of 4 blocks
+  // covers it), at most 512 blocks: ~Kp * 128 partial-sum atomics per apply
+  const int unit = std::max(1, kp4 / 256);
+  int blocks = (int)std::min<int64_t>((n4 + 255) / 256, 512);
+  blocks = std::max(unit, blocks / unit * unit);
+  hipLaunchKernelGGL(k_apply_cols, dim3(blocks), dim3(256), 0, st, reinterpret_cast<int4*>(nw),
+                     reinterpret_cast<int4*>(delta), n4, dsum, kp4);
   return hipGetLastError();
 }
 
