@@ -315,6 +315,9 @@ def main():
     ap.add_argument("--exchange-parts", type=int, default=None,
                     help="N > 1: split every sweep into P parts whose all-reduces overlap the "
                          "next part's sampling (default 1: DESIGN.md §5)")
+    ap.add_argument("--int32-exchange", action="store_true",
+                    help="N > 1: all-reduce the int32 exchange buffer instead of the compact "
+                         "packed form (A/B)")
     ap.add_argument("--reserve-cus", type=int, default=-1,
                     help="split sweeps: CUs' worth of sampler blocks left free for RCCL (-1: the library default, 1/32 of the CUs)")
     args = ap.parse_args()
@@ -408,7 +411,8 @@ def main():
         args.exchange_parts = 1
     if args.exchange_parts > 1:
         sampler.set_exchange_parts(args.exchange_parts, args.reserve_cus)
-    trainer = ADLDATrainer(sampler, sync_before_reduce=False, time_reduce=True)
+    trainer = ADLDATrainer(sampler, sync_before_reduce=False, time_reduce=True,
+                           compact=not args.int32_exchange)
     trainer.init_counts()
 
     def step():
@@ -502,15 +506,31 @@ def main():
                             "plus the token's dependency chain")
         coll = None
         if world > 1:
-            nbytes = 4 * (V * sampler.Kp + sampler.Kp)
-            coll = {"op": ("all_reduce(SUM, int32) of the nw/nwsum delta, once per sweep"
-                           if parts == 1 else
-                           f"all_reduce(SUM, int32) of the nw/nwsum delta of each of {parts} "
-                           f"sweep parts, part i's overlapping part i+1's sampling"),
+            xb = trainer.exchange_bytes()
+            nbytes = xb["allreduce_bytes"] + xb["allgather_bytes"]
+            int32_bytes = 4 * (V * sampler.Kp + sampler.Kp)
+            # modelled time of one exchange at N = 8 on one ring over xGMI links of
+            # ~153 GB/s (the per-link figure; RCCL's several rings only cut it):
+            # all-reduce 2 (W-1)/W M, all-gather (W-1)/W of the W lists
+            link = 153e9
+            model8 = (2 * 7 / 8 * xb["allreduce_bytes"] + 7 / 8 * xb["allgather_bytes"] * 8 / world) / link
+            coll = {"op": (("compact exchange (lda_exchange_pack: two cells per int32 word + escape "
+                            "lists): all_reduce(SUM, int32) of the packed words + all_gather of the "
+                            "escape lists" if trainer.compact else
+                            "all_reduce(SUM, int32) of the nw/nwsum delta")
+                           + (", once per sweep" if parts == 1 else
+                              f", for each of {parts} sweep parts, part i's overlapping part "
+                              f"i+1's sampling")),
+                    "compact": trainer.compact,
                     "exchange_parts": parts,
                     "reserve_cus": args.reserve_cus if parts > 1 else 0,
                     "bytes_per_sweep": nbytes * parts,
-                    "ring_bytes_per_rank_per_sweep": 2 * (world - 1) * nbytes * parts // world,
+                    "allreduce_bytes_per_part": xb["allreduce_bytes"],
+                    "allgather_bytes_per_part": xb["allgather_bytes"],
+                    "int32_bytes_per_sweep": int32_bytes * parts,
+                    "ring_bytes_per_rank_per_sweep": 2 * (world - 1) * xb["allreduce_bytes"] * parts // world,
+                    "modelled_n8_ms_per_sweep": model8 * parts * 1e3,
+                    "model": "one ring, 153 GB/s per xGMI link, N = 8, bytes as above",
                     # parts == 1: the whole collective; > 1: the exposed tail after
                     # the last part's sampling
                     "ms_per_sweep": trainer.reduce_ms(args.steps),

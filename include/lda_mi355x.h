@@ -173,6 +173,33 @@ lda_status lda_get_exchange_parts(lda_ctx* ctx, int32_t* parts);
 lda_status lda_sample_part(lda_ctx* ctx, int32_t part);
 lda_status lda_delta_buffer_part(lda_ctx* ctx, int32_t part, void** dev_ptr, size_t* count);
 
+/* Compact exchange.  The buffer of lda_delta_buffer_part
+ * holds int32 cells [V*Kp | Kp]; summed across `world` ranks as they are,
+ * that is 4 (V Kp + Kp) bytes per sweep (C5: 4.3 GB).  Instead a driver may
+ * exchange it packed, two cells per int32 word:
+ *   lda_exchange_sizes: packed_count int32 words [V*Kp/2 | Kp] and
+ *     escape_count int32 of one rank's escape list, for `world` ranks whose
+ *     largest shard holds max_shard_tokens tokens (the same on every rank);
+ *   lda_exchange_pack(part): packs the part's buffer on the context's stream
+ *     and returns the context-owned device arrays to exchange;
+ *   the driver: SUM all-reduce (int32) of `packed` in place, and an
+ *     all-gather of every rank's `escapes` into one device array
+ *     [world x escape_count] in rank order;
+ *   lda_exchange_unpack(part, escapes_all): the part's buffer = the unpacked
+ *     sum plus every rank's escapes (then lda_apply as usual).
+ * Cell 2i packs as d + 2^15/world (bits 0..15), cell 2i+1 as d + 2^14/world
+ * (bits 16..30): the sum over the ranks cannot carry between the halves or
+ * overflow int32.  Cells outside that range travel in the escape list
+ * (count, then (cell lo, cell hi, value) triples); each rank has at most
+ * 2 max_shard_tokens / (2^14/world) of them, since a rank's |cells| sum to
+ * at most twice its tokens.  The result is the int32 sum, bit for bit. */
+lda_status lda_exchange_sizes(lda_ctx* ctx, int32_t world, int64_t max_shard_tokens, size_t* packed_count,
+                              size_t* escape_count);
+lda_status lda_exchange_pack(lda_ctx* ctx, int32_t part, int32_t world, int64_t max_shard_tokens, void** packed,
+                             void** escapes);
+lda_status lda_exchange_unpack(lda_ctx* ctx, int32_t part, int32_t world, int64_t max_shard_tokens,
+                               const void* escapes_all);
+
 /* Warm start.  The GPU sweep samples every document against one snapshot
  * (AD-LDA), while Mallet's setNumThreads(4) workers each see their own
  * changes live: from a random start the snapshot sweep falls into a local

@@ -294,6 +294,11 @@ struct lda_ctx {
   // split sweep (lda_set_exchange_parts): part i samples the work ranges
   // [part_range[i], part_range[i+1]) into delta_part[i] (delta_part[0] == delta)
   int parts = 1, next_part = 0, reserve_cus = 0;
+  // compact exchange (lda_exchange_pack): per buffer slot, the packed words
+  // [V*Kp/2 | Kp] and the escape list [1 + 3 cap], grow-only
+  int32_t* exch_packed[LDA_MAX_EXCHANGE_PARTS] = {};
+  int32_t* exch_esc[LDA_MAX_EXCHANGE_PARTS] = {};
+  size_t exch_esc_cap[LDA_MAX_EXCHANGE_PARTS] = {};
   int32_t* delta_part[LDA_MAX_EXCHANGE_PARTS] = {};
   std::vector<int64_t> part_range{0, 0};
   double* alpha_d = nullptr;
@@ -373,6 +378,10 @@ struct lda_ctx {
       if (p) (void)hipFree(p);
     for (int i = 1; i < LDA_MAX_EXCHANGE_PARTS; ++i)
       if (delta_part[i]) (void)hipFree(delta_part[i]);
+    for (int i = 0; i < LDA_MAX_EXCHANGE_PARTS; ++i) {
+      if (exch_packed[i]) (void)hipFree(exch_packed[i]);
+      if (exch_esc[i]) (void)hipFree(exch_esc[i]);
+    }
     for (auto& sl : ll) {
       if (sl.done) (void)hipEventSynchronize(sl.done);
       if (sl.host) (void)hipHostFree(sl.host);
@@ -1031,6 +1040,89 @@ lda_status lda_delta_buffer_part(lda_ctx* c, int32_t part, void** dev_ptr, size_
   const bool seq = c->next_part != 0 || c->pending ? c->sweep_seq : next_sweep_sequential(c);
   *dev_ptr = c->delta_part[seq ? 0 : part];
   *count = (size_t)c->V * c->Kp + c->Kp;
+  return LDA_OK;
+  });
+}
+
+// ---- compact exchange
+static lda_status exchange_dims(lda_ctx* c, int32_t world, int64_t max_tokens, size_t* packed_count,
+                                size_t* escape_count, int32_t* cap) {
+  if (world < 2 || world > 16384) return fail(LDA_ERR_INVALID_ARG, "world must be in [2, 16384]");
+  if (max_tokens < c->N) return fail(LDA_ERR_INVALID_ARG, "max_shard_tokens below this shard's tokens");
+  // sum |cell| of one rank's buffer <= 2 x its tokens, so at most that over
+  // the smaller bias can escape
+  const int64_t k = 2 * max_tokens / lda::exch_bias1(world) + 1;
+  if (k > (int64_t)INT32_MAX / 3 - 1) return fail(LDA_ERR_UNSUPPORTED, "escape list beyond int32 indexing");
+  *cap = (int32_t)k;
+  *packed_count = (size_t)c->V * c->Kp / 2 + c->Kp;
+  *escape_count = 1 + 3 * (size_t)k;
+  return LDA_OK;
+}
+
+// the buffer slot a part's changes are in (a warm-start sweep: always 0)
+static int exchange_slot(lda_ctx* c, int32_t part) {
+  const bool seq = c->next_part != 0 || c->pending ? c->sweep_seq : next_sweep_sequential(c);
+  return seq ? 0 : part;
+}
+
+lda_status lda_exchange_sizes(lda_ctx* c, int32_t world, int64_t max_shard_tokens, size_t* packed_count,
+                              size_t* escape_count) {
+  return lda_abi::guarded([&]() -> lda_status {
+  if (!c || !packed_count || !escape_count) return fail(LDA_ERR_INVALID_ARG, "null argument");
+  int32_t cap = 0;
+  return exchange_dims(c, world, max_shard_tokens, packed_count, escape_count, &cap);
+  });
+}
+
+lda_status lda_exchange_pack(lda_ctx* c, int32_t part, int32_t world, int64_t max_shard_tokens, void** packed,
+                             void** escapes) {
+  return lda_abi::guarded([&]() -> lda_status {
+  if (!c || !packed || !escapes) return fail(LDA_ERR_INVALID_ARG, "null argument");
+  if (part < 0 || part >= sweep_parts(c)) return fail(LDA_ERR_INVALID_ARG, "part out of range [0, parts)");
+  size_t np = 0, ne = 0;
+  int32_t cap = 0;
+  lda_status s = exchange_dims(c, world, max_shard_tokens, &np, &ne, &cap);
+  if (s) return s;
+  const int slot = exchange_slot(c, part);
+  HIP_TRY(hipSetDevice(c->device));
+  if (!c->exch_packed[slot]) HIP_TRY(dalloc(&c->exch_packed[slot], np));
+  if (c->exch_esc_cap[slot] < ne) {
+    if (c->exch_esc[slot]) HIP_TRY(hipFree(c->exch_esc[slot]));
+    c->exch_esc[slot] = nullptr;
+    c->exch_esc_cap[slot] = 0;
+    HIP_TRY(dalloc(&c->exch_esc[slot], ne));
+    c->exch_esc_cap[slot] = ne;
+  }
+  const int64_t cells = (int64_t)c->V * c->Kp;
+  int32_t* buf = c->delta_part[slot];
+  int32_t* pk = c->exch_packed[slot];
+  int32_t* es = c->exch_esc[slot];
+  HIP_TRY(hipMemsetAsync(es, 0, sizeof(int32_t), c->stream));
+  HIP_TRY(lda::launch_exch_pack(buf, cells, pk, world, es, cap, c->stream));
+  HIP_TRY(hipMemcpyAsync(pk + cells / 2, buf + cells, sizeof(int32_t) * c->Kp, hipMemcpyDeviceToDevice, c->stream));
+  *packed = pk;
+  *escapes = es;
+  return LDA_OK;
+  });
+}
+
+lda_status lda_exchange_unpack(lda_ctx* c, int32_t part, int32_t world, int64_t max_shard_tokens,
+                               const void* escapes_all) {
+  return lda_abi::guarded([&]() -> lda_status {
+  if (!c || !escapes_all) return fail(LDA_ERR_INVALID_ARG, "null argument");
+  if (part < 0 || part >= sweep_parts(c)) return fail(LDA_ERR_INVALID_ARG, "part out of range [0, parts)");
+  size_t np = 0, ne = 0;
+  int32_t cap = 0;
+  lda_status s = exchange_dims(c, world, max_shard_tokens, &np, &ne, &cap);
+  if (s) return s;
+  const int slot = exchange_slot(c, part);
+  if (!c->exch_packed[slot]) return fail(LDA_ERR_STATE, "lda_exchange_unpack before lda_exchange_pack");
+  HIP_TRY(hipSetDevice(c->device));
+  const int64_t cells = (int64_t)c->V * c->Kp;
+  int32_t* buf = c->delta_part[slot];
+  const int32_t* pk = c->exch_packed[slot];
+  HIP_TRY(hipMemcpyAsync(buf + cells, pk + cells / 2, sizeof(int32_t) * c->Kp, hipMemcpyDeviceToDevice, c->stream));
+  HIP_TRY(lda::launch_exch_unpack(pk, cells, buf, world, static_cast<const int32_t*>(escapes_all), cap, c->stream));
   return LDA_OK;
   });
 }

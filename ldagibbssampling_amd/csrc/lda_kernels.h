@@ -155,6 +155,16 @@ hipError_t launch_apply(int32_t* nw, int32_t* delta, int64_t n, hipStream_t st);
 // sums (dsum must hold only what is to be added: the caller zeroes it)
 hipError_t launch_apply_cols(int32_t* nw, int32_t* delta, int64_t V, int32_t Kp, int32_t* dsum,
                              hipStream_t st);
+// compact exchange (lda_exchange_pack / _unpack): 2 cells per int32 word,
+// biases b0 = 2^15 / world (bits 0..15) and b1 = 2^14 / world (bits 16..30)
+inline int32_t exch_bias0(int32_t world) { return 32768 / world; }
+inline int32_t exch_bias1(int32_t world) { return 16384 / world; }
+// cells: a multiple of 4; packed: cells / 2 words; esc: [1 + 3 cap] with esc[0] zeroed
+hipError_t launch_exch_pack(const int32_t* buf, int64_t cells, int32_t* packed, int32_t world,
+                            int32_t* esc, int32_t cap, hipStream_t st);
+// buf[cells] = the unpacked sum, then + every rank's escapes (esc_all: world x [1 + 3 cap])
+hipError_t launch_exch_unpack(const int32_t* packed, int64_t cells, int32_t* buf, int32_t world,
+                              const int32_t* esc_all, int32_t cap, hipStream_t st);
 hipError_t launch_fold_delta(int32_t* dst, int32_t* src, int64_t n, hipStream_t st);
 hipError_t launch_prepare_topics(int32_t* nwsum, int32_t* dsum, const double* alpha, double beta,
                                  double vbeta, int32_t K, int32_t Kp, float* alpha_f, float* inv,

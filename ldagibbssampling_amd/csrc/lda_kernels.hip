@@ -2644,6 +2644,67 @@ __global__ __launch_bounds__(256) void k_apply_cols(int4* __restrict__ nw, int4*
   if (acc.w) atomicAdd(ds + 3, acc.w);
 }
 
+// ---- compact exchange (lda_exchange_pack / lda_exchange_unpack)
+// Two exchange cells per int32 word, biased so that the SUM over `world`
+// ranks cannot carry between the halves: cell 2i as d + b0 in bits 0..15
+// (b0 = 2^15 / world, so the sum stays below 2^16), cell 2i+1 as d + b1 in
+// bits 16..30 (b1 = 2^14 / world: the word's sum stays below 2^31, no int32
+// overflow in the collective).  A cell outside [-b, b) packs as b (a zero
+// change) and goes to the escape list {count, (cell lo, cell hi, value)...}
+// instead; every rank's list is all-gathered and added after the unpack.
+// Sum |d| over a shard's cells is at most 2 x its tokens (each changed token
+// is -1 and +1; a recount buffer holds counts summing to the tokens), so at
+// most 2 N / b1 cells can escape: the caller's capacity (lda_exchange_sizes).
+__device__ __forceinline__ uint32_t exch_field(int32_t d, int32_t b, int64_t cell, int32_t* __restrict__ esc,
+                                               int32_t cap) {
+  if (d >= -b && d < b) return (uint32_t)(d + b);
+  const int pos = atomicAdd(esc, 1);
+  if (pos < cap) {
+    int32_t* e = esc + 1 + 3 * (int64_t)pos;
+    e[0] = (int32_t)(uint32_t)cell;
+    e[1] = (int32_t)(cell >> 32);
+    e[2] = d;
+  }
+  return (uint32_t)b;
+}
+
+__global__ __launch_bounds__(256) void k_exch_pack(const int4* __restrict__ buf, int64_t n4,
+                                                   uint2* __restrict__ packed, int32_t b0, int32_t b1,
+                                                   int32_t* __restrict__ esc, int32_t cap) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += (int64_t)gridDim.x * 256) {
+    const int4 d = buf[i];
+    const int64_t c = 4 * i;
+    const uint32_t w0 = exch_field(d.x, b0, c, esc, cap) | (exch_field(d.y, b1, c + 1, esc, cap) << 16);
+    const uint32_t w1 = exch_field(d.z, b0, c + 2, esc, cap) | (exch_field(d.w, b1, c + 3, esc, cap) << 16);
+    packed[i] = make_uint2(w0, w1);
+  }
+}
+
+// the summed words back into int32 cells (every cell written: the buffer
+// held this rank's own changes before the exchange)
+__global__ __launch_bounds__(256) void k_exch_unpack(const uint2* __restrict__ packed, int64_t n4,
+                                                     int4* __restrict__ buf, int32_t wb0, int32_t wb1) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += (int64_t)gridDim.x * 256) {
+    const uint2 p = packed[i];
+    buf[i] = make_int4((int32_t)(p.x & 0xFFFFu) - wb0, (int32_t)(p.x >> 16) - wb1,
+                       (int32_t)(p.y & 0xFFFFu) - wb0, (int32_t)(p.y >> 16) - wb1);
+  }
+}
+
+// every rank's escapes (the all-gathered lists, `world` x (1 + 3 cap) int32)
+// added into the cells; blocks [4r, 4r + 4) take rank r's list
+__global__ __launch_bounds__(256) void k_exch_escapes(const int32_t* __restrict__ esc_all, int32_t cap,
+                                                      int32_t* __restrict__ buf) {
+  const int r = blockIdx.x >> 2;
+  const int32_t* e = esc_all + (int64_t)r * (1 + 3 * (int64_t)cap);
+  const int n = min(e[0], cap);
+  for (int j = (blockIdx.x & 3) * 256 + threadIdx.x; j < n; j += 1024) {
+    const int32_t* x = e + 1 + 3 * (int64_t)j;
+    const int64_t cell = (int64_t)(uint32_t)x[0] | ((int64_t)x[1] << 32);
+    atomicAdd(buf + cell, x[2]);
+  }
+}
+
 // Split sweep (lda_set_exchange_parts): dst += src; src = 0 over the whole
 // [V*Kp | Kp] delta region (a multiple of 4 int32: Kp is a multiple of 64).
 // int4 groups that are zero in src are neither written nor re-zeroed.
@@ -3423,6 +3484,30 @@ hipError_t launch_apply_cols(int32_t* nw, int32_t* delta, int64_t V, int32_t Kp,
   blocks = std::max(unit, blocks / unit * unit);
   hipLaunchKernelGGL(k_apply_cols, dim3(blocks), dim3(256), 0, st, reinterpret_cast<int4*>(nw),
                      reinterpret_cast<int4*>(delta), n4, dsum, kp4);
+  return hipGetLastError();
+}
+
+hipError_t launch_exch_pack(const int32_t* buf, int64_t cells, int32_t* packed, int32_t world,
+                            int32_t* esc, int32_t cap, hipStream_t st) {
+  const int64_t n4 = cells / 4;
+  if (n4 <= 0) return hipSuccess;
+  const int blocks = (int)std::min<int64_t>((n4 + 255) / 256, 8192);
+  hipLaunchKernelGGL(k_exch_pack, dim3(blocks), dim3(256), 0, st, reinterpret_cast<const int4*>(buf), n4,
+                     reinterpret_cast<uint2*>(packed), exch_bias0(world), exch_bias1(world), esc, cap);
+  return hipGetLastError();
+}
+
+hipError_t launch_exch_unpack(const int32_t* packed, int64_t cells, int32_t* buf, int32_t world,
+                              const int32_t* esc_all, int32_t cap, hipStream_t st) {
+  const int64_t n4 = cells / 4;
+  if (n4 > 0) {
+    const int blocks = (int)std::min<int64_t>((n4 + 255) / 256, 8192);
+    hipLaunchKernelGGL(k_exch_unpack, dim3(blocks), dim3(256), 0, st, reinterpret_cast<const uint2*>(packed),
+                       n4, reinterpret_cast<int4*>(buf), world * exch_bias0(world), world * exch_bias1(world));
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+  }
+  hipLaunchKernelGGL(k_exch_escapes, dim3(4 * world), dim3(256), 0, st, esc_all, cap, buf);
   return hipGetLastError();
 }
 

@@ -23,6 +23,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <climits>
 #include <cstdio>
 #include <cstring>
@@ -118,6 +119,15 @@ class ShardGroup {
   std::vector<hipEvent_t> events;
   std::vector<hipEvent_t> sum_events;     // local_sum: per shard "sampled" / shard 0 "summed"
   int parts = 1;
+  // RCCL exchange in the compact form (lda_exchange_pack): the largest
+  // shard's tokens (sizes the escape lists), the packed words and escape
+  // list of every shard per part, and per shard and part the gathered lists
+  // of all shards [G x escape_count]
+  int64_t max_tokens = 0;
+  bool compact = true;
+  size_t packed_count = 0, escape_count = 0;
+  std::vector<std::vector<void*>> packed, escapes;        // [part][shard]
+  std::vector<std::vector<int32_t*>> escapes_all;         // [part][shard], device buffers
 
   ~ShardGroup() {
     for (auto c : comms) ncclCommDestroy(c);
@@ -130,6 +140,12 @@ class ShardGroup {
       (void)hipSetDevice(dev[g]);
       (void)hipEventDestroy(sum_events[g]);
     }
+    for (auto& v : escapes_all)
+      for (size_t g = 0; g < v.size(); ++g)
+        if (v[g]) {
+          (void)hipSetDevice(dev[g]);
+          (void)hipFree(v[g]);
+        }
     for (auto c : ctx) lda_destroy(c);
   }
 
@@ -187,8 +203,45 @@ class ShardGroup {
     return static_cast<hipStream_t>(s);
   }
 
-  // one grouped SUM all-reduce of part `part`'s delta buffers, each on
-  // streams[g] (the shard's own stream, or its collective stream)
+  bool use_compact() const { return compact && !local_sum && ctx.size() > 1; }
+
+  // the compact exchange's first step, on every shard's own stream: part
+  // `part`'s buffer packed (lda_exchange_pack)
+  void pack_part(int part) {
+    if (!use_compact()) return;
+    const size_t G = ctx.size();
+    if (packed.size() <= (size_t)part) {
+      packed.resize((size_t)part + 1, std::vector<void*>(G));
+      escapes.resize((size_t)part + 1, std::vector<void*>(G));
+      escapes_all.resize((size_t)part + 1, std::vector<int32_t*>(G, nullptr));
+    }
+    check(lda_exchange_sizes(ctx[0], (int32_t)G, max_tokens, &packed_count, &escape_count), "lda_exchange_sizes");
+    for (size_t g = 0; g < G; ++g) {
+      check(lda_exchange_pack(ctx[g], part, (int32_t)G, max_tokens, &packed[(size_t)part][g],
+                              &escapes[(size_t)part][g]),
+            "lda_exchange_pack");
+      if (!escapes_all[(size_t)part][g]) {
+        hip_check(hipSetDevice(dev[g]), "hipSetDevice");
+        hip_check(hipMalloc(reinterpret_cast<void**>(&escapes_all[(size_t)part][g]),
+                            sizeof(int32_t) * escape_count * G),
+                  "hipMalloc");
+      }
+    }
+  }
+
+  // ... and its last, on every shard's own stream: the part's buffer = the sum
+  void unpack_part(int part) {
+    if (!use_compact()) return;
+    for (size_t g = 0; g < ctx.size(); ++g)
+      check(lda_exchange_unpack(ctx[g], part, (int32_t)ctx.size(), max_tokens, escapes_all[(size_t)part][g]),
+            "lda_exchange_unpack");
+  }
+
+  // the sum of part `part`'s buffers across the shards, each shard's on
+  // streams[g] (its own stream, or its collective stream): compact, one
+  // grouped SUM all-reduce of the packed words and an all-gather of the
+  // escape lists (pack_part before, unpack_part after); or the int32
+  // buffers themselves (all-reduce / the device-side sum)
   void reduce_part(int part, const std::vector<hipStream_t>& streams) {
     std::vector<void*> ptr(ctx.size());
     size_t count = 0;
@@ -198,19 +251,32 @@ class ShardGroup {
       local_reduce(ptr, count, streams);
       return;
     }
+    const bool cmp = use_compact();
     ncclResult_t r = ncclGroupStart();
-    for (size_t g = 0; g < ctx.size() && r == ncclSuccess; ++g)
-      r = ncclAllReduce(ptr[g], ptr[g], count, ncclInt32, ncclSum, comms[g], streams[g]);
+    for (size_t g = 0; g < ctx.size() && r == ncclSuccess; ++g) {
+      if (cmp) {
+        void* pk = packed[(size_t)part][g];
+        r = ncclAllReduce(pk, pk, packed_count, ncclInt32, ncclSum, comms[g], streams[g]);
+        if (r == ncclSuccess)
+          r = ncclAllGather(escapes[(size_t)part][g], escapes_all[(size_t)part][g], escape_count, ncclInt32,
+                            comms[g], streams[g]);
+      } else {
+        r = ncclAllReduce(ptr[g], ptr[g], count, ncclInt32, ncclSum, comms[g], streams[g]);
+      }
+    }
     const ncclResult_t r2 = ncclGroupEnd();
     if (r != ncclSuccess || r2 != ncclSuccess)
-      raise(LDA_ERR_DEVICE, std::string("ncclAllReduce: ") + ncclGetErrorString(r != ncclSuccess ? r : r2));
+      raise(LDA_ERR_DEVICE, std::string(cmp ? "ncclAllReduce / ncclAllGather: " : "ncclAllReduce: ") +
+                                ncclGetErrorString(r != ncclSuccess ? r : r2));
   }
 
   void reduce() {
     if (ctx.size() < 2) return;
     std::vector<hipStream_t> st(ctx.size());
     for (size_t g = 0; g < ctx.size(); ++g) st[g] = stream(g);
+    pack_part(0);
     reduce_part(0, st);
+    unpack_part(0);
   }
 
   void set_parts(int p) {
@@ -254,8 +320,9 @@ class ShardGroup {
       if (e != hipSuccess) raise(LDA_ERR_DEVICE, std::string(what) + ": " + hipGetErrorString(e));
     };
     for (int i = 0; i < parts; ++i) {
+      for (size_t g = 0; g < ctx.size(); ++g) check(lda_sample_part(ctx[g], i), "lda_sample_part");
+      pack_part(i);                       // on the shards' streams, before the event
       for (size_t g = 0; g < ctx.size(); ++g) {
-        check(lda_sample_part(ctx[g], i), "lda_sample_part");
         hip(hipSetDevice(dev[g]), "hipSetDevice");
         hip(hipEventRecord(events[g], st[g]), "hipEventRecord");           // part i sampled
         hip(hipStreamWaitEvent(comm_streams[g], events[g], 0), "hipStreamWaitEvent");
@@ -267,6 +334,7 @@ class ShardGroup {
       hip(hipEventRecord(events[g], comm_streams[g]), "hipEventRecord");   // every sum landed
       hip(hipStreamWaitEvent(st[g], events[g], 0), "hipStreamWaitEvent");
     }
+    for (int i = 0; i < parts; ++i) unpack_part(i);
     apply();
   }
   void apply() {
@@ -472,6 +540,12 @@ void ParallelTopicModel::ensureShards() {
     }
   }
   sg->init_exchange();
+  for (int g = 0; g < G; ++g)
+    sg->max_tokens = std::max(sg->max_tokens, doc_off_[sg->doc_begin[(size_t)g + 1]] - doc_off_[sg->doc_begin[(size_t)g]]);
+  {
+    const char* e = std::getenv("LDA_EXCHANGE_INT32");
+    sg->compact = compact_exchange_ && !(e && e[0] == '1');
+  }
   if (G > 1) {
     // shards recount (or keep a delta) in the same sweeps: the smallest
     // AUTO recount count of any shard on all of them

@@ -129,6 +129,9 @@ class ParallelTopicModel {
   bool symmetric_alpha_ = false, print_log_likelihood_ = true;
   uint64_t seed_ = 0;
   int32_t num_threads_ = 1, sampler_ = LDA_SAMPLER_DENSE, verbosity_ = 0, exchange_parts_ = 1;
+  // shards on distinct GPUs exchange packed words (lda_exchange_pack);
+  // LDA_EXCHANGE_INT32=1 in the environment sends the int32 buffers (A/B)
+  bool compact_exchange_ = true;
   int32_t warm_parts_ = 4, warm_sweeps_ = 50;
 
   std::vector<int32_t> devices_;  // setDevices (empty: plan_shards)

@@ -119,6 +119,35 @@ class GibbsSampler:
         assert t.data_ptr() == ptr and t.dtype == torch.int32
         return t
 
+    # ------------------------------------------------ compact exchange (§5)
+    def exchange_sizes(self, world: int, max_tokens: int):
+        """(packed int32 words, escape-list int32 words) of lda_exchange_pack."""
+        a, b = C.c_size_t(), C.c_size_t()
+        capi.check(self._L.lda_exchange_sizes(self._h, int(world), int(max_tokens), C.byref(a),
+                                              C.byref(b)), "lda_exchange_sizes")
+        return int(a.value), int(b.value)
+
+    def exchange_pack(self, part: int, world: int, max_tokens: int):
+        """Pack part `part`'s exchange buffer (lda_exchange_pack, on this
+        context's stream): zero-copy torch int32 views (packed words to
+        SUM-all-reduce, this rank's escape list to all-gather)."""
+        import torch
+        pk, es = C.c_void_p(), C.c_void_p()
+        capi.check(self._L.lda_exchange_pack(self._h, int(part), int(world), int(max_tokens),
+                                             C.byref(pk), C.byref(es)), "lda_exchange_pack")
+        n_pk, n_es = self.exchange_sizes(world, max_tokens)
+        dev = f"cuda:{self.device}"
+        return (torch.as_tensor(_DeviceArray(int(pk.value), n_pk), device=dev),
+                torch.as_tensor(_DeviceArray(int(es.value), n_es), device=dev))
+
+    def exchange_unpack(self, part: int, world: int, max_tokens: int, escapes_all):
+        """lda_exchange_unpack: the part's buffer = the summed packed words +
+        every rank's escapes (escapes_all: device int32 [world x escape len])."""
+        assert escapes_all.dtype.itemsize == 4 and escapes_all.is_contiguous()
+        capi.check(self._L.lda_exchange_unpack(self._h, int(part), int(world), int(max_tokens),
+                                               C.c_void_p(escapes_all.data_ptr())),
+                   "lda_exchange_unpack")
+
     # ------------------------------------------------- split sweep (§5)
     def set_exchange_parts(self, parts: int, reserve_cus: int = 0):
         """Cut each sweep into `parts` token-balanced parts with their own delta

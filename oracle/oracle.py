@@ -399,3 +399,64 @@ def doc_completion_loglik(K, V, nw, nwsum, beta, theta, doc_off, words) -> float
     words = np.ascontiguousarray(words, dtype=np.int32)
     return float(lib().orc_doc_completion_loglik(K, V, nw, nwsum, float(beta), len(doc_off) - 1,
                                                  theta, doc_off, words))
+
+
+# ------------------------------------------------ compact exchange (checker)
+def exchange_biases(world: int):
+    """lda_kernels.h exch_bias0 / exch_bias1."""
+    return 32768 // world, 16384 // world
+
+
+def exchange_cap(world: int, max_tokens: int) -> int:
+    """lda_capi.cpp exchange_dims: escapes per rank <= 2 N / b1 (+1)."""
+    return 2 * int(max_tokens) // exchange_biases(world)[1] + 1
+
+
+def exchange_pack(buf, world: int, Kp: int, max_tokens: int):
+    """Numpy restatement of lda_exchange_pack (k_exch_pack): buf int32
+    [cells | Kp] -> (packed int32 [cells/2 | Kp], escapes int32 [1 + 3 cap]).
+    Escapes are listed in cell order here (the GPU's order is scheduling-
+    dependent; the sum they produce is not)."""
+    b0, b1 = exchange_biases(world)
+    cap = exchange_cap(world, max_tokens)
+    buf = np.asarray(buf, dtype=np.int64)
+    cells = buf.size - Kp
+    d = buf[:cells].reshape(-1, 2)
+    lo, hi = d[:, 0], d[:, 1]
+    esc_lo = (lo < -b0) | (lo >= b0)
+    esc_hi = (hi < -b1) | (hi >= b1)
+    f0 = np.where(esc_lo, b0, lo + b0)
+    f1 = np.where(esc_hi, b1, hi + b1)
+    packed = np.empty(cells // 2 + Kp, dtype=np.int64)
+    packed[:cells // 2] = f0 + (f1 << 16)
+    packed[cells // 2:] = buf[cells:]
+    idx = np.flatnonzero(np.stack([esc_lo, esc_hi], axis=1).reshape(-1))
+    assert len(idx) <= cap, "escape bound violated"
+    esc = np.zeros(1 + 3 * cap, dtype=np.int64)
+    esc[0] = len(idx)
+    e = esc[1:1 + 3 * len(idx)].reshape(-1, 3)
+    e[:, 0] = idx & 0xFFFFFFFF
+    e[:, 1] = idx >> 32
+    e[:, 2] = buf[idx]
+    return packed.astype(np.int32), esc.astype(np.int32)
+
+
+def exchange_unpack(packed_sum, escapes_all, world: int, Kp: int, max_tokens: int):
+    """lda_exchange_unpack: the summed packed words (int32 [cells/2 | Kp]) and
+    every rank's escape list (world x [1 + 3 cap], rank order) -> the int32
+    sum of the ranks' buffers [cells | Kp]."""
+    b0, b1 = exchange_biases(world)
+    cap = exchange_cap(world, max_tokens)
+    p = np.asarray(packed_sum, dtype=np.int64) & 0xFFFFFFFF
+    half = p.size - Kp
+    out = np.empty(2 * half + Kp, dtype=np.int64)
+    out[0:2 * half:2] = (p[:half] & 0xFFFF) - world * b0
+    out[1:2 * half:2] = (p[:half] >> 16) - world * b1
+    out[2 * half:] = np.asarray(packed_sum[half:], dtype=np.int64)
+    ea = np.asarray(escapes_all, dtype=np.int64).reshape(world, 1 + 3 * cap)
+    for r in range(world):
+        n = min(int(ea[r, 0]), cap)
+        e = ea[r, 1:1 + 3 * n].reshape(-1, 3)
+        cell = (e[:, 0] & 0xFFFFFFFF) | (e[:, 1] << 32)
+        np.add.at(out, cell, e[:, 2])
+    return out.astype(np.int32)

@@ -37,6 +37,30 @@ class OracleEngine:
     def log_likelihood_parts(self):
         return self.s.log_likelihood_parts()
 
+    # the compact exchange (lda_exchange_pack / _unpack) restated in numpy
+    @property
+    def N(self):
+        return self.s.N
+
+    def _buf(self, part):
+        return self.s.delta()
+
+    def exchange_sizes(self, world, max_tokens):
+        from oracle import oracle as O
+        return self.s.V * self.s.Kp // 2 + self.s.Kp, 1 + 3 * O.exchange_cap(world, max_tokens)
+
+    def exchange_pack(self, part, world, max_tokens):
+        from oracle import oracle as O
+        pk, es = O.exchange_pack(self._buf(part), world, self.s.Kp, max_tokens)
+        self._packed = getattr(self, "_packed", {})
+        self._packed[part] = torch.from_numpy(pk)
+        return self._packed[part], torch.from_numpy(es)
+
+    def exchange_unpack(self, part, world, max_tokens, escapes_all):
+        from oracle import oracle as O
+        self._buf(part)[:] = O.exchange_unpack(self._packed[part].numpy(), escapes_all.numpy(), world,
+                                               self.s.Kp, max_tokens)
+
 
 class SplitOracleEngine(OracleEngine):
     """cpu_exact behind the split-sweep engine interface (lda_sample_part /
@@ -80,6 +104,9 @@ class SplitOracleEngine(OracleEngine):
     def delta_tensor(self, part=0):
         return torch.from_numpy(self.bufs[part])
 
+    def _buf(self, part):
+        return self.bufs[part]
+
 
 class WarmOracleEngine(OracleEngine):
     """cpu_exact with the warm start (lda_set_warm_start): the sampler ABI's
@@ -106,7 +133,7 @@ def _corpus():
 WARM = (3, 2)          # sweeps 0 and 1 in 3 sequential parts
 
 
-def _worker(rank, world, port, outdir, parts=1):
+def _worker(rank, world, port, outdir, parts=1, compact=True):
     sys.path.insert(0, ROOT)
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -117,10 +144,12 @@ def _worker(rank, world, port, outdir, parts=1):
     o = O.ExactSampler(K, c.num_types, sh.doc_off, sh.words, 0.1, 0.01, SEED, token_base=sh.token_base)
     if parts == "warm":
         o.set_warm_start(*WARM, 0, c.num_tokens)        # parts cut in the whole corpus
-        tr = ADLDATrainer(WarmOracleEngine(o))
+        tr = ADLDATrainer(WarmOracleEngine(o), compact=compact)
     else:
-        tr = ADLDATrainer(OracleEngine(o) if parts == 1 else SplitOracleEngine(o, parts))
+        tr = ADLDATrainer(OracleEngine(o) if parts == 1 else SplitOracleEngine(o, parts),
+                          compact=compact)
         assert tr.parts == parts
+    assert tr.compact == compact
     tr.sweep(SWEEPS)
     ll = tr.log_likelihood()
     nw, nwsum, _, _ = o.counts()
@@ -139,14 +168,18 @@ def _free_port():
     return p
 
 
-@pytest.mark.parametrize("world,parts", [(2, 1), (3, 1), (2, 3), (3, 2), (2, "warm"), (3, "warm")])
-def test_gloo_adlda_matches_single(oracle, world, parts):
+@pytest.mark.parametrize("world,parts,compact", [(2, 1, True), (3, 1, True), (2, 3, True), (3, 2, True),
+                                                 (2, "warm", True), (3, "warm", True), (2, 1, False),
+                                                 (3, 2, False)])
+def test_gloo_adlda_matches_single(oracle, world, parts, compact):
     """parts > 1: split sweeps, every part's all-reduce overlapping the next
     part's sampling (async gloo collectives) -- the same result bit for bit.
     "warm": the warm start (sequential parts cut in the whole corpus, each
-    part summed and applied before the next) against one context's."""
+    part summed and applied before the next) against one context's.
+    compact: the packed exchange (two cells per int32 word + escape lists);
+    False: the int32 buffers."""
     with tempfile.TemporaryDirectory() as d:
-        mp.start_processes(_worker, args=(world, _free_port(), d, parts), nprocs=world,
+        mp.start_processes(_worker, args=(world, _free_port(), d, parts, compact), nprocs=world,
                            start_method="spawn")
         res = [np.load(os.path.join(d, f"r{r}.npz")) for r in range(world)]
     c = _corpus()
@@ -175,3 +208,38 @@ def test_shard_balanced_by_tokens():
     assert sum(toks) == c.num_tokens
     assert max(toks) - min(toks) <= 200                    # within ~one doc
     assert [s.token_base for s in shards] == list(np.cumsum([0] + toks[:-1]))
+
+
+@pytest.mark.parametrize("world", [2, 3, 8, 16])
+def test_compact_exchange_roundtrip_with_escapes(world):
+    """The packed exchange restated in numpy (oracle.exchange_pack / _unpack,
+    the checker of lda_exchange_pack): summing `world` ranks' packed words
+    plus their escape lists gives the int32 sum, bit for bit, with cells at
+    and beyond the biases (escapes), at both halves of a word, negative and
+    positive, and the nwsum tail; each rank's escapes stay within the bound
+    2 N / b1 when its |cells| sum to at most 2 N."""
+    from oracle import oracle as O
+    rng = np.random.default_rng(world)
+    Kp, V = 64, 40
+    cells = V * Kp
+    b0, b1 = O.exchange_biases(world)
+    bufs = []
+    for r in range(world):
+        b = np.zeros(cells + Kp, dtype=np.int64)
+        idx = rng.choice(cells, size=300, replace=False)
+        b[idx] = rng.integers(-3, 4, size=300)
+        # boundary and escape values in both halves
+        for v in (b0 - 1, -b0, b0, -b0 - 1, b1 - 1, -b1, b1, -b1 - 1, 3 * b0):
+            b[rng.integers(cells)] = v
+        b[cells:] = rng.integers(-50, 50, size=Kp)
+        bufs.append(b.astype(np.int32))
+    # the escape bound's premise: a rank's |cells| sum to at most 2 N (N: the
+    # largest shard's tokens)
+    N = max(int(np.abs(b[:cells].astype(np.int64)).sum()) for b in bufs) // 2 + 1
+    packed, escs = zip(*(O.exchange_pack(b, world, Kp, N) for b in bufs))
+    psum = np.sum(np.stack([p.astype(np.int64) for p in packed]), axis=0)
+    assert psum.max() < 2 ** 31                 # no int32 overflow in the collective
+    out = O.exchange_unpack(psum.astype(np.int32), np.concatenate(escs), world, Kp, N)
+    np.testing.assert_array_equal(out, np.sum(np.stack(bufs).astype(np.int64), axis=0).astype(np.int32))
+    assert all(int(e[0]) <= O.exchange_cap(world, N) for e in escs)
+    assert sum(int(e[0]) for e in escs) >= 1

@@ -82,3 +82,66 @@ def test_split_sweep_ordering_rules(oracle):
     o = oracle.ExactSampler(64, c.num_types, c.doc_off, c.words, 0.1, 0.01, 3)
     o.sweep(1)
     np.testing.assert_array_equal(g.z(), o.z())
+
+
+@pytest.mark.parametrize("world,kind,K", [(2, "dense", 4), (4, "dense", 20), (8, "dense", 4),
+                                          (3, "sparse", 1500), (8, "sparse", 4096)])
+def test_compact_exchange_bit_exact(oracle, world, kind, K):
+    """lda_exchange_pack / lda_exchange_unpack on `world`
+    shards held in one process on one GPU: the packed words summed across the
+    shards (torch, in place of RCCL) plus every shard's all-gathered escape
+    list unpack to the int32 sum of the shards' buffers, bit for bit, on
+    every shard.  The buffers are the shards' initial counts (what the first
+    exchange sums): a hot word (half the tokens) puts counts far beyond the
+    biases 2^15/world and 2^14/world, so escapes occur in both word halves.
+    The packed words and escape lists match the numpy restatement
+    (oracle.exchange_pack) up to the escapes' order, which the GPU's atomic
+    appends leave open."""
+    import torch
+    from ldagibbssampling_amd.distributed import shard_corpus
+    from ldagibbssampling_amd.sampler import GibbsSampler
+    rng = np.random.default_rng(world * 7 + K)
+    D, L = 600, 150
+    words = rng.integers(1, 500, size=D * L).astype(np.int32)
+    words[rng.random(D * L) < 0.5] = 0                        # the hot word
+    doc_off = np.arange(D + 1, dtype=np.int64) * L
+    shards = [shard_corpus(doc_off, words, world, r) for r in range(world)]
+    gs = [GibbsSampler(K, 500, sh.doc_off, sh.words, np.full(K, 0.1), 0.01, seed=5,
+                       token_base=sh.token_base, sampler=kind) for sh in shards]
+    N = max(g.N for g in gs)
+    before = [g.delta_tensor().clone() for g in gs]
+    want = torch.stack([b.to(torch.int64) for b in before]).sum(0).to(torch.int32)
+    packs = [g.exchange_pack(0, world, N) for g in gs]
+    torch.cuda.synchronize()
+    n_esc = [int(e[0]) for _, e in packs]
+    assert sum(n_esc) > 0
+    Kp = gs[0].Kp
+    for (pk, es), b in zip(packs, before):
+        opk, oes = oracle.exchange_pack(b.cpu().numpy(), world, Kp, N)
+        np.testing.assert_array_equal(pk.cpu().numpy(), opk)
+        n = int(oes[0])
+        assert int(es[0]) == n
+        got = es[1:1 + 3 * n].cpu().numpy().reshape(-1, 3)
+        ref = oes[1:1 + 3 * n].reshape(-1, 3)
+        np.testing.assert_array_equal(got[np.lexsort(got.T[::-1])], ref[np.lexsort(ref.T[::-1])])
+    total = torch.stack([pk.to(torch.int64) for pk, _ in packs]).sum(0)
+    assert int(total.max()) < 2 ** 31
+    esc_all = torch.cat([es for _, es in packs])
+    for g, (pk, _) in zip(gs, packs):
+        pk.copy_(total.to(torch.int32))
+        g.exchange_unpack(0, world, N, esc_all)
+    torch.cuda.synchronize()
+    for g in gs:
+        assert torch.equal(g.delta_tensor(), want)
+    # and the shards then agree with one context over the whole corpus
+    for g in gs:
+        g.apply()
+    one = GibbsSampler(K, 500, doc_off, words, np.full(K, 0.1), 0.01, seed=5, sampler=kind)
+    one.sweep(0)
+    nw1, ns1, _, _ = one.counts()
+    for g in gs:
+        nw, ns, _, _ = g.counts()
+        np.testing.assert_array_equal(nw, nw1)
+        np.testing.assert_array_equal(ns, ns1)
+        g.close()
+    one.close()
