@@ -917,8 +917,9 @@ static lda_status sample_part_impl(lda_ctx* c, int part) {
     p.delta = c->sweep_recount ? nullptr : buf;   // recount: the sampler writes z only
     p.zw = c->sweep_zw ? c->zw : nullptr;
     p.zpos = c->sweep_zw ? c->zpos : nullptr;
-    // the sparse samplers leave the nwsum delta to k_apply_cols
-    p.dsum = c->sweep_recount || c->sampler == LDA_SAMPLER_SPARSE ? nullptr : buf + (int64_t)c->V * c->Kp;
+    // (the sparse apply recomputes the nwsum delta from the nw delta
+    // (k_apply_cols) and drops what a sampler put there)
+    p.dsum = c->sweep_recount ? nullptr : buf + (int64_t)c->V * c->Kp;
     const int64_t wpb = c->waves_per_block;
     // a split sweep leaves reserve_cus CUs' worth of sampler blocks free, so
     // the collective of the part before this one finds CUs to run on

@@ -1895,6 +1895,11 @@ __global__ __launch_bounds__(256) void k_sample_sparse(SampleParams p) {
 #ifndef SB_OFF32
 #define SB_OFF32 1
 #endif
+// A/B only: keep round 3's two per-token nwsum atomics (into a scratch
+// region: the sparse apply derives the nwsum delta itself)
+#ifndef SB_DSUM_ATOMICS
+#define SB_DSUM_ATOMICS 0
+#endif
 // the per-token document-count updates as no-return LDS atomics
 #ifndef SB_NDATOM
 #define SB_NDATOM 1
@@ -2073,6 +2078,11 @@ __global__ __launch_bounds__(64 * sb_waves<C>()) void k_sample_sparse_big(Sample
         const uint64_t rb = (uint64_t)(uint32_t)cw * (uint64_t)KP;
         atomicAdd(p.delta + (rb + (uint32_t)cz), -1);
         atomicAdd(p.delta + (rb + (uint32_t)cn), 1);
+#if SB_DSUM_ATOMICS
+        // A/B only: round 3's nwsum atomics (the apply recomputes dsum anyway)
+        atomicAdd(p.dsum + cz, -1);
+        atomicAdd(p.dsum + cn, 1);
+#endif
       }
     };
 

@@ -90,31 +90,51 @@ class _SlowCollective:
     delay and adds a marker; torch's current stream waits for it, the host
     does not."""
 
-    def __init__(self, marker_cells):
+    def __init__(self, marker_cells, twice=False):
         self.marker_cells = marker_cells
+        self.twice = twice
 
     class ReduceOp:
         SUM = "sum"
         MIN = "min"
+        MAX = "max"
 
-    def all_reduce(self, t, op=None, group=None):
+    def get_backend(self, group=None):
+        return "nccl"
+
+    def all_reduce(self, t, op=None, group=None, async_op=False):
         import torch
-        if op == self.ReduceOp.MIN:
-            return                                   # one real rank: the minimum is its own value
+        if op in (self.ReduceOp.MIN, self.ReduceOp.MAX):
+            return                                   # one real rank: the extreme is its own value
         cur = torch.cuda.current_stream(t.device)
         side = torch.cuda.Stream(device=t.device)
         side.wait_stream(cur)
         with torch.cuda.stream(side):
             torch.cuda._sleep(200_000_000)            # ~0.1 s of spinning
+            if self.twice:
+                t.mul_(2)                             # two identical ranks
             for i in self.marker_cells:
                 t[i] += 7
         cur.wait_stream(side)
 
+    def all_gather_into_tensor(self, out, t, group=None, async_op=False):
+        import torch
+        cur = torch.cuda.current_stream(t.device)
+        side = torch.cuda.Stream(device=t.device)
+        side.wait_stream(cur)
+        with torch.cuda.stream(side):
+            torch.cuda._sleep(100_000_000)
+            out.view(2, -1).copy_(t.view(1, -1).expand(2, -1))
+        cur.wait_stream(side)
 
-def test_default_mode_waits_for_async_collective():
+
+@pytest.mark.parametrize("compact", [False, True])
+def test_default_mode_waits_for_async_collective(compact):
     """ADLDATrainer's default mode (engine on its own stream): the apply after
     an all-reduce that returns before the collective has landed must still
-    see the reduced delta (the RCCL/apply race)."""
+    see the reduced delta (the RCCL/apply race).  compact: the
+    packed exchange, whose unpack runs on the engine's stream after the
+    collectives (two identical "ranks": the sum is twice the counts)."""
     from ldagibbssampling_amd.corpus import synthetic_lda
     from ldagibbssampling_amd.distributed import ADLDATrainer
     from ldagibbssampling_amd.sampler import GibbsSampler
@@ -127,10 +147,17 @@ def test_default_mode_waits_for_async_collective():
     tr.world = 2                               # as if sharded: reduce, then apply
     tr._delta = g.delta_tensor()
     Kp = g.Kp
-    tr.dist = _SlowCollective([0, c.num_types * Kp])   # nw[0][0] and nwsum[0]
+    if compact:
+        tr.compact, tr.max_tokens = True, g.N
+        # packed word 0 (nw[0][0] in its low half) and the packed nwsum tail
+        tr.dist = _SlowCollective([0, c.num_types * Kp // 2], twice=True)
+    else:
+        tr.dist = _SlowCollective([0, c.num_types * Kp])   # nw[0][0] and nwsum[0]
     tr.init_counts()
     nw, nwsum, _, _ = g.counts()
     rnw, rnwsum, _, _ = ref.counts()
+    if compact:
+        rnw, rnwsum = 2 * rnw, 2 * rnwsum
     assert nw[0, 0] == rnw[0, 0] + 7 and nwsum[0] == rnwsum[0] + 7
     nw[0, 0] -= 7
     nwsum[0] -= 7

@@ -92,8 +92,9 @@ def test_compact_exchange_bit_exact(oracle, world, kind, K):
     shards (torch, in place of RCCL) plus every shard's all-gathered escape
     list unpack to the int32 sum of the shards' buffers, bit for bit, on
     every shard.  The buffers are the shards' initial counts (what the first
-    exchange sums): a hot word (half the tokens) puts counts far beyond the
-    biases 2^15/world and 2^14/world, so escapes occur in both word halves.
+    exchange sums): a hot word (half the tokens) whose tokens start in topics
+    0 and 1 (z_init) puts counts far beyond the biases 2^15/world and
+    2^14/world, so escapes occur in both halves of a word.
     The packed words and escape lists match the numpy restatement
     (oracle.exchange_pack) up to the escapes' order, which the GPU's atomic
     appends leave open."""
@@ -101,20 +102,24 @@ def test_compact_exchange_bit_exact(oracle, world, kind, K):
     from ldagibbssampling_amd.distributed import shard_corpus
     from ldagibbssampling_amd.sampler import GibbsSampler
     rng = np.random.default_rng(world * 7 + K)
-    D, L = 600, 150
+    D, L = 1500, 150
     words = rng.integers(1, 500, size=D * L).astype(np.int32)
-    words[rng.random(D * L) < 0.5] = 0                        # the hot word
+    hot = rng.random(D * L) < 0.5
+    words[hot] = 0                                            # the hot word
+    z0 = rng.integers(0, K, size=D * L).astype(np.int32)
+    z0[hot] = rng.integers(0, 2, size=int(hot.sum()))        # ... in topics 0 and 1
     doc_off = np.arange(D + 1, dtype=np.int64) * L
     shards = [shard_corpus(doc_off, words, world, r) for r in range(world)]
     gs = [GibbsSampler(K, 500, sh.doc_off, sh.words, np.full(K, 0.1), 0.01, seed=5,
-                       token_base=sh.token_base, sampler=kind) for sh in shards]
+                       token_base=sh.token_base, sampler=kind,
+                       z_init=z0[sh.token_base:sh.token_base + len(sh.words)]) for sh in shards]
     N = max(g.N for g in gs)
     before = [g.delta_tensor().clone() for g in gs]
     want = torch.stack([b.to(torch.int64) for b in before]).sum(0).to(torch.int32)
     packs = [g.exchange_pack(0, world, N) for g in gs]
     torch.cuda.synchronize()
     n_esc = [int(e[0]) for _, e in packs]
-    assert sum(n_esc) > 0
+    assert min(n_esc) >= 2          # topic 0 (low half) and topic 1 (high half) of the hot word
     Kp = gs[0].Kp
     for (pk, es), b in zip(packs, before):
         opk, oes = oracle.exchange_pack(b.cpu().numpy(), world, Kp, N)
@@ -136,7 +141,7 @@ def test_compact_exchange_bit_exact(oracle, world, kind, K):
     # and the shards then agree with one context over the whole corpus
     for g in gs:
         g.apply()
-    one = GibbsSampler(K, 500, doc_off, words, np.full(K, 0.1), 0.01, seed=5, sampler=kind)
+    one = GibbsSampler(K, 500, doc_off, words, np.full(K, 0.1), 0.01, seed=5, sampler=kind, z_init=z0)
     one.sweep(0)
     nw1, ns1, _, _ = one.counts()
     for g in gs:
