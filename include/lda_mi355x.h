@@ -224,6 +224,9 @@ lda_status lda_exchange_unpack(lda_ctx* ctx, int32_t part, int32_t world, int64_
  * shard of a token-balanced sharding into <= LDA_WARM_BLOCKS shards has work
  * in every step. */
 #define LDA_WARM_BLOCKS 64
+/* Sequential parts are cut at cumulative fractions of each block in units of
+ * 1 / LDA_SEQ_FRACTION_UNIT (lcm(1..16): equal parts are exact). */
+#define LDA_SEQ_FRACTION_UNIT 720720
 /* Host-only (no device call): the tokens a shard (documents doc_off[0..D],
  * global token base + doc_off[d] - doc_off[0]) samples in each warm-start
  * part of the corpus [corpus_first_token, + corpus_tokens), as
@@ -233,6 +236,30 @@ lda_status lda_warm_part_tokens(const int64_t* doc_off, int64_t num_docs, int32_
 lda_status lda_set_warm_start(lda_ctx* ctx, int32_t parts, int32_t sweeps, int64_t corpus_first_token,
                               int64_t corpus_tokens);
 lda_status lda_get_warm_start(lda_ctx* ctx, int32_t* parts, int32_t* sweeps);
+/* Steady sequential sweeps: Mallet's staleness.  The snapshot sweep shows
+ * every token none of the sweep's other changes; Mallet's setNumThreads(T)
+ * workers each see their own changes live, so a token sees on average
+ * 1/(2T) of them.  That difference is measurable at the reference's own
+ * training settings: with hyperparameter optimisation the snapshot sweep
+ * learns beta ~9% higher and alphaSum ~4% lower than Mallet's 4 threads and,
+ * at K = 500, traps more chains.
+ * lda_set_sequential_sweeps(ctx, parts, fractions, first, tokens): every
+ * sweep that is not a warm-start sweep runs in `parts` sequential parts (as
+ * the warm start's, each applied before the next samples, all through buffer
+ * 0), part i taking the fraction fractions[i] of each of the
+ * LDA_WARM_BLOCKS blocks of the corpus (fractions NULL: equal parts); parts
+ * = 1 turns it off (the default: lda_sweep's plain snapshot sweeps).  The
+ * corpus arguments are lda_set_warm_start's.  lda_staleness_schedule(T)
+ * gives the schedule with Mallet's mean live fraction for T threads: two
+ * parts, the first f = (1 - sqrt(1 - 2/T)) / 2 of every block (T = 4: f =
+ * 0.146), so that f (1 - f) = 1/(2T); T = 1 gives LDA_MAX_EXCHANGE_PARTS
+ * equal parts (mean 3/8, the nearest to sequential Mallet's 1/2).
+ * lda_get_sequential_sweeps: the parts and the cumulative cut fractions
+ * cum_units[parts + 1] in units of 1 / LDA_SEQ_FRACTION_UNIT. */
+lda_status lda_set_sequential_sweeps(lda_ctx* ctx, int32_t parts, const double* fractions,
+                                     int64_t corpus_first_token, int64_t corpus_tokens);
+lda_status lda_get_sequential_sweeps(lda_ctx* ctx, int32_t* parts, int64_t* cum_units);
+lda_status lda_staleness_schedule(int32_t threads, int32_t* parts, double* fractions);
 /* The parts of the sweep in progress (or of the next one) and whether they
  * are sequential (a warm-start sweep) or exchange-overlapped. */
 lda_status lda_sweep_parts(lda_ctx* ctx, int32_t* parts, int32_t* sequential);

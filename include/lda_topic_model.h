@@ -89,6 +89,15 @@ lda_status ldatm_set_exchange_parts(ldatm* m, int32_t parts);
  * worse local optimum instead of 18 / 48; cpu_mallet 16 / 48).
  * (1, 0) turns it off.  Carried by checkpoints and by the sweep counter. */
 lda_status ldatm_set_warm_start(ldatm* m, int32_t parts, int32_t sweeps);
+/* Sweeps past the warm start show each token the share of the sweep's other
+ * changes that Mallet's T worker threads would (lda_set_sequential_sweeps /
+ * lda_staleness_schedule): threads = 0 (the default) takes T
+ * from ldatm_set_num_threads (the reference's setNumThreads(4)), threads > 0
+ * sets T, threads < 0 runs plain snapshot sweeps.  Without it the learned
+ * hyperparameters drift from Mallet's at the reference's settings (beta
+ * ~9% high, alphaSum ~4% low) and K = 500 traps more chains.  Carried by
+ * checkpoints (files before format v3 continue with snapshot sweeps). */
+lda_status ldatm_set_staleness_threads(ldatm* m, int32_t threads);
 /* State a Java-side ParallelTopicModel already holds, for GpuParallelTopicModel
  * (integration/): the topics Mallet's own addInstances drew (z[n], n = every
  * token of the model), alpha[K] / alphaSum / beta after an earlier optimisation,

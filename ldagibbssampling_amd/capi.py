@@ -117,6 +117,9 @@ SIGNATURES = {
     "lda_exchange_pack": (C.c_int32, [_vp, C.c_int32, C.c_int32, C.c_int64, C.POINTER(_vp),
                                       C.POINTER(_vp)]),
     "lda_exchange_unpack": (C.c_int32, [_vp, C.c_int32, C.c_int32, C.c_int64, _vp]),
+    "lda_set_sequential_sweeps": (C.c_int32, [_vp, C.c_int32, _vp, C.c_int64, C.c_int64]),
+    "lda_get_sequential_sweeps": (C.c_int32, [_vp, C.POINTER(C.c_int32), _vp]),
+    "lda_staleness_schedule": (C.c_int32, [C.c_int32, C.POINTER(C.c_int32), _vp]),
     "lda_warm_part_tokens": (C.c_int32, [_vp, C.c_int64, C.c_int32, C.c_int64, C.c_int64, C.c_int64, _vp]),
     "lda_sweep_parts": (C.c_int32, [_vp, C.POINTER(C.c_int32), C.POINTER(C.c_int32)]),
     "lda_get_count_update": (C.c_int32, [_vp, C.POINTER(C.c_int32), C.POINTER(C.c_int32)]),

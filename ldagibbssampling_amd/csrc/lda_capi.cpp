@@ -126,32 +126,45 @@ std::vector<int64_t> make_cut_ranges(const std::vector<int64_t>& off, int64_t ta
   return r;
 }
 
-// Warm-start parts (lda_set_warm_start), seen from a shard whose documents
-// start at global token base + off[d]: the corpus [g0, g0 + gn) is cut into
-// S = parts * LDA_WARM_BLOCKS token-balanced segments (cut j = the first
-// document starting at or after g0 + gn * j / S) and segment j belongs to
-// part j % parts.  Every shard of a token-balanced sharding into up to
-// LDA_WARM_BLOCKS shards therefore holds documents of every part (round 3
-// had cut P contiguous parts, so at G = 8, P = 4 only 2 of 8 GPUs sampled in
-// each step).  runs[i] = part i's local document runs [d0, d1), in order.
-std::vector<std::vector<std::pair<int64_t, int64_t>>> warm_part_runs(const std::vector<int64_t>& off,
-                                                                     int parts, int64_t base,
-                                                                     int64_t g0, int64_t gn) {
+// Sequential-sweep parts (lda_set_warm_start, lda_set_sequential_sweeps),
+// seen from a shard whose documents start at global token base + off[d]:
+// the corpus [g0, g0 + gn) is cut into LDA_WARM_BLOCKS token-balanced blocks,
+// and block b into `parts` pieces at the cumulative fractions cum[i] / Q
+// (Q = LDA_SEQ_FRACTION_UNIT; cum[0] = 0, cum[parts] = Q): the cut at (b, i)
+// is the first document starting at or after g0 + gn (b Q + cum[i]) / (B Q),
+// and piece i of every block belongs to part i.  Every shard of a
+// token-balanced sharding into up to LDA_WARM_BLOCKS shards therefore holds
+// documents of every part (round 3 had cut P contiguous parts, so at G = 8,
+// P = 4 only 2 of 8 GPUs sampled in each step).  runs[i] = part i's local
+// document runs [d0, d1), in order.  Integer arithmetic: the oracle cuts the
+// same documents (gn < 2^40 keeps gn B Q < 2^63).
+std::vector<std::vector<std::pair<int64_t, int64_t>>> seq_part_runs(const std::vector<int64_t>& off,
+                                                                    const std::vector<int64_t>& cum,
+                                                                    int64_t base, int64_t g0, int64_t gn) {
   const int64_t D = (int64_t)off.size() - 1;
-  const int64_t S = (int64_t)parts * LDA_WARM_BLOCKS;
+  const int parts = (int)cum.size() - 1;
+  const int64_t B = LDA_WARM_BLOCKS, Q = LDA_SEQ_FRACTION_UNIT;
   std::vector<std::vector<std::pair<int64_t, int64_t>>> runs((size_t)parts);
   int64_t prev = 0;
-  for (int64_t j = 0; j < S; ++j) {
-    int64_t next = D;
-    if (j + 1 < S) {
-      const int64_t tgt = g0 + gn * (j + 1) / S - base;
-      next = std::lower_bound(off.begin(), off.end(), tgt) - off.begin();
-      next = std::min(std::max(next, prev), D);
+  for (int64_t b = 0; b < B; ++b)
+    for (int i = 0; i < parts; ++i) {
+      int64_t next = D;
+      if (b + 1 < B || i + 1 < parts) {
+        const int64_t tgt = g0 + gn * (b * Q + cum[(size_t)i + 1]) / (B * Q) - base;
+        next = std::lower_bound(off.begin(), off.end(), tgt) - off.begin();
+        next = std::min(std::max(next, prev), D);
+      }
+      if (next > prev) runs[(size_t)i].push_back({prev, next});
+      prev = next;
     }
-    if (next > prev) runs[(size_t)(j % parts)].push_back({prev, next});
-    prev = next;
-  }
   return runs;
+}
+
+// cumulative fractions of `parts` equal parts, in units of 1 / LDA_SEQ_FRACTION_UNIT (exact)
+std::vector<int64_t> equal_cum(int parts) {
+  std::vector<int64_t> cum((size_t)parts + 1);
+  for (int i = 0; i <= parts; ++i) cum[(size_t)i] = (int64_t)LDA_SEQ_FRACTION_UNIT * i / parts;
+  return cum;
 }
 
 // The work ranges of each part's document runs: ranges never cross a run
@@ -272,12 +285,20 @@ struct lda_ctx {
   // warm start (lda_set_warm_start): sweeps with a sweep counter below
   // warm_sweeps run in warm_parts SEQUENTIAL parts (each applied before
   // the next part samples; all through buffer 0), over their own ranges
-  int warm_parts = 1;
+  // A sequential schedule: parts sampled in order, each applied before the
+  // next samples (all through buffer 0), over their own work ranges
+  struct SeqSchedule {
+    int parts = 1;
+    int64_t* range_doc = nullptr;    // range starts [R], then the ends (range_end)
+    int64_t* range_end = nullptr;
+    std::vector<int64_t> part_range{0, 0};
+    std::vector<int64_t> cum{0, LDA_SEQ_FRACTION_UNIT};
+  };
+  SeqSchedule warm;                  // lda_set_warm_start: sweeps below warm_sweeps
   int32_t warm_sweeps = 0;
-  int64_t* warm_range_doc = nullptr;   // range starts [R_warm], then the ends (warm_range_end)
-  int64_t* warm_range_end = nullptr;
-  std::vector<int64_t> warm_part_range{0, 0};
-  bool sweep_seq = false;          // the sweep being sampled is a warm-start sweep
+  SeqSchedule steady;                // lda_set_sequential_sweeps: every other sweep
+  bool sweep_seq = false;            // the sweep being sampled is sequential ...
+  int sweep_kind = 0;                // ... 1: a warm-start sweep, 2: a steady one
   uint32_t* perm = nullptr;        // [N] token indices grouped by (part, word)
   int32_t* items = nullptr;        // int4 {word, first perm index, tokens, split} per work item
   std::vector<int64_t> part_item{0, 0};
@@ -374,7 +395,7 @@ struct lda_ctx {
                     (void*)inv, (void*)inv_m1, (void*)partial, (void*)nonzero, (void*)ent,
                     (void*)row_off, (void*)row_nnz, (void*)row_rnd, (void*)nw16, (void*)wide, (void*)inf_words,
                     (void*)inf_z, (void*)inf_acc, (void*)inf_q, (void*)inf_doff, (void*)inf_range,
-                    (void*)perm, (void*)items, (void*)warm_range_doc})
+                    (void*)perm, (void*)items, (void*)warm.range_doc, (void*)steady.range_doc})
       if (p) (void)hipFree(p);
     for (int i = 1; i < LDA_MAX_EXCHANGE_PARTS; ++i)
       if (delta_part[i]) (void)hipFree(delta_part[i]);
@@ -578,13 +599,20 @@ static lda_status apply_impl(lda_ctx* c) {
 // Is the next sweep a warm-start sweep (sequential parts)?
 // (keyed by the sweep counter, which a resumed model carries: estimate(15) +
 // estimate(25) runs the same warm start as estimate(40))
-static bool next_sweep_sequential(const lda_ctx* c) {
-  return c->warm_parts > 1 && (int64_t)c->sweep < (int64_t)c->warm_sweeps;
+static int next_sweep_kind(const lda_ctx* c) {
+  if (c->warm.parts > 1 && (int64_t)c->sweep < (int64_t)c->warm_sweeps) return 1;
+  return c->steady.parts > 1 ? 2 : 0;
+}
+static bool next_sweep_sequential(const lda_ctx* c) { return next_sweep_kind(c) != 0; }
+// the schedule of the sweep in progress (or of the next one)
+static const lda_ctx::SeqSchedule& seq_schedule(const lda_ctx* c) {
+  const int kind = c->next_part != 0 ? c->sweep_kind : next_sweep_kind(c);
+  return kind == 1 ? c->warm : c->steady;
 }
 // Parts of the sweep in progress, or of the next one
 static int sweep_parts(const lda_ctx* c) {
   const bool seq = c->next_part != 0 ? c->sweep_seq : next_sweep_sequential(c);
-  return seq ? c->warm_parts : c->parts;
+  return seq ? seq_schedule(c).parts : c->parts;
 }
 
 // Will the next sweep recount?  (never a warm-start sweep: its parts are
@@ -884,7 +912,8 @@ static lda_status sample_part_impl(lda_ctx* c, int part) {
                                          : "warm-start sweep: apply each part before sampling the next");
   HIP_TRY(hipSetDevice(c->device));
   if (part == 0) {
-    c->sweep_seq = next_sweep_sequential(c);
+    c->sweep_kind = next_sweep_kind(c);
+    c->sweep_seq = c->sweep_kind != 0;
     c->sweep_recount = next_sweep_recounts(c);
     if (c->sweep_recount && !c->perm && c->N > 0) {
       lda_status s = build_recount_index(c);
@@ -901,8 +930,9 @@ static lda_status sample_part_impl(lda_ctx* c, int part) {
     c->zw_valid = c->sweep_zw;
   }
   const bool seq = c->sweep_seq;
-  const int nparts = seq ? c->warm_parts : c->parts;
-  const std::vector<int64_t>& prange = seq ? c->warm_part_range : c->part_range;
+  const lda_ctx::SeqSchedule& sch = c->sweep_kind == 1 ? c->warm : c->steady;
+  const int nparts = seq ? sch.parts : c->parts;
+  const std::vector<int64_t>& prange = seq ? sch.part_range : c->part_range;
   const int64_t r0 = prange[(size_t)part], r1 = prange[(size_t)part + 1];
   int32_t* buf = c->delta_part[seq ? 0 : part];
   if (r1 > r0) {
@@ -910,8 +940,8 @@ static lda_status sample_part_impl(lda_ctx* c, int part) {
     if (c->sampler != LDA_SAMPLER_DENSE || part > 0)
       HIP_TRY(hipMemsetAsync(c->queue + part, 0, sizeof(int32_t), c->stream));
     lda::SampleParams p = c->params(false);
-    p.range_doc = (seq ? c->warm_range_doc : c->range_doc) + r0;
-    p.range_end = (seq ? c->warm_range_end : c->range_doc + 1) + r0;
+    p.range_doc = (seq ? sch.range_doc : c->range_doc) + r0;
+    p.range_end = (seq ? sch.range_end : c->range_doc + 1) + r0;
     p.num_ranges = r1 - r0;
     p.queue = c->queue + part;
     p.delta = c->sweep_recount ? nullptr : buf;   // recount: the sampler writes z only
@@ -1217,6 +1247,33 @@ lda_status lda_recount_times(lda_ctx* c, int32_t max, float* ms, int32_t* n) {
   });
 }
 
+// (re)builds a sequential schedule's work ranges on the device
+static lda_status build_schedule(lda_ctx* c, const std::vector<int64_t>& cum, int64_t g0, int64_t gn,
+                                 lda_ctx::SeqSchedule& sch) {
+  const int parts = (int)cum.size() - 1;
+  if (parts > 1) {
+    std::vector<int64_t> pr, st, en;
+    make_run_ranges(c->doc_off_h, c->tokens_per_range, seq_part_runs(c->doc_off_h, cum, c->token_base, g0, gn),
+                    st, en, pr);
+    // one device buffer: starts [R] then ends [R]
+    const size_t R = st.size();
+    st.insert(st.end(), en.begin(), en.end());
+    int64_t* dr = nullptr;
+    HIP_TRY(dalloc(&dr, st.size()));
+    hipError_t e = hipMemcpyAsync(dr, st.data(), sizeof(int64_t) * st.size(), hipMemcpyHostToDevice, c->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    if (e != hipSuccess) (void)hipFree(dr);
+    HIP_TRY(e);
+    if (sch.range_doc) (void)hipFree(sch.range_doc);
+    sch.range_doc = dr;
+    sch.range_end = dr + R;
+    sch.part_range = pr;
+  }
+  sch.parts = parts;
+  sch.cum = cum;
+  return LDA_OK;
+}
+
 lda_status lda_set_warm_start(lda_ctx* c, int32_t parts, int32_t sweeps, int64_t corpus_first_token,
                               int64_t corpus_tokens) {
   return lda_abi::guarded([&]() -> lda_status {
@@ -1229,27 +1286,78 @@ lda_status lda_set_warm_start(lda_ctx* c, int32_t parts, int32_t sweeps, int64_t
     corpus_tokens = c->N;
   }
   HIP_TRY(hipSetDevice(c->device));
-  if (parts > 1) {
-    std::vector<int64_t> pr, st, en;
-    make_run_ranges(c->doc_off_h, c->tokens_per_range,
-                    warm_part_runs(c->doc_off_h, parts, c->token_base, corpus_first_token, corpus_tokens),
-                    st, en, pr);
-    // one device buffer: starts [R] then ends [R]
-    const size_t R = st.size();
-    st.insert(st.end(), en.begin(), en.end());
-    int64_t* dr = nullptr;
-    HIP_TRY(dalloc(&dr, st.size()));
-    hipError_t e = hipMemcpyAsync(dr, st.data(), sizeof(int64_t) * st.size(), hipMemcpyHostToDevice, c->stream);
-    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
-    if (e != hipSuccess) (void)hipFree(dr);
-    HIP_TRY(e);
-    if (c->warm_range_doc) (void)hipFree(c->warm_range_doc);
-    c->warm_range_doc = dr;
-    c->warm_range_end = dr + R;
-    c->warm_part_range = pr;
-  }
-  c->warm_parts = parts;
+  lda_status s = build_schedule(c, equal_cum(parts), corpus_first_token, corpus_tokens, c->warm);
+  if (s) return s;
   c->warm_sweeps = parts > 1 ? sweeps : 0;
+  c->graph_key = lda_ctx::GraphKey{};
+  return LDA_OK;
+  });
+}
+
+// fractions[parts] > 0 summing to 1 -> cumulative units of 1 / LDA_SEQ_FRACTION_UNIT
+static bool quantise_fractions(int32_t parts, const double* fractions, std::vector<int64_t>& cum) {
+  cum.assign((size_t)parts + 1, 0);
+  double acc = 0.0;
+  for (int i = 0; i < parts; ++i) {
+    if (!(fractions[i] > 0.0)) return false;
+    acc += fractions[i];
+    cum[(size_t)i + 1] = i + 1 == parts ? LDA_SEQ_FRACTION_UNIT
+                                        : (int64_t)std::llround(acc * (double)LDA_SEQ_FRACTION_UNIT);
+    if (cum[(size_t)i + 1] <= cum[(size_t)i]) return false;
+  }
+  return std::fabs(acc - 1.0) <= 1e-9 && cum[(size_t)parts - 1] < LDA_SEQ_FRACTION_UNIT;
+}
+
+lda_status lda_set_sequential_sweeps(lda_ctx* c, int32_t parts, const double* fractions, int64_t corpus_first_token,
+                                     int64_t corpus_tokens) {
+  return lda_abi::guarded([&]() -> lda_status {
+  if (!c) return fail(LDA_ERR_INVALID_ARG, "null ctx");
+  if (parts < 1 || parts > LDA_MAX_EXCHANGE_PARTS)
+    return fail(LDA_ERR_INVALID_ARG, "parts must be in [1, LDA_MAX_EXCHANGE_PARTS]");
+  std::vector<int64_t> cum;
+  if (parts > 1 && !fractions) cum = equal_cum(parts);
+  else if (parts > 1 && !quantise_fractions(parts, fractions, cum))
+    return fail(LDA_ERR_INVALID_ARG, "fractions must be > 0, increasing when quantised, and sum to 1");
+  if (parts == 1) cum = equal_cum(1);
+  if (c->next_part != 0) return fail(LDA_ERR_STATE, "inside a split sweep");
+  if (corpus_tokens <= 0) {
+    corpus_first_token = c->token_base;
+    corpus_tokens = c->N;
+  }
+  HIP_TRY(hipSetDevice(c->device));
+  lda_status s = build_schedule(c, cum, corpus_first_token, corpus_tokens, c->steady);
+  if (s) return s;
+  c->graph_key = lda_ctx::GraphKey{};
+  return LDA_OK;
+  });
+}
+
+lda_status lda_get_sequential_sweeps(lda_ctx* c, int32_t* parts, int64_t* cum_units) {
+  return lda_abi::guarded([&]() -> lda_status {
+  if (!c) return fail(LDA_ERR_INVALID_ARG, "null ctx");
+  if (parts) *parts = c->steady.parts;
+  if (cum_units)
+    for (size_t i = 0; i < c->steady.cum.size(); ++i) cum_units[i] = c->steady.cum[i];
+  return LDA_OK;
+  });
+}
+
+lda_status lda_staleness_schedule(int32_t threads, int32_t* parts, double* fractions) {
+  return lda_abi::guarded([&]() -> lda_status {
+  if (threads < 1 || !parts || !fractions) return fail(LDA_ERR_INVALID_ARG, "threads >= 1 and outputs needed");
+  if (threads == 1) {
+    // sequential Mallet (mean live fraction 1/2): the most parts allowed
+    *parts = LDA_MAX_EXCHANGE_PARTS;
+    for (int i = 0; i < *parts; ++i) fractions[i] = 1.0 / *parts;
+    return LDA_OK;
+  }
+  // two parts, the first a fraction f of every block: its tokens see none of
+  // the sweep's changes, the second part's see f, so the mean live fraction
+  // is f (1 - f) = 1 / (2 T), Mallet's with T worker threads
+  const double f = 0.5 * (1.0 - std::sqrt(1.0 - 2.0 / threads));
+  *parts = 2;
+  fractions[0] = f;
+  fractions[1] = 1.0 - f;
   return LDA_OK;
   });
 }
@@ -1261,7 +1369,7 @@ lda_status lda_warm_part_tokens(const int64_t* doc_off, int64_t num_docs, int32_
     return fail(LDA_ERR_INVALID_ARG, "null pointer, num_docs < 0, parts outside [1, LDA_MAX_EXCHANGE_PARTS] or corpus_tokens <= 0");
   std::vector<int64_t> off(doc_off, doc_off + num_docs + 1);
   for (auto& o : off) o -= doc_off[0];
-  const auto runs = warm_part_runs(off, parts, token_base, corpus_first_token, corpus_tokens);
+  const auto runs = seq_part_runs(off, equal_cum(parts), token_base, corpus_first_token, corpus_tokens);
   for (int i = 0; i < parts; ++i) {
     int64_t n = 0;
     for (const auto& r : runs[(size_t)i]) n += off[(size_t)r.second] - off[(size_t)r.first];
@@ -1273,7 +1381,7 @@ lda_status lda_warm_part_tokens(const int64_t* doc_off, int64_t num_docs, int32_
 
 lda_status lda_get_warm_start(lda_ctx* c, int32_t* parts, int32_t* sweeps) {
   if (!c) return fail(LDA_ERR_INVALID_ARG, "null ctx");
-  if (parts) *parts = c->warm_parts;
+  if (parts) *parts = c->warm.parts;
   if (sweeps) *sweeps = c->warm_sweeps;
   return LDA_OK;
 }
@@ -1281,7 +1389,7 @@ lda_status lda_get_warm_start(lda_ctx* c, int32_t* parts, int32_t* sweeps) {
 lda_status lda_sweep_parts(lda_ctx* c, int32_t* parts, int32_t* sequential) {
   if (!c) return fail(LDA_ERR_INVALID_ARG, "null ctx");
   const bool seq = c->next_part != 0 ? c->sweep_seq : next_sweep_sequential(c);
-  if (parts) *parts = seq ? c->warm_parts : c->parts;
+  if (parts) *parts = seq ? seq_schedule(c).parts : c->parts;
   if (sequential) *sequential = seq ? 1 : 0;
   return LDA_OK;
 }

@@ -419,9 +419,27 @@ void ParallelTopicModel::setWarmStart(int32_t parts, int32_t sweeps) {
     raise(LDA_ERR_INVALID_ARG, "warm start: parts in [1, 4], sweeps >= 0");
   warm_parts_ = parts;
   warm_sweeps_ = sweeps;
-  if (shards_ && !shards_dirty_)
-    for (auto c : shards_->ctx)
-      check(lda_set_warm_start(c, warm_parts_, warm_sweeps_, 0, numTokens()), "lda_set_warm_start");
+  if (shards_ && !shards_dirty_) applySweepSchedule();
+}
+
+void ParallelTopicModel::setStalenessThreads(int32_t threads) {
+  staleness_threads_ = threads;
+  if (shards_ && !shards_dirty_) applySweepSchedule();
+}
+
+// the shards' sequential sweeps: the warm start, then Mallet's staleness for
+// T threads; parts cut in the whole corpus, so the sweeps are
+// the same for any shard count
+void ParallelTopicModel::applySweepSchedule() {
+  const int64_t N = numTokens();
+  int32_t parts = 1;
+  double fr[LDA_MAX_EXCHANGE_PARTS] = {1.0};
+  const int32_t T = staleness_threads_ == 0 ? num_threads_ : staleness_threads_;
+  if (T > 0) check(lda_staleness_schedule(T, &parts, fr), "lda_staleness_schedule");
+  for (auto c : shards_->ctx) {
+    check(lda_set_warm_start(c, warm_parts_, warm_sweeps_, 0, N), "lda_set_warm_start");
+    check(lda_set_sequential_sweeps(c, parts, parts > 1 ? fr : nullptr, 0, N), "lda_set_sequential_sweeps");
+  }
 }
 
 void ParallelTopicModel::setDevices(const int32_t* devices, int32_t n) {
@@ -565,10 +583,9 @@ void ParallelTopicModel::ensureShards() {
   sg->reduce();
   sg->apply();
   sg->set_parts(exchange_parts_);
-  // warm-start parts cut in the whole corpus: the same sweeps for any shard count
-  for (auto c : sg->ctx) check(lda_set_warm_start(c, warm_parts_, warm_sweeps_, 0, N), "lda_set_warm_start");
   for (auto c : sg->ctx) check(lda_set_sweep(c, sweep_), "lda_set_sweep");
   shards_ = std::move(sg);
+  applySweepSchedule();
   shards_dirty_ = false;
   z_dirty_ = true;
   // word totals never change between addInstances calls: the bound of beta's
@@ -839,7 +856,8 @@ std::string ParallelTopicModel::displayTopWords(int32_t num_words, bool using_ne
 // Mallet 2.0.7's new WorkerRunnables drop theirs, so a resumed model starts
 // its statistics empty whatever the file holds.
 namespace {
-constexpr char kMagic[8] = {'L', 'D', 'A', 'T', 'M', 0, 'v', '2'};    // v2: + warm start
+constexpr char kMagic[8] = {'L', 'D', 'A', 'T', 'M', 0, 'v', '3'};    // v3: + staleness threads
+constexpr char kMagicV2[8] = {'L', 'D', 'A', 'T', 'M', 0, 'v', '2'};  // v2: + warm start
 constexpr char kMagicV1[8] = {'L', 'D', 'A', 'T', 'M', 0, 'v', '1'};
 
 struct Writer {
@@ -919,6 +937,7 @@ void ParallelTopicModel::save(const std::string& path) {
   w.vec(topic_doc_counts_);
   w.pod(warm_parts_);
   w.pod(warm_sweeps_);
+  w.pod(staleness_threads_);
   w.f.flush();
   if (!w.f) raise(LDA_ERR_INVALID_ARG, "write failed: " + path);
 }
@@ -929,7 +948,8 @@ std::unique_ptr<ParallelTopicModel> ParallelTopicModel::load(const std::string& 
   char magic[8];
   r.f.read(magic, 8);
   const bool v1 = r.f && std::memcmp(magic, kMagicV1, 8) == 0;
-  if (!r.f || (!v1 && std::memcmp(magic, kMagic, 8) != 0))
+  const bool v2 = r.f && std::memcmp(magic, kMagicV2, 8) == 0;
+  if (!r.f || (!v1 && !v2 && std::memcmp(magic, kMagic, 8) != 0))
     raise(LDA_ERR_INVALID_ARG, "not an lda_topic_model checkpoint");
   const int32_t K = r.pod<int32_t>(), V = r.pod<int32_t>();
   const double alpha_sum = r.pod<double>(), beta = r.pod<double>();
@@ -978,6 +998,8 @@ std::unique_ptr<ParallelTopicModel> ParallelTopicModel::load(const std::string& 
     m->warm_parts_ = r.pod<int32_t>();
     m->warm_sweeps_ = r.pod<int32_t>();
   }
+  // files before v3 continue with the snapshot sweeps they were made with
+  m->staleness_threads_ = (v1 || v2) ? -1 : r.pod<int32_t>();
   m->shards_dirty_ = true;
   return m;
 }
@@ -1126,6 +1148,11 @@ TM_SETTER(ldatm_set_exchange_parts, setExchangeParts(n))
 lda_status ldatm_set_warm_start(ldatm* m, int32_t parts, int32_t sweeps) {
   TM_CHECK(m);
   return guard([&] { m->model.setWarmStart(parts, sweeps); });
+}
+
+lda_status ldatm_set_staleness_threads(ldatm* m, int32_t threads) {
+  TM_CHECK(m);
+  return guard([&] { m->model.setStalenessThreads(threads); });
 }
 
 lda_status ldatm_set_devices(ldatm* m, int32_t n, const int32_t* devices) {

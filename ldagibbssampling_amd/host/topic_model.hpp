@@ -62,6 +62,10 @@ class ParallelTopicModel {
   // warm start (lda_set_warm_start): sweeps 0..sweeps-1 in `parts` sequential
   // parts; the default 4 x 50 (held-out perplexity at K = 20)
   void setWarmStart(int32_t parts, int32_t sweeps);
+  // sweeps past the warm start emulate the staleness of Mallet's T worker
+  // threads (lda_staleness_schedule): T = 0 -> numThreads (the default),
+  // T < 0 -> plain snapshot sweeps
+  void setStalenessThreads(int32_t threads);
   int32_t numShards();
   void setVerbosity(int32_t v) { verbosity_ = v; }
   // state a Java-side ParallelTopicModel already holds (GpuParallelTopicModel:
@@ -133,6 +137,8 @@ class ParallelTopicModel {
   // LDA_EXCHANGE_INT32=1 in the environment sends the int32 buffers (A/B)
   bool compact_exchange_ = true;
   int32_t warm_parts_ = 4, warm_sweeps_ = 50;
+  int32_t staleness_threads_ = 0;
+  void applySweepSchedule();
 
   std::vector<int32_t> devices_;  // setDevices (empty: plan_shards)
   std::unique_ptr<ShardGroup> shards_;

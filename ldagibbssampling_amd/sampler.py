@@ -217,6 +217,27 @@ class GibbsSampler:
         capi.check(self._L.lda_set_warm_start(self._h, int(parts), int(sweeps), int(corpus_first_token),
                                               int(corpus_tokens)), "lda_set_warm_start")
 
+    def set_sequential_sweeps(self, parts: int = 1, fractions=None, corpus_first_token: int = 0,
+                              corpus_tokens: int = 0):
+        """lda_set_sequential_sweeps: every sweep past the warm start in `parts`
+        sequential parts, part i the fraction fractions[i] of every block
+        (None: equal parts; parts = 1: plain snapshot sweeps)."""
+        fr = None
+        if parts > 1 and fractions is not None:
+            self._seq_fr = np.ascontiguousarray(fractions, dtype=np.float64)
+            assert self._seq_fr.shape == (parts,)
+            fr = self._seq_fr.ctypes.data
+        capi.check(self._L.lda_set_sequential_sweeps(self._h, int(parts), fr, int(corpus_first_token),
+                                                     int(corpus_tokens)), "lda_set_sequential_sweeps")
+
+    def sequential_sweeps(self):
+        """(parts, cumulative cuts in units of 1/LDA_SEQ_FRACTION_UNIT)."""
+        n = C.c_int32()
+        cum = np.zeros(capi.MAX_EXCHANGE_PARTS + 1, dtype=np.int64)
+        capi.check(self._L.lda_get_sequential_sweeps(self._h, C.byref(n), cum.ctypes.data),
+                   "lda_get_sequential_sweeps")
+        return int(n.value), cum[:n.value + 1].tolist()
+
     def sweep_parts(self):
         """(parts, sequential) of the sweep in progress or the next one."""
         p, q = C.c_int32(), C.c_int32()

@@ -53,6 +53,7 @@ TM_SIGNATURES = {
     "ldatm_set_exchange_parts": (_i32, [_vp, _i32]),
     "ldatm_set_devices": (_i32, [_vp, _i32, _vp]),
     "ldatm_set_warm_start": (_i32, [_vp, _i32, _i32]),
+    "ldatm_set_staleness_threads": (_i32, [_vp, _i32]),
     "ldatm_num_shards": (_i32, [_vp, C.POINTER(_i32)]),
     "ldatm_plan_shards": (_i32, [_i32, _i32, C.c_int64, _i32, _i32, C.c_int64]),
     "ldatm_set_topics": (_i32, [_vp, C.c_int64, _vp]),
@@ -297,6 +298,11 @@ class ParallelTopicModel:
     def setWarmStart(self, parts: int, sweeps: int):
         """Sweeps 0..sweeps-1 in `parts` sequential parts (default 4 x 50; (1, 0) = off)."""
         _check(self._L.ldatm_set_warm_start(self._h, int(parts), int(sweeps)), "setWarmStart")
+
+    def setStalenessThreads(self, threads: int):
+        """Sweeps past the warm start with the staleness of Mallet's T worker
+        threads (0 = setNumThreads' T, the default; < 0 = snapshot sweeps)."""
+        _check(self._L.ldatm_set_staleness_threads(self._h, int(threads)), "setStalenessThreads")
 
     def numShards(self) -> int:
         n = C.c_int32()

@@ -170,6 +170,34 @@ class JavaRandom:
 
 
 # ---------------------------------------------------------------- cpu_exact
+SEQ_FRACTION_UNIT = 720720      # include/lda_mi355x.h LDA_SEQ_FRACTION_UNIT
+
+
+def equal_cum(parts: int):
+    """lda_capi.cpp equal_cum: cumulative cuts of equal parts (exact)."""
+    return [SEQ_FRACTION_UNIT * i // parts for i in range(parts + 1)]
+
+
+def quantise_fractions(fractions):
+    """lda_capi.cpp quantise_fractions: cumulative fractions in units of
+    1 / SEQ_FRACTION_UNIT (llround of the running double sum; the last = 1)."""
+    import math
+    cum, acc = [0], 0.0
+    for i, f in enumerate(fractions):
+        acc += float(f)
+        cum.append(SEQ_FRACTION_UNIT if i + 1 == len(fractions)
+                   else int(math.floor(acc * SEQ_FRACTION_UNIT + 0.5)))
+    return cum
+
+
+def staleness_schedule(threads: int):
+    """lda_staleness_schedule: (parts, fractions) with Mallet's mean live
+    fraction 1/(2T) for T worker threads."""
+    import math
+    if threads == 1:
+        return 4, [0.25] * 4
+    f = 0.5 * (1.0 - math.sqrt(1.0 - 2.0 / threads))
+    return 2, [f, 1.0 - f]
 class ExactSampler:
     """cpu_exact: the bit-exact definition of the GPU sampler (one shard)."""
 
@@ -214,46 +242,74 @@ class ExactSampler:
 
     def set_warm_start(self, parts: int, sweeps: int, corpus_first_token: int = 0, corpus_tokens: int = 0):
         """lda_set_warm_start: sweeps whose sweep counter is below `sweeps` run in
-        `parts` sequential parts (interleaved token-balanced segments of the
-        corpus, _warm_runs), each applied before the next."""
+        `parts` sequential parts (equal pieces of each block of the corpus,
+        _seq_runs), each applied before the next."""
         self._warm = (int(parts), int(sweeps) if parts > 1 else 0)
-        if corpus_tokens <= 0:                      # this shard is the whole corpus
-            corpus_first_token, corpus_tokens = self.token_base, self.N
-        self._warm_corpus = (int(corpus_first_token), int(corpus_tokens))
+        self._warm_cum = equal_cum(int(parts))
+        self._warm_corpus = self._corpus(corpus_first_token, corpus_tokens)
+
+    def set_sequential_sweeps(self, parts: int, fractions=None, corpus_first_token: int = 0,
+                              corpus_tokens: int = 0):
+        """lda_set_sequential_sweeps: every sweep that is not a warm-start sweep
+        in `parts` sequential parts, part i the fraction fractions[i] of every
+        block (quantised as lda_capi.cpp quantise_fractions)."""
+        parts = int(parts)
+        self._steady_cum = equal_cum(parts) if (parts == 1 or fractions is None) else \
+            quantise_fractions(fractions)
+        self._steady_corpus = self._corpus(corpus_first_token, corpus_tokens)
+
+    def _corpus(self, g0, gn):
+        if gn <= 0:                                  # this shard is the whole corpus
+            return (self.token_base, self.N)
+        return (int(g0), int(gn))
 
     WARM_BLOCKS = 64      # include/lda_mi355x.h LDA_WARM_BLOCKS
 
-    def _warm_runs(self):
-        """lda_capi.cpp warm_part_runs: the corpus [g0, g0 + gn) is cut into
-        S = P * WARM_BLOCKS token-balanced segments (cut j = the first
-        document starting at or after g0 + gn * j // S) and segment j belongs
-        to part j % P; returns part i's local document runs [(d0, d1), ...]."""
-        P = self._warm[0]
-        S = P * self.WARM_BLOCKS
-        g0, gn = self._warm_corpus
+    def _seq_runs(self, cum, corpus):
+        """lda_capi.cpp seq_part_runs: the corpus [g0, g0 + gn) cut into
+        WARM_BLOCKS blocks, block b into pieces at the cumulative fractions
+        cum[i] / Q; the cut at (b, i) is the first document starting at or
+        after g0 + gn (b Q + cum[i]) // (B Q); piece i of every block is part
+        i.  Returns part i's local document runs [(d0, d1), ...]."""
+        P, B, Q = len(cum) - 1, self.WARM_BLOCKS, SEQ_FRACTION_UNIT
+        g0, gn = corpus
         off = self.doc_off - self.doc_off[0]
         runs = [[] for _ in range(P)]
         prev = 0
-        for j in range(S):
-            nxt = self.D
-            if j + 1 < S:
-                d = int(np.searchsorted(off, g0 + gn * (j + 1) // S - self.token_base, side="left"))
-                nxt = min(max(d, prev), self.D)
-            if nxt > prev:
-                runs[j % P].append((prev, nxt))
-            prev = nxt
+        for b in range(B):
+            for i in range(P):
+                nxt = self.D
+                if b + 1 < B or i + 1 < P:
+                    d = int(np.searchsorted(off, g0 + gn * (b * Q + cum[i + 1]) // (B * Q) - self.token_base,
+                                            side="left"))
+                    nxt = min(max(d, prev), self.D)
+                if nxt > prev:
+                    runs[i].append((prev, nxt))
+                prev = nxt
         return runs
+
+    def _warm_runs(self):
+        return self._seq_runs(self._warm_cum, self._warm_corpus)
+
+    def _sweep_runs(self):
+        """The runs of the next sweep's sequential parts, or None (a plain sweep)."""
+        warm = getattr(self, "_warm", (1, 0))
+        if warm[0] > 1 and self.sweep_index < warm[1]:
+            return self._warm_runs()
+        cum = getattr(self, "_steady_cum", None)
+        if cum is not None and len(cum) > 2:
+            return self._seq_runs(cum, self._steady_corpus)
+        return None
 
     def sample(self, frozen=False):
         if self._pending:
             raise RuntimeError("sample with a pending delta: apply first (as lda_sample)")
-        warm = getattr(self, "_warm", (1, 0))
-        if not frozen and warm[0] > 1 and self.sweep_index < warm[1]:
-            runs = self._warm_runs()
-            for i in range(warm[0]):
-                for d0, d1 in runs[i]:
+        runs = None if frozen else self._sweep_runs()
+        if runs is not None:
+            for i, part in enumerate(runs):
+                for d0, d1 in part:
                     self.sample_docs(d0, d1)
-                if i + 1 < warm[0]:
+                if i + 1 < len(runs):
                     self.apply()
             self.end_sweep()
             return

@@ -171,3 +171,27 @@ def test_warm_start_parts_keep_every_shard_busy(lib):
         one = _warm_tokens(lib, doc_off, P, 0, 0, N)
         np.testing.assert_array_equal(tot, one)
         assert (abs(one - N / P) < 0.02 * N).all()
+
+
+def test_staleness_schedule_matches_mallet_threads(lib):
+    """lda_staleness_schedule (host-only): the sequential-sweep schedule whose
+    mean live fraction is that of Mallet's T worker threads, 1/(2T) -- two
+    parts, the first f of every block with f (1 - f) = 1/(2T) -- and the
+    oracle's restatement of it, fraction for fraction."""
+    import ctypes as C
+    import numpy as np
+    from oracle import oracle as O
+    for T in (1, 2, 3, 4, 8, 64):
+        n = C.c_int32()
+        fr = np.zeros(capi.MAX_EXCHANGE_PARTS, dtype=np.float64)
+        capi.check(lib.lda_staleness_schedule(T, C.byref(n), fr.ctypes.data), "lda_staleness_schedule")
+        parts, ofr = O.staleness_schedule(T)
+        assert n.value == parts and list(fr[:parts]) == ofr
+        live = sum(ofr[i] * sum(ofr[:i]) for i in range(parts))
+        if T > 1:
+            assert abs(live - 1 / (2 * T)) < 1e-12 and parts == 2
+        else:
+            assert parts == capi.MAX_EXCHANGE_PARTS and abs(live - 3 / 8) < 1e-12
+    # the quantised cuts are exact for equal parts
+    assert O.quantise_fractions([1 / 3] * 3) == O.equal_cum(3)
+    assert O.quantise_fractions([0.5, 0.5]) == O.equal_cum(2)

@@ -113,11 +113,11 @@ class WarmOracleEngine(OracleEngine):
     sweep_parts / sample_part protocol of a sequential sweep."""
 
     def sweep_parts(self):
-        P, S = self.s._warm
-        return (P, True) if P > 1 and self.s.sweep_index < S else (1, False)
+        runs = self.s._sweep_runs()
+        return (len(runs), True) if runs is not None else (1, False)
 
     def sample_part(self, i):
-        runs = self.s._warm_runs()
+        runs = self.s._sweep_runs()
         for d0, d1 in runs[i]:
             self.s.sample_docs(d0, d1)
         if i + 1 == len(runs):
@@ -142,8 +142,10 @@ def _worker(rank, world, port, outdir, parts=1, compact=True):
     c = _corpus()
     sh = shard_corpus(c.doc_off, c.words, world, rank)
     o = O.ExactSampler(K, c.num_types, sh.doc_off, sh.words, 0.1, 0.01, SEED, token_base=sh.token_base)
-    if parts == "warm":
+    if parts in ("warm", "steady"):
         o.set_warm_start(*WARM, 0, c.num_tokens)        # parts cut in the whole corpus
+        if parts == "steady":                           # + Mallet-staleness sweeps after it
+            o.set_sequential_sweeps(*O.staleness_schedule(4), 0, c.num_tokens)
         tr = ADLDATrainer(WarmOracleEngine(o), compact=compact)
     else:
         tr = ADLDATrainer(OracleEngine(o) if parts == 1 else SplitOracleEngine(o, parts),
@@ -169,7 +171,8 @@ def _free_port():
 
 
 @pytest.mark.parametrize("world,parts,compact", [(2, 1, True), (3, 1, True), (2, 3, True), (3, 2, True),
-                                                 (2, "warm", True), (3, "warm", True), (2, 1, False),
+                                                 (2, "warm", True), (3, "warm", True), (3, "steady", True),
+                                                 (2, "steady", False), (2, 1, False),
                                                  (3, 2, False)])
 def test_gloo_adlda_matches_single(oracle, world, parts, compact):
     """parts > 1: split sweeps, every part's all-reduce overlapping the next
@@ -184,8 +187,10 @@ def test_gloo_adlda_matches_single(oracle, world, parts, compact):
         res = [np.load(os.path.join(d, f"r{r}.npz")) for r in range(world)]
     c = _corpus()
     single = oracle.ExactSampler(K, c.num_types, c.doc_off, c.words, 0.1, 0.01, SEED)
-    if parts == "warm":
+    if parts in ("warm", "steady"):
         single.set_warm_start(*WARM)
+    if parts == "steady":
+        single.set_sequential_sweeps(*oracle.staleness_schedule(4))
     single.sweep(SWEEPS)
     np.testing.assert_array_equal(np.concatenate([r["z"] for r in res]), single.z())
     nw, nwsum, _, _ = single.counts()

@@ -71,12 +71,15 @@ def _run(K, V, corpus, z, alpha, hyper, sweep, options, seed):
 
 
 def _oracle_schedule(oracle, corpus, V, K, z0, alpha, alpha_sum, beta, seed, sweep0, iters,
-                     interval, burnin, save, symmetric=False, kind="dense"):
+                     interval, burnin, save, symmetric=False, kind="dense", threads=1):
     """Mallet's estimate() over cpu_exact from a given state (the test-side
-    restatement: sweeps, statistics, optimizeAlpha / optimizeBeta, LL/10)."""
+    restatement: sweeps, statistics, optimizeAlpha / optimizeBeta, LL/10).
+    threads: the options' numThreads, whose staleness the sweeps past the
+    warm start emulate (lda_staleness_schedule)."""
     o = oracle.ExactSampler(K, V, corpus.doc_off, corpus.words, alpha, beta, seed, z_init=z0,
                             kind=kind)
     o.set_warm_start(4, 50)       # the native model's default warm start, keyed by the sweep counter
+    o.set_sequential_sweeps(*oracle.staleness_schedule(threads))
     o.sweep_index = sweep0
     lens = np.diff(corpus.doc_off)
     L = int(lens.max())
@@ -152,7 +155,7 @@ def test_estimate_then_update_model(oracle):
     opts = [iters, burnin, interval, save, 0, 4, 0]             # numThreads 4 -> the GPUs here
     out1 = _run(K, V1, first, z0, alpha0, hyper0, 0, opts, seed)
     o, alpha, alpha_sum, beta, ll = _oracle_schedule(oracle, first, V1, K, z0, alpha0, 8.0, 0.05,
-                                                     seed, 0, iters, interval, burnin, save)
+                                                     seed, 0, iters, interval, burnin, save, threads=4)
     _check(out1, o, alpha, alpha_sum, beta, ll, K, V1, iters)
     assert out1["sweep"] == iters
     assert not np.allclose(alpha, alpha0) and beta != 0.05
@@ -171,7 +174,7 @@ def test_estimate_then_update_model(oracle):
                                                  out1["hyper"][1] * V2], out1["sweep"], opts2, seed)
     o2, alpha2, alpha_sum2, beta2, ll2 = _oracle_schedule(
         oracle, both, V2, K, z1, out1["alpha"], out1["hyper"][0], out1["hyper"][1], seed,
-        iters, iters2, interval, burnin, save)
+        iters, iters2, interval, burnin, save, threads=4)
     _check(out2, o2, alpha2, alpha_sum2, beta2, ll2, K, V2, iters2)
     assert out2["sweep"] == iters + iters2
     # without the carried counter the second estimate() would replay sweep 0's uniforms
@@ -221,7 +224,7 @@ def test_checkpoint_resume_equals_uninterrupted(oracle):
     np.testing.assert_array_equal(resumed["rows"], whole["rows"])
     np.testing.assert_array_equal(resumed["tpt"], whole["tpt"])
     assert resumed["sweep"] == whole["sweep"] == 40
-    o, *_ = _oracle_schedule(oracle, c, V, K, z0, alpha0, 6.0, 0.02, seed, 0, 40, 0, 200, 10)
+    o, *_ = _oracle_schedule(oracle, c, V, K, z0, alpha0, 6.0, 0.02, seed, 0, 40, 0, 200, 10, threads=2)
     np.testing.assert_array_equal(whole["z"], o.z())
 
 
@@ -243,13 +246,13 @@ def test_estimate_ending_between_statistics_and_optimisation(oracle):
     iters, interval, burnin, save = 35, 10, 10, 5
     out1 = _run(K, V, c, z0, alpha0, hyper0, 0, [iters, burnin, interval, save, 0, 2, 0], seed)
     o, alpha, alpha_sum, beta, ll = _oracle_schedule(oracle, c, V, K, z0, alpha0, 8.0, 0.05, seed, 0,
-                                                     iters, interval, burnin, save)
+                                                     iters, interval, burnin, save, threads=2)
     _check(out1, o, alpha, alpha_sum, beta, ll, K, V, iters)
     iters2 = 20
     out2 = _run(K, V, c, out1["z"], out1["alpha"], out1["hyper"], out1["sweep"],
                 [iters2, burnin, interval, save, 0, 2, 0], seed)
     o2, alpha2, alpha_sum2, beta2, ll2 = _oracle_schedule(
         oracle, c, V, K, out1["z"], out1["alpha"], out1["hyper"][0], out1["hyper"][1], seed,
-        iters, iters2, interval, burnin, save)
+        iters, iters2, interval, burnin, save, threads=2)
     _check(out2, o2, alpha2, alpha_sum2, beta2, ll2, K, V, iters2)
     assert out2["sweep"] == iters + iters2

@@ -34,6 +34,7 @@ def _oracle_estimate(oracle, corpus, K, alpha_sum, beta, seed, iters, interval, 
     alpha = np.full(K, alpha_sum / K)
     o = oracle.ExactSampler(K, V, corpus.doc_off, corpus.words, alpha, beta, seed)
     o.set_warm_start(*WARM)               # the model's default warm start
+    o.set_sequential_sweeps(*oracle.staleness_schedule(1))   # numThreads 1: sequential Mallet's staleness
     lens = np.diff(corpus.doc_off)
     L = int(lens.max())
     dl = np.zeros(L + 1, np.int32)
@@ -75,6 +76,7 @@ def test_estimate_plain_equals_sampler(oracle):
     m.estimate()
     o = oracle.ExactSampler(20, c.num_types, c.doc_off, c.words, np.full(20, 0.5), 0.01, 7)
     o.set_warm_start(*WARM)
+    o.set_sequential_sweeps(*oracle.staleness_schedule(1))
     o.sweep(12)
     np.testing.assert_array_equal(m.topicAssignments(), o.z())
     nw, nwsum = m.typeTopicCounts()
@@ -202,6 +204,7 @@ def test_inferencer_matches_sampler_inference():
     m.estimate()
     g = GibbsSampler(32, c.num_types, train.doc_off, train.words, np.full(32, 0.1), 0.01, seed=9)
     g.set_warm_start(*WARM)
+    g.set_sequential_sweeps(4)            # the model's numThreads 1: 4 equal sequential parts
     g.sweep(15)
     np.testing.assert_array_equal(g.z(), m.topicAssignments())
     inf = m.getInferencer()
@@ -278,3 +281,36 @@ def test_num_threads_at_reference_scale_uses_one_gpu():
     c = synthetic_changelists(num_docs=2000, num_types=5000, seed=20261015)
     m, _ = _model(c, 500, 100.0, 1.0, 1, setNumThreads=4, setNumIterations=1)
     assert m.numShards() == 1
+
+
+@pytest.mark.parametrize("kind,K,threads", [("dense", 20, 4), ("dense", 100, 3), ("dense", 500, 4),
+                                            ("dense", 500, 1), ("sparse", 1500, 4)])
+def test_staleness_sweeps_bit_exact(oracle, kind, K, threads):
+    """lda_set_sequential_sweeps with lda_staleness_schedule(T):
+    after a warm start, every sweep in the sequential parts that give Mallet's
+    mean live fraction 1/(2T) -- unequal pieces of every block for T > 1 --
+    bit-exact against cpu_exact's same schedule, through lda_sweep (which
+    runs them one part at a time) and lda_sample."""
+    from ldagibbssampling_amd.sampler import GibbsSampler
+    c = synthetic_lda(num_docs=300, num_types=800, num_topics=min(K, 40), doc_len=None, mean_len=50,
+                      min_len=0, max_len=180, seed=K + threads)
+    alpha = np.full(K, 20.0 / K)
+    parts, fr = oracle.staleness_schedule(threads)
+    g = GibbsSampler(K, c.num_types, c.doc_off, c.words, alpha, 0.02, seed=5, sampler=kind,
+                     tokens_per_range=64)
+    g.set_warm_start(3, 4)
+    g.set_sequential_sweeps(parts, fr)
+    assert g.sequential_sweeps() == (parts, oracle.quantise_fractions(fr))
+    o = oracle.ExactSampler(K, c.num_types, c.doc_off, c.words, alpha, 0.02, 5, kind=kind)
+    o.set_warm_start(3, 4)
+    o.set_sequential_sweeps(parts, fr)
+    g.sweep(7)
+    o.sweep(7)
+    np.testing.assert_array_equal(g.z(), o.z())
+    g.sample()
+    g.apply()
+    o.sweep(1)
+    np.testing.assert_array_equal(g.z(), o.z())
+    for a, b in zip(g.counts()[:2], o.counts()[:2]):
+        np.testing.assert_array_equal(a, b)
+    g.close()

@@ -36,7 +36,29 @@ def run(args):
     alpha = np.full(K, alpha_sum / K)
     o = oracle.ExactSampler(K, V, train.doc_off, train.words, alpha, beta, seed,
                             half=2 if K <= 128 else 0)
-    o.set_warm_start(4, 50) if parts == 1 else o.set_warm_start(parts, 1000)
+    if isinstance(parts, tuple):
+        # two sequential parts of unequal size: part 0 takes the first
+        # fraction f of each of the 64 blocks (the warm start's layout)
+        f = parts[1]
+        o.set_warm_start(2, 1000)
+        off = o.doc_off - o.doc_off[0]
+        N = int(off[-1])
+
+        def runs():
+            r = [[], []]
+            prev = 0
+            for b in range(64):
+                for i, frac in enumerate((f, 1.0)):
+                    tgt = int(N * (b + frac) / 64)
+                    nxt = o.D if (b == 63 and i == 1) else int(np.searchsorted(off, tgt, side="left"))
+                    nxt = min(max(nxt, prev), o.D)
+                    if nxt > prev:
+                        r[i].append((prev, nxt))
+                    prev = nxt
+            return r
+        o._warm_runs = runs
+    else:
+        o.set_warm_start(4, 50) if parts == 1 else o.set_warm_start(parts, 1000)
     lens = np.diff(train.doc_off)
     L = int(lens.max())
     dl = np.zeros(L + 1, np.int32)
@@ -68,7 +90,9 @@ def run(args):
 
 
 def main():
-    K, asum, beta, parts = int(sys.argv[1]), float(sys.argv[2]), float(sys.argv[3]), int(sys.argv[4])
+    K, asum, beta = int(sys.argv[1]), float(sys.argv[2]), float(sys.argv[3])
+    # parts: "P" (P equal sequential parts) or "2:f" (two parts, the first a fraction f)
+    parts = (2, float(sys.argv[4][2:])) if sys.argv[4].startswith("2:") else int(sys.argv[4])
     s0, s1 = int(sys.argv[5]), int(sys.argv[6])
     jobs = int(sys.argv[7]) if len(sys.argv) > 7 else 8
     out = {"K": K, "alpha_sum": asum, "beta": beta, "parts": parts, "seeds": [], "perplexity": [],
