@@ -375,8 +375,11 @@ struct lda_ctx {
     const void* range_doc = nullptr;
     int64_t R = -1;
     hipStream_t stream = nullptr;
+    const void* seq = nullptr;         // steady sequential sweeps: their ranges (else null)
+    int seq_parts = 0;
     bool operator==(const GraphKey& o) const {
-      return range_doc == o.range_doc && R == o.R && stream == o.stream;
+      return range_doc == o.range_doc && R == o.R && stream == o.stream && seq == o.seq &&
+             seq_parts == o.seq_parts;
     }
   } graph_key;
   // event pairs around the last LDA_TIME_RING sampler launches (lda_sample_times)
@@ -1432,17 +1435,26 @@ lda_status lda_delta_buffer(lda_ctx* c, void** dev_ptr, size_t* count) {
 
 // Can the next sweep run inside a graph?  A plain dense sweep: one part, not
 // a warm-start or recount sweep (and once one is, every later one is).
+// Steady sequential sweeps (lda_set_sequential_sweeps) qualify too: their
+// parts go into the graph one after the other, each followed by its apply.
 static bool graph_eligible(const lda_ctx* c) {
   return c->use_graphs && c->sampler == LDA_SAMPLER_DENSE && c->parts == 1 && c->R > 0 && !c->pending &&
-         c->next_part == 0 && !next_sweep_sequential(c) && !next_sweep_recounts(c);
+         c->next_part == 0 && next_sweep_kind(c) != 1 && !next_sweep_recounts(c);
 }
 
-// k x (sampler, apply) captured on the context's stream and instantiated once
+// k sweeps captured on the context's stream and instantiated once: k x
+// (sampler, apply), or for steady sequential sweeps k x parts x (sampler
+// over the part's ranges, apply), where only a sweep's last apply advances
+// the device sweep counter and every part takes work-queue counter 0 (the
+// apply before it zeroed it)
 static lda_status sweep_graph(lda_ctx* c, int k, hipGraphExec_t* out) {
+  const bool seq = next_sweep_kind(c) == 2;
   lda_ctx::GraphKey key;
   key.range_doc = c->range_doc;
   key.R = c->R;
   key.stream = c->stream;
+  key.seq = seq ? c->steady.range_doc : nullptr;
+  key.seq_parts = seq ? c->steady.parts : 0;
   if (!(key == c->graph_key)) {
     // a graph launched earlier (perhaps on another stream: lda_set_stream does
     // not synchronize) may still run; it finishes before it is destroyed
@@ -1461,14 +1473,33 @@ static lda_status sweep_graph(lda_ctx* c, int k, hipGraphExec_t* out) {
     p.delta = c->delta;
     p.dsum = c->delta + (int64_t)c->V * c->Kp;
     const int64_t wpb = c->waves_per_block;
-    const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>(c->sample_blocks, (c->R + wpb - 1) / wpb));
+    auto blocks_for = [&](int64_t R) {
+      return (int)std::max<int64_t>(1, std::min<int64_t>(c->sample_blocks, (R + wpb - 1) / wpb));
+    };
     lda::TopicTables t{c->nwsum, c->alpha_d, c->alpha_f, c->inv, c->inv_m1, 0.0f, c->K, c->queue, 0,
-                       c->state_dev};
+                       c->state_dev, 1};
+    lda::TopicTables t_part = t;
+    t_part.advance = 0;
     HIP_TRY(hipStreamBeginCapture(c->stream, hipStreamCaptureModeRelaxed));
     hipError_t e = hipSuccess;
     for (int i = 0; i < k && e == hipSuccess; ++i) {
-      e = lda::launch_sample(c->C, false, p, blocks, c->stream, c->half);
-      if (e == hipSuccess) e = lda::launch_apply_packed(c->nw, c->delta, c->V, c->Kp, c->nw16, c->wide, t, c->stream);
+      if (!seq) {
+        e = lda::launch_sample(c->C, false, p, blocks_for(c->R), c->stream, c->half);
+        if (e == hipSuccess) e = lda::launch_apply_packed(c->nw, c->delta, c->V, c->Kp, c->nw16, c->wide, t, c->stream);
+        continue;
+      }
+      for (int part = 0; part < c->steady.parts && e == hipSuccess; ++part) {
+        const int64_t r0 = c->steady.part_range[(size_t)part], r1 = c->steady.part_range[(size_t)part + 1];
+        lda::SampleParams pp = p;
+        pp.range_doc = c->steady.range_doc + r0;
+        pp.range_end = c->steady.range_end + r0;
+        pp.num_ranges = r1 - r0;
+        if (r1 > r0) e = lda::launch_sample(c->C, false, pp, blocks_for(r1 - r0), c->stream, c->half);
+        const bool last = part + 1 == c->steady.parts;
+        if (e == hipSuccess)
+          e = lda::launch_apply_packed(c->nw, c->delta, c->V, c->Kp, c->nw16, c->wide, last ? t : t_part,
+                                       c->stream);
+      }
     }
     hipGraph_t g = nullptr;
     const hipError_t e2 = hipStreamEndCapture(c->stream, &g);

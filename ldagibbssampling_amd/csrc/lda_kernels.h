@@ -127,6 +127,7 @@ struct TopicTables {
   int32_t* queue;           // work-queue counter zeroed for the next sample (nullable)
   int32_t absolute;         // 1: the buffer holds recounted counts that replace nw / nwsum
   uint32_t* state_dev;      // graph-launched sweeps: [0] advanced by one, [2] vbeta's fp32 bits read in place of vbeta
+  int32_t advance;          // with state_dev: 1 = this apply ends a sweep (advance [0]); 0 = a part's apply inside one
 };
 // dense sampler's apply: nw += delta, delta = 0, 16-bit rows + wide flags,
 // nwsum/tables (k_apply + k_build_packed + k_prepare_topics in one launch)

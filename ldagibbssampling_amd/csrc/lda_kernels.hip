@@ -2764,7 +2764,7 @@ __global__ __launch_bounds__(256) void k_apply_packed(int32_t* __restrict__ nw, 
       }
     }
     if (threadIdx.x == 0 && t.queue) *t.queue = 0;
-    if (threadIdx.x == 0 && t.state_dev) t.state_dev[0] += 1u;   // the next graph sweep's counter
+    if (threadIdx.x == 0 && t.state_dev && t.advance) t.state_dev[0] += 1u;   // the next graph sweep's counter
   }
   for (int64_t w = (int64_t)blockIdx.x * 4 + wid; w < V; w += (int64_t)gridDim.x * 4) {
     int32_t c[C], d[C];

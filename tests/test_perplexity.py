@@ -23,8 +23,11 @@ same estimator and the GPU default kernel's inference draw).  Bars, each
 against cpu_mallet (profiles/r03/ppl/ has the per-seed evidence and
 bootstrap CIs, tools/ppl_stats.py):
   1. mean over the 96 seeds within 1% (north_star's tolerance);
-  2. median within 0.5%: a +1% shift of the typical (untrapped) chain fails
-     this bar with certainty (the median's bootstrap CI is ~+-0.1%);
+  2. median not worse by more than 0.5% (and not better by more than 1%): a
+     +1% shift of the typical (untrapped) chain fails this bar with
+     certainty (the median's bootstrap CI is ~+-0.1%); a sampler that mixes
+     better than the reference is not a parity failure, so the bar is
+     one-sided at 0.5% and two-sided only at north_star's 1%;
   3. trapped-seed rate (perplexity > 1.02 x the pooled median) not larger
      than cpu_mallet's at one-sided Fisher p < 0.01: a mean shift carried by
      more trapped seeds is caught here or by bar 1.
@@ -110,7 +113,7 @@ def test_heldout_perplexity_within_1pct(oracle, K):
           f"cpu_mallet mean {pm.mean():.3f} median {np.median(pm):.3f} trapped {b}/{len(pm)} | "
           f"mean {dmean:+.3%} median {dmed:+.3%} Fisher p {p:.3f}")
     assert abs(dmean) <= 0.01
-    assert abs(dmed) <= 0.005
+    assert -0.01 <= dmed <= 0.005
     assert p >= 0.01
 
 
@@ -131,11 +134,13 @@ REF_SEEDS = range(1, 49)
 # alphaSum and beta within 3% of cpu_mallet's mean.  Both learn them from
 # their own chains with the same Minka fixed points (lda_dirichlet.cpp /
 # oracle, identical fp64 code on identical histograms, test_hyper.py), so a
-# difference in the means is a difference in the chains' statistics; the
-# seed-to-seed spread of each is ~0.3-1% (the fixtures), so 3% is several
-# standard errors of a 48-seed mean, yet a sampler that over- or
-# under-disperses topics moves alphaSum by far more (K = 500 starts at 100
-# and learns ~4.5).
+# difference in the means is a difference in the chains' statistics: the
+# seed-to-seed spread is ~0.2% (alphaSum) and ~1.5% (beta), so the means
+# of 48 seeds carry ~0.05% / ~0.3% of noise and 3% is many standard errors;
+# yet the staleness of the sweep moves them by more: snapshot sweeps learned
+# beta +8..10% and alphaSum -3.7%, two equal sequential parts beta -9% and
+# alphaSum +3%, the emulation of Mallet's 4 threads within ~0.6%
+# (profiles/r04/hyper/).
 HYPER_TOL = 0.03
 
 
@@ -155,7 +160,11 @@ def test_heldout_perplexity_reference_settings(oracle, K, alpha_sum, beta):
     """The reference's own training configuration -- the one the Java drop-in
     (GpuParallelTopicModel) runs: hyperparameter optimisation on
     (setOptimizeInterval(20), Mallet's default burn-in 200), setNumThreads(4),
-    1000 sweeps, the native ParallelTopicModel's default warm start.  48
+    1000 sweeps, the native ParallelTopicModel's default sweep schedule (the
+    warm start, then sweeps with the staleness of Mallet's 4 worker threads,
+    lda_staleness_schedule: without it the model learned beta ~9% higher and
+    alphaSum ~4% lower than cpu_mallet, and at K = 500 trapped 8 of 48
+    chains).  48
     seeds of the native ParallelTopicModel on the GPU against the committed
     48-seed cpu_mallet fixture (tests/golden/mallet_ppl_ref_k{K}.json,
     tools/ppl_mallet_ref_seeds.py); each model is scored with its own learned
@@ -200,6 +209,6 @@ def test_heldout_perplexity_reference_settings(oracle, K, alpha_sum, beta):
     print("GPU_PER_SEED " + json.dumps({"K": K, "perplexity": pg, "alpha_sum_learned": asum,
                                          "beta_learned": bet}))
     assert abs(dmean) <= 0.01
-    assert abs(dmed) <= 0.005
+    assert -0.01 <= dmed <= 0.005
     assert p >= 0.01
     assert abs(da) <= HYPER_TOL and abs(db) <= HYPER_TOL
