@@ -12,7 +12,7 @@ export TMPDIR=/tmp
 for spec in "$@"; do
   set -- $spec
   L=$1; KN=$2; TOK=$3; K=$4; BI=$5; shift 5
-  KN=${KN//_/ }
+  KN=${KN//\~/ }
   BURNIN=$BI PASSES="kt fetch write sq lds grbm" LABEL=$L BENCH_ARGS="$*" bash tools/profile.sh > $O/profile_$L.log 2>&1 || { echo "PROFILE $L FAILED"; tail -20 $O/profile_$L.log; exit 1; }
   mkdir -p $O/prof_$L && cp gpurun_out/prof_$L/summary_*.json $O/prof_$L/ && cp gpurun_out/prof_$L/*kernel_stats.csv $O/prof_$L/ 2>/dev/null
   python3 tools/make_traffic.py gpurun_out/prof_$L "$KN" $TOK "$L" $O/traffic_$L.json $K $BI > /dev/null || { echo "TRAFFIC $L FAILED"; exit 1; }
