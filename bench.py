@@ -233,8 +233,9 @@ def estimate_side_figure(device: int, iters: int = 100, burnin: int = 50):
     ParallelTopicModel (liblda_topic_model.so, the host mirror the JNI shim
     drives) running estimate() on the C4 shard (block 0 of the C4 corpus:
     1.25M docs x 200 tokens, V = 100k, K = 512, alphaSum 51.2, beta 0.01)
-    with its defaults -- the 4 x 50 warm start (sweeps 0..49 in 4 sequential
-    parts), LL/token every 10 iterations -- and setOptimizeInterval(20) with
+    with the reference's setNumThreads(4) (its staleness schedule, one GPU
+    shard) and its defaults -- the 4 x 50 warm start (sweeps 0..49 in 4
+    sequential parts), LL/token every 10 iterations -- and setOptimizeInterval(20) with
     burn-in `burnin` (Mallet's default 200 would put no optimisation inside
     100 iterations; 50 gives 3: iterations 60, 80, 100).  Timed: the
     estimate() call of `iters` iterations, after an estimate() of 0
@@ -258,6 +259,9 @@ def estimate_side_figure(device: int, iters: int = 100, burnin: int = 50):
         _check(L.ldatm_set_topic_display(h, 0, 0), "ldatm_set_topic_display")
         _check(L.ldatm_set_optimize_interval(h, 20), "ldatm_set_optimize_interval")
         _check(L.ldatm_set_burnin_period(h, burnin), "ldatm_set_burnin_period")
+        # the reference's setNumThreads(4) (src/cmu_ron/TrainAndPredict.java:164):
+        # its staleness schedule; the shard stays on this one GPU
+        _check(L.ldatm_set_num_threads(h, 4), "ldatm_set_num_threads")
         _check(L.ldatm_set_devices(h, 1, (C.c_int32 * 1)(device)), "ldatm_set_devices")
         _check(L.ldatm_set_num_iterations(h, 0), "ldatm_set_num_iterations")
         t0 = time.perf_counter()
@@ -281,7 +285,8 @@ def estimate_side_figure(device: int, iters: int = 100, burnin: int = 50):
         "tokens": n,
         "shard_build_s": t_build,
         "workload": "C4 shard (block 0 of C4: 1.25M docs x 200 tok, V=100k, K=512), one GPU",
-        "settings": (f"native ParallelTopicModel.estimate(): warm start 4 x 50 (default), LL/token "
+        "settings": (f"native ParallelTopicModel.estimate(): setNumThreads(4) (one GPU shard; "
+                     f"sweeps with 4 threads' staleness), warm start 4 x 50 (default), LL/token "
                      f"every 10, setOptimizeInterval(20), setBurninPeriod({burnin}) -> "
                      f"{len([i for i in range(1, iters + 1) if i > burnin and i % 20 == 0])} "
                      f"optimisations"),
