@@ -1875,6 +1875,11 @@ __global__ __launch_bounds__(256) void k_sample_sparse(SampleParams p) {
 #ifndef SB_TGKEY
 #define SB_TGKEY 1
 #endif
+// group-sum updates as one select under a scalar lane mask, the group by a
+// uniform switch (A/B: NG <= 4)
+#ifndef SB_TGMASK
+#define SB_TGMASK 0
+#endif
 // word-row loads as buffer loads bounded by the row (a load past it returns
 // 0 without a memory access): the ring prefetch is issued for every token
 // slot without a per-round branch, so every path round the loop issues the
@@ -1993,7 +1998,24 @@ __global__ __launch_bounds__(64 * sb_waves<C>()) void k_sample_sparse_big(Sample
   // the lane's NG group sums as one register vector: a wave-uniform group
   // index becomes an indexed register move (an array was placed in scratch)
   typedef float tg_t __attribute__((ext_vector_type(NG)));
-#if SB_TGKEY
+#if SB_TGMASK
+  // lane `owner` writes group g: the lane as a scalar mask (s_lshl_b64, an
+  // inverse ballot) and the uniform g as a uniform switch, so one update is
+  // one VALU select (the keyed form is NG compares + NG selects; the scalar
+  // unit has the headroom since v8.4 moved work off it)
+  auto set_tg = [&](tg_t& TG, int owner, int g, float v) {
+    const bool me = __builtin_amdgcn_inverse_ballot_w64(1ull << (uint32_t)owner);
+    switch (uniform_i(g)) {
+      default:
+        break;
+      case 0: TG[0] = me ? v : TG[0]; break;
+      case 1: if (NG > 1) TG[1 % NG] = me ? v : TG[1 % NG]; break;
+      case 2: if (NG > 2) TG[2 % NG] = me ? v : TG[2 % NG]; break;
+      case 3: if (NG > 3) TG[3 % NG] = me ? v : TG[3 % NG]; break;
+    }
+  };
+  [[maybe_unused]] auto tg_at = [&](const tg_t& TG, int owner, int g) -> float { return readlane_f(TG[g], owner); };
+#elif SB_TGKEY
   // lane*NG + q per element; the asm keeps them opaque VGPRs, so the
   // compare against a uniform key stays one VALU compare per element
   int tkey[NG];
