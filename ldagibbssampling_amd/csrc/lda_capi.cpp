@@ -245,6 +245,17 @@ struct lda_ctx {
   int64_t* row_off = nullptr;
   int32_t* row_nnz = nullptr;
   uint32_t* row_rnd = nullptr;   // row_off / 64: the large-K sampler's 32-bit row starts
+  // the large-K sampler's ring depth (register rounds): SB_RB_SHORT_ROUNDS
+  // while the rows' token-weighted mean rounds (from the last apply's
+  // k_build_sparse, read back without a wait) are at most big_rb_switch, the
+  // default depth otherwise; LDA_SB_RB=<n> at lda_create fixes it (A/B)
+  bool big_rb_auto = true;
+  int big_rb = 0;
+  double big_rb_switch = 8.0;
+  unsigned long long* big_stats = nullptr;
+  unsigned long long* big_stats_pin = nullptr;
+  hipEvent_t big_stats_ev = nullptr;
+  bool big_stats_live = false;
   bool rows_ready = false;
   int half = 0;    // dense K <= 128: 1 = the half-wave variant, 2 = the quarter-wave one (LDA_DENSE_HALF)
   // lda_infer: word totals of the snapshot (TopicInferencer's empty-row test),
@@ -416,6 +427,9 @@ struct lda_ctx {
     for (auto& g : graphs)
       if (g) (void)hipGraphExecDestroy(g);
     if (graph_ev) (void)hipEventDestroy(graph_ev);
+    if (big_stats) (void)hipFree(big_stats);
+    if (big_stats_pin) (void)hipHostFree(big_stats_pin);
+    if (big_stats_ev) (void)hipEventDestroy(big_stats_ev);
     if (switch_ev) (void)hipEventDestroy(switch_ev);
     if (state_dev) (void)hipFree(state_dev);
     if (zw) (void)hipFree(zw);
@@ -591,7 +605,29 @@ static lda_status apply_impl(lda_ctx* c) {
       lda_status s = build_row_capacity(c);
       if (s) return s;
     }
-    HIP_TRY(lda::launch_build_sparse(c->nw, c->V, c->Kp, c->row_off, c->ent, c->row_nnz, c->stream));
+    // the large-K sampler's ring depth for the next sweep: the rows'
+    // token-weighted mean rounds, copied back without a wait (the choice
+    // reads the copy of an earlier apply once it has landed)
+    const bool stats = c->C >= 32 && c->big_rb_auto;
+    if (stats) {
+      if (!c->big_stats) {
+        HIP_TRY(dalloc(&c->big_stats, 2));
+        HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&c->big_stats_pin), 2 * sizeof(unsigned long long)));
+        HIP_TRY(hipEventCreateWithFlags(&c->big_stats_ev, hipEventDisableTiming));
+      }
+      if (!c->big_stats_live) {
+        HIP_TRY(hipMemsetAsync(c->big_stats, 0, 2 * sizeof(unsigned long long), c->stream));
+      }
+    }
+    const bool take = stats && !c->big_stats_live;
+    HIP_TRY(lda::launch_build_sparse(c->nw, c->V, c->Kp, c->row_off, c->ent, c->row_nnz, c->stream,
+                                     take ? c->big_stats : nullptr));
+    if (take) {
+      HIP_TRY(hipMemcpyAsync(c->big_stats_pin, c->big_stats, 2 * sizeof(unsigned long long),
+                             hipMemcpyDeviceToHost, c->stream));
+      HIP_TRY(hipEventRecord(c->big_stats_ev, c->stream));
+      c->big_stats_live = true;
+    }
   } else {
     HIP_TRY(lda::launch_build_packed(c->nw, c->V, c->Kp, c->nw16, c->wide, c->stream));
   }
@@ -799,6 +835,11 @@ lda_status lda_create(lda_ctx** out, const lda_config* cfg, const int64_t* doc_o
   {
     const char* gv = std::getenv("LDA_GRAPHS");
     c->use_graphs = !(gv && gv[0] == '0');
+    const char* rbv = std::getenv("LDA_SB_RB");
+    if (rbv && rbv[0]) {
+      c->big_rb_auto = false;
+      c->big_rb = std::atoi(rbv) == lda::SB_RB_SHORT_ROUNDS ? lda::SB_RB_SHORT_ROUNDS : 0;
+    }
     const char* zv = std::getenv("LDA_ZW");
     c->use_zw = !(zv && zv[0] == '0');
   }
@@ -917,6 +958,12 @@ static lda_status sample_part_impl(lda_ctx* c, int part) {
   if (part == 0) {
     c->sweep_kind = next_sweep_kind(c);
     c->sweep_seq = c->sweep_kind != 0;
+    if (c->big_stats_live && hipEventQuery(c->big_stats_ev) == hipSuccess) {
+      const unsigned long long* h = c->big_stats_pin;
+      const double mean_rounds = h[1] ? (double)h[0] / (double)h[1] : 0.0;
+      c->big_rb = mean_rounds <= c->big_rb_switch ? lda::SB_RB_SHORT_ROUNDS : 0;
+      c->big_stats_live = false;
+    }
     c->sweep_recount = next_sweep_recounts(c);
     if (c->sweep_recount && !c->perm && c->N > 0) {
       lda_status s = build_recount_index(c);
@@ -963,7 +1010,7 @@ static lda_status sample_part_impl(lda_ctx* c, int part) {
     const int slot = (int)(c->launches % lda_ctx::LDA_TIME_RING);
     HIP_TRY(hipEventRecord(c->ev0[slot], c->stream));
     if (c->sampler == LDA_SAMPLER_SPARSE)
-      HIP_TRY(lda::launch_sample_sparse(c->C, false, p, blocks, c->stream));
+      HIP_TRY(lda::launch_sample_sparse(c->C, false, p, blocks, c->stream, c->big_rb));
     else
       HIP_TRY(lda::launch_sample(c->C, false, p, blocks, c->stream, c->half));
     HIP_TRY(hipEventRecord(c->ev1[slot], c->stream));

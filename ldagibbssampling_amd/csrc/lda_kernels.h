@@ -106,13 +106,17 @@ hipError_t launch_sample(int C, bool frozen, const SampleParams& p, int blocks, 
 int sample_blocks_per_cu(int C, bool frozen, int K, int half = 0);
 int half_topics_per_lane(int K);
 int quarter_topics_per_lane(int K);
+// rb: register rounds of the large-K sampler (C >= 32): SB_RB_SHORT_ROUNDS
+// for short rows, anything else the default depth
 hipError_t launch_sample_sparse(int C, bool frozen, const SampleParams& p, int blocks,
-                                hipStream_t st);
+                                hipStream_t st, int rb = 0);
+constexpr int SB_RB_SHORT_ROUNDS = 8;   // == SB_RB_SHORT in lda_kernels.hip
 int sample_sparse_blocks_per_cu(int C, bool frozen);
 // row totals of nw (saturating at Kp) -> host prefix -> capacity offsets
 hipError_t launch_row_caps(const int32_t* nw, int64_t V, int32_t Kp, int32_t* caps, hipStream_t st);
 hipError_t launch_build_sparse(const int32_t* nw, int64_t V, int32_t Kp, const int64_t* row_off,
-                               uint32_t* ent, int32_t* row_nnz, hipStream_t st);
+                               uint32_t* ent, int32_t* row_nnz, hipStream_t st,
+                               unsigned long long* stats = nullptr);
 hipError_t launch_build_packed(const int32_t* nw, int64_t V, int32_t Kp, uint16_t* nw16,
                                uint8_t* wide, hipStream_t st);
 // per-topic state refreshed by an apply (k_prepare_topics' arguments)

@@ -1843,6 +1843,13 @@ __global__ __launch_bounds__(256) void k_sample_sparse(SampleParams p) {
 #ifndef SB_RB
 #define SB_RB 10
 #endif
+// the ring's depth for short rows (round 4: after burn-in a C5 row is ~4-5
+// rounds; 8 register rounds were +2% there and -3% on the ~11-round rows
+// near init, so the launch picks by the rows' token-weighted mean rounds)
+#ifndef SB_RB_SHORT
+#define SB_RB_SHORT 8
+#endif
+static_assert(SB_RB_SHORT == SB_RB_SHORT_ROUNDS, "lda_kernels.h names the short depth");
 #ifndef SB_BATCH
 #define SB_BATCH 4
 #endif
@@ -1938,7 +1945,7 @@ __device__ __forceinline__ float row_scan16(float x) {
   return x;
 }
 
-template <int C, int NS, bool FROZEN>
+template <int C, int NS, int RB, bool FROZEN>
 __global__ __launch_bounds__(64 * sb_waves<C>()) void k_sample_sparse_big(SampleParams p) {
   extern __shared__ __attribute__((aligned(16))) int32_t smem[];
   constexpr int KP = C * 64;
@@ -2142,10 +2149,10 @@ __global__ __launch_bounds__(64 * sb_waves<C>()) void k_sample_sparse_big(Sample
     build_doc(0, doc_end);
 
     // ring slot of token t: t % NS; slot (t + NS - 1) % NS is refilled during t
-    uint32_t ring[NS][SB_RB];
+    uint32_t ring[NS][RB];
     float cinv[NS];
-    // the first SB_RB rounds of token tp (< t1, at most 70 tokens past cbase)
-    auto prefetch = [&](uint32_t (&rg)[SB_RB], float& ci, int tp) {
+    // the first RB rounds of token tp (< t1, at most 70 tokens past cbase)
+    auto prefetch = [&](uint32_t (&rg)[RB], float& ci, int tp) {
       const int pidx = tp - cbase;
       int np, zp;
       roff_t op;
@@ -2164,12 +2171,12 @@ __global__ __launch_bounds__(64 * sb_waves<C>()) void k_sample_sparse_big(Sample
       const __amdgpu_buffer_rsrc_t rs =
           __builtin_amdgcn_make_buffer_rsrc((void*)row_ptr(op), (short)0, nrp * 256, kBufWord3);
 #pragma unroll
-      for (int q = 0; q < SB_RB; ++q) rg[q] = __builtin_amdgcn_raw_buffer_load_b32(rs, lane * 4 + q * 256, 0, 0);
+      for (int q = 0; q < RB; ++q) rg[q] = __builtin_amdgcn_raw_buffer_load_b32(rs, lane * 4 + q * 256, 0, 0);
 #else
       const int nrp = ((np & 0x7FFFFFFF) + 63) >> 6;
       const uint32_t* rp = row_ptr(op) + lane;
 #pragma unroll
-      for (int q = 0; q < SB_RB; ++q)
+      for (int q = 0; q < RB; ++q)
         if (q < nrp) rg[q] = rp[q * 64];
 #endif
       if (!FROZEN) ci = inv_m1[zp];
@@ -2277,14 +2284,14 @@ __global__ __launch_bounds__(64 * sb_waves<C>()) void k_sample_sparse_big(Sample
           // word part, register rounds: lane l holds entry l + 64 q; accq[q]
           // = the lane's running sum after round q
           const int nr_all = (n + 63) >> 6;
-          float accq[SB_RB];
+          float accq[RB];
           float acc = 0.0f;
           // rounds in groups of SB_GRP under one uniform branch, so the
           // group's LDS reads are in flight together (a round past the row's
           // last one is evaluated and not added)
           auto rounds = [&](bool sat) {
 #pragma unroll
-            for (int q = 0; q < SB_RB; q += SB_GRP) {
+            for (int q = 0; q < RB; q += SB_GRP) {
               if (q < nr_all) {
                 float tt[SB_GRP];
 #pragma unroll
@@ -2311,7 +2318,7 @@ __global__ __launch_bounds__(64 * sb_waves<C>()) void k_sample_sparse_big(Sample
             const int tp = t + NS - 1;
             if (SB_BUF || tp < t1) prefetch(ring[sp], cinv[sp], tp);
           }
-          // the rounds past SB_RB (long rows), streamed in batches; the
+          // the rounds past RB (long rows), streamed in batches; the
           // lane's running sum after each of the first SB_NB batches is kept
           // so the draw re-reads one batch of the selected lane, not all
           float accb[SB_NB];
@@ -2330,16 +2337,16 @@ __global__ __launch_bounds__(64 * sb_waves<C>()) void k_sample_sparse_big(Sample
             uint32_t ea[SB_BATCH];
 #pragma unroll
             for (int b = 0; b < SB_BATCH; ++b)
-              ea[b] = __builtin_amdgcn_raw_buffer_load_b32(rb, lane * 4 + (SB_RB + b) * 256, 0, 0);
+              ea[b] = __builtin_amdgcn_raw_buffer_load_b32(rb, lane * 4 + (RB + b) * 256, 0, 0);
             int mb = 0;
 #if SB_REM
             // whole batches only; the row's last 1..SB_BATCH-1 rounds below,
             // without the zero rounds that pad them to a batch (a +0 term
             // leaves the sum unchanged, so skipping it keeps the order)
-            int q0 = SB_RB;
+            int q0 = RB;
             for (; q0 + SB_BATCH <= nr_all; q0 += SB_BATCH, ++mb) {
 #else
-            for (int q0 = SB_RB; q0 < nr_all; q0 += SB_BATCH, ++mb) {
+            for (int q0 = RB; q0 < nr_all; q0 += SB_BATCH, ++mb) {
 #endif
               uint32_t en[SB_BATCH];
               const int vo = lane * 4 + (q0 + SB_BATCH) * 256;
@@ -2366,7 +2373,7 @@ __global__ __launch_bounds__(64 * sb_waves<C>()) void k_sample_sparse_big(Sample
 #else
           auto batches = [&](bool sat) {
             int mb = 0;
-            for (int q0 = SB_RB; q0 < nr_all; q0 += SB_BATCH, ++mb) {
+            for (int q0 = RB; q0 < nr_all; q0 += SB_BATCH, ++mb) {
               uint32_t eb[SB_BATCH];
               const uint32_t* rp = erow + lane + q0 * 64;
 #pragma unroll
@@ -2390,7 +2397,7 @@ __global__ __launch_bounds__(64 * sb_waves<C>()) void k_sample_sparse_big(Sample
           };
 #endif
 #if SB_SAT_SPLIT
-          if (nr_all > SB_RB) {
+          if (nr_all > RB) {
             if (!row_sat) batches(false);
             else batches(true);
           }
@@ -2415,24 +2422,24 @@ __global__ __launch_bounds__(64 * sb_waves<C>()) void k_sample_sparse_big(Sample
 #if SB_VCOUNT
             int cv = 0;
 #pragma unroll
-            for (int q = 0; q < SB_RB; ++q) cv += (E + accq[q] <= thr) ? 1 : 0;
+            for (int q = 0; q < RB; ++q) cv += (E + accq[q] <= thr) ? 1 : 0;
             const int cnt = readlane_i(cv, lstar);
 #else
             int cnt = 0;
 #pragma unroll
-            for (int q = 0; q < SB_RB; ++q) cnt = add_lane_bit(cnt, __ballot(E + accq[q] <= thr), lstar);
+            for (int q = 0; q < RB; ++q) cnt = add_lane_bit(cnt, __ballot(E + accq[q] <= thr), lstar);
 #endif
             int sel;
-            if (cnt < nr && cnt < SB_RB) {
+            if (cnt < nr && cnt < RB) {
               sel = cnt;
               kn = (int)((uint32_t)readlane_i((int)ring[s][sel], lstar) & ENT_TOPIC_MASK);
-            } else if (nr <= SB_RB) {
+            } else if (nr <= RB) {
               sel = nr - 1;
               kn = (int)((uint32_t)readlane_i((int)ring[s][sel], lstar) & ENT_TOPIC_MASK);
             } else {
               // lane lstar's batches: the first whose end sum exceeds (its
               // sums are monotone), among the SB_NB kept ones
-              const int nbl = (nr - SB_RB + SB_BATCH - 1) / SB_BATCH;
+              const int nbl = (nr - RB + SB_BATCH - 1) / SB_BATCH;
               int cb = 0;
 #pragma unroll
               for (int i = 0; i < SB_NB; ++i)
@@ -2444,11 +2451,11 @@ __global__ __launch_bounds__(64 * sb_waves<C>()) void k_sample_sparse_big(Sample
               } else {
                 // rounds r0.. of lane lstar (one batch, or all the rest past the
                 // kept batches), one per lane, continuing its serial sum
-                const int r0 = SB_RB + SB_BATCH * cb;
+                const int r0 = RB + SB_BATCH * cb;
                 const int nx = (cb < SB_NB ? min(nr, r0 + SB_BATCH) : nr) - r0;
                 const uint32_t e = lane < nx ? erow[lstar + 64 * (r0 + lane)] : 0u;
                 const float term = term_of(e, w, zc, invc, row_sat);
-                float a = readlane_f(accq[SB_RB - 1], lstar);
+                float a = readlane_f(accq[RB - 1], lstar);
 #pragma unroll
                 for (int i = 0; i < SB_NB; ++i)
                   if (cb == i + 1) a = readlane_f(accb[i], lstar);
@@ -2546,22 +2553,33 @@ __global__ __launch_bounds__(256) void k_row_caps(const int32_t* __restrict__ nw
 
 // Compact every nw row into its sparse entries, topic ascending, zero-padded
 // to a whole number of 64-entry rounds (one wave per row).
+// stats (nullable): += {sum over rows of total * rounds, sum of totals}, the
+// token-weighted mean 64-entry rounds of a row (the large-K sampler's ring
+// depth choice)
 template <int C>
 __global__ __launch_bounds__(256) void k_build_sparse(const int32_t* __restrict__ nw, int64_t V,
                                                       const int64_t* __restrict__ row_off,
                                                       uint32_t* __restrict__ ent,
-                                                      int32_t* __restrict__ row_nnz) {
+                                                      int32_t* __restrict__ row_nnz,
+                                                      unsigned long long* __restrict__ stats) {
   constexpr int KP = C * 64;
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  unsigned long long wsum = 0, wtot = 0;
   for (int64_t w = (int64_t)blockIdx.x * 4 + wid; w < V; w += (int64_t)gridDim.x * 4) {
     int32_t c[C];
     load_row<C>(c, nw + w * KP + lane * C);
     int cnt = 0;
     bool sat = false;
+    unsigned long long tot = 0;
 #pragma unroll
     for (int j = 0; j < C; ++j) {
       cnt += c[j] > 0 ? 1 : 0;
       sat |= (uint32_t)c[j] >= ENT_COUNT_SAT;
+      tot += (unsigned long long)(uint32_t)c[j];
+    }
+    if (stats) {
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) tot += __shfl_xor(tot, o);
     }
     const bool row_sat = __ballot(sat) != 0;
     const int incl = wave_incl_scan_i(cnt);
@@ -2584,6 +2602,14 @@ __global__ __launch_bounds__(256) void k_build_sparse(const int32_t* __restrict_
     // sign bit: the row holds a saturated count (the sampler then checks
     // entries for the escape; otherwise it skips that per-entry branch)
     if (lane == 63) row_nnz[w] = row_sat ? (int32_t)((uint32_t)incl | 0x80000000u) : incl;
+    if (stats) {
+      wsum += tot * (unsigned long long)((nnz + 63) >> 6);
+      wtot += tot;
+    }
+  }
+  if (stats && lane == 0 && wtot) {
+    atomicAdd(&stats[0], wsum);
+    atomicAdd(&stats[1], wtot);
   }
 }
 
@@ -3350,29 +3376,37 @@ static int occupancy_sparse_t() {
     return 1;
   return nb > 0 ? nb : 1;
 }
-template <int C, bool FROZEN>
+template <int C, int RB, bool FROZEN>
 static size_t sparse_big_lds() {
   // {alpha, inv} table + per-wave 16-bit nd pairs; > 64 KiB at C = 64
   constexpr size_t lds = (2 * 64 * C + sb_waves<C>() * 32 * C) * sizeof(int32_t);
   static bool attr = [] {
-    return hipFuncSetAttribute(reinterpret_cast<const void*>(&k_sample_sparse_big<C, SB_NS, FROZEN>),
+    return hipFuncSetAttribute(reinterpret_cast<const void*>(&k_sample_sparse_big<C, SB_NS, RB, FROZEN>),
                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) == hipSuccess;
   }();
   (void)attr;
   return lds;
 }
-template <int C, bool FROZEN>
-static hipError_t launch_sparse_big_t(const SampleParams& p, int blocks, hipStream_t st) {
-  const size_t lds = sparse_big_lds<C, FROZEN>();
-  hipLaunchKernelGGL((k_sample_sparse_big<C, SB_NS, FROZEN>), dim3(blocks), dim3(64 * sb_waves<C>()),
+template <int C, int RB, bool FROZEN>
+static hipError_t launch_sparse_big_rb(const SampleParams& p, int blocks, hipStream_t st) {
+  const size_t lds = sparse_big_lds<C, RB, FROZEN>();
+  hipLaunchKernelGGL((k_sample_sparse_big<C, SB_NS, RB, FROZEN>), dim3(blocks), dim3(64 * sb_waves<C>()),
                      lds, st, p);
   return hipGetLastError();
+}
+// rb: the register rounds per token (the ring's depth); SB_RB_SHORT for
+// short rows (the caller's choice from the rows' token-weighted mean rounds),
+// SB_RB otherwise.  The same sums in the same order either way.
+template <int C, bool FROZEN>
+static hipError_t launch_sparse_big_t(const SampleParams& p, int blocks, hipStream_t st, int rb) {
+  if (!FROZEN && rb == SB_RB_SHORT) return launch_sparse_big_rb<C, SB_RB_SHORT, FROZEN>(p, blocks, st);
+  return launch_sparse_big_rb<C, SB_RB, FROZEN>(p, blocks, st);
 }
 template <int C, bool FROZEN>
 static int occupancy_sparse_big_t() {
   int nb = 0;
-  const size_t lds = sparse_big_lds<C, FROZEN>();
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_sample_sparse_big<C, SB_NS, FROZEN>,
+  const size_t lds = sparse_big_lds<C, SB_RB, FROZEN>();
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_sample_sparse_big<C, SB_NS, SB_RB, FROZEN>,
                                                    64 * sb_waves<C>(), lds) != hipSuccess)
     return 1;
   return nb > 0 ? nb : 1;
@@ -3387,9 +3421,9 @@ static int occupancy_sparse_big_t() {
     default: break;                                                 \
   }
 template <bool FROZEN>
-static hipError_t launch_sparse_c(int C, const SampleParams& p, int blocks, hipStream_t st) {
-  if (C == 32) return launch_sparse_big_t<32, FROZEN>(p, blocks, st);
-  if (C == 64) return launch_sparse_big_t<64, FROZEN>(p, blocks, st);
+static hipError_t launch_sparse_c(int C, const SampleParams& p, int blocks, hipStream_t st, int rb) {
+  if (C == 32) return launch_sparse_big_t<32, FROZEN>(p, blocks, st, rb);
+  if (C == 64) return launch_sparse_big_t<64, FROZEN>(p, blocks, st, rb);
   LDA_DISPATCH_SPARSE(C, launch_sparse_t, p, blocks, st)
   return hipErrorInvalidValue;
 }
@@ -3401,8 +3435,8 @@ static int occupancy_sparse_c(int C) {
   return 1;
 }
 hipError_t launch_sample_sparse(int C, bool frozen, const SampleParams& p, int blocks,
-                                hipStream_t st) {
-  return frozen ? launch_sparse_c<true>(C, p, blocks, st) : launch_sparse_c<false>(C, p, blocks, st);
+                                hipStream_t st, int rb) {
+  return frozen ? launch_sparse_c<true>(C, p, blocks, st, rb) : launch_sparse_c<false>(C, p, blocks, st, rb);
 }
 int sample_sparse_blocks_per_cu(int C, bool frozen) {
   return frozen ? occupancy_sparse_c<true>(C) : occupancy_sparse_c<false>(C);
@@ -3433,17 +3467,18 @@ hipError_t launch_row_caps(const int32_t* nw, int64_t V, int32_t Kp, int32_t* ca
 }
 
 hipError_t launch_build_sparse(const int32_t* nw, int64_t V, int32_t Kp, const int64_t* row_off,
-                               uint32_t* ent, int32_t* row_nnz, hipStream_t st) {
+                               uint32_t* ent, int32_t* row_nnz, hipStream_t st,
+                               unsigned long long* stats) {
   if (V <= 0) return hipSuccess;
   const int blocks = (int)std::min<int64_t>((V + 3) / 4, 16384);
   switch (Kp / 64) {
-    case 1: hipLaunchKernelGGL(k_build_sparse<1>, dim3(blocks), dim3(256), 0, st, nw, V, row_off, ent, row_nnz); break;
-    case 2: hipLaunchKernelGGL(k_build_sparse<2>, dim3(blocks), dim3(256), 0, st, nw, V, row_off, ent, row_nnz); break;
-    case 4: hipLaunchKernelGGL(k_build_sparse<4>, dim3(blocks), dim3(256), 0, st, nw, V, row_off, ent, row_nnz); break;
-    case 8: hipLaunchKernelGGL(k_build_sparse<8>, dim3(blocks), dim3(256), 0, st, nw, V, row_off, ent, row_nnz); break;
-    case 16: hipLaunchKernelGGL(k_build_sparse<16>, dim3(blocks), dim3(256), 0, st, nw, V, row_off, ent, row_nnz); break;
-    case 32: hipLaunchKernelGGL(k_build_sparse<32>, dim3(blocks), dim3(256), 0, st, nw, V, row_off, ent, row_nnz); break;
-    case 64: hipLaunchKernelGGL(k_build_sparse<64>, dim3(blocks), dim3(256), 0, st, nw, V, row_off, ent, row_nnz); break;
+    case 1: hipLaunchKernelGGL(k_build_sparse<1>, dim3(blocks), dim3(256), 0, st, nw, V, row_off, ent, row_nnz, stats); break;
+    case 2: hipLaunchKernelGGL(k_build_sparse<2>, dim3(blocks), dim3(256), 0, st, nw, V, row_off, ent, row_nnz, stats); break;
+    case 4: hipLaunchKernelGGL(k_build_sparse<4>, dim3(blocks), dim3(256), 0, st, nw, V, row_off, ent, row_nnz, stats); break;
+    case 8: hipLaunchKernelGGL(k_build_sparse<8>, dim3(blocks), dim3(256), 0, st, nw, V, row_off, ent, row_nnz, stats); break;
+    case 16: hipLaunchKernelGGL(k_build_sparse<16>, dim3(blocks), dim3(256), 0, st, nw, V, row_off, ent, row_nnz, stats); break;
+    case 32: hipLaunchKernelGGL(k_build_sparse<32>, dim3(blocks), dim3(256), 0, st, nw, V, row_off, ent, row_nnz, stats); break;
+    case 64: hipLaunchKernelGGL(k_build_sparse<64>, dim3(blocks), dim3(256), 0, st, nw, V, row_off, ent, row_nnz, stats); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();

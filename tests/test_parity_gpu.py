@@ -471,12 +471,17 @@ def test_dense_half_wave_variant(oracle, K, variant, monkeypatch):
     np.testing.assert_allclose(tg, to, rtol=0, atol=1e-12)
 
 
-def test_large_k_sparse_very_long_rows(oracle):
+@pytest.mark.parametrize("ring", ["8", "10", "auto"])
+def test_large_k_sparse_very_long_rows(oracle, monkeypatch, ring):
     """Word rows far longer than the register rounds (K = 4096): rows of up
     to ~3500 entries, so a draw can land in the register rounds, in either of
     the batches whose running sums are kept, or past them (the re-read of
     the rest of the selected lane), and the sparse rows are padded to whole
-    64-entry rounds."""
+    64-entry rounds.  ring: the sampler's register rounds, fixed at 8 or 10
+    (LDA_SB_RB) or chosen per sweep from the rows' mean rounds (round 4):
+    the same sums in the same order, so the same draws."""
+    if ring != "auto":
+        monkeypatch.setenv("LDA_SB_RB", ring)
     from ldagibbssampling_amd.corpus import Corpus
     rng = np.random.default_rng(12)
     D, L, V = 600, 300, 2000
@@ -490,6 +495,10 @@ def test_large_k_sparse_very_long_rows(oracle):
     g.sweep(2)
     o.sweep(2)
     _assert_same_state(g, o, with_nd=False)
+    if ring == "auto":          # more sweeps: the depth choice lands and may switch
+        g.sweep(4)
+        o.sweep(4)
+        _assert_same_state(g, o, with_nd=False)
     nnz = (g.counts()[0] > 0).sum(1)
     rounds = (nnz + 63) // 64
     assert rounds.max() > 10 + 8 * 3                 # past every kept batch
