@@ -245,17 +245,21 @@ struct lda_ctx {
   int64_t* row_off = nullptr;
   int32_t* row_nnz = nullptr;
   uint32_t* row_rnd = nullptr;   // row_off / 64: the large-K sampler's 32-bit row starts
-  // the large-K sampler's ring depth (register rounds): SB_RB_SHORT_ROUNDS
-  // while the rows' token-weighted mean rounds (from the last apply's
-  // k_build_sparse, read back without a wait) are at most big_rb_switch, the
-  // default depth otherwise; LDA_SB_RB=<n> at lda_create fixes it (A/B)
+  // the large-K sampler's ring depth (register rounds): 0 = the default,
+  // lda::SB_RB_SHORT_ROUNDS = the short ring.  Both give the same draws; which
+  // is faster depends on the rows' lengths, which shrink as the chain burns
+  // in, so the context times them (big_rb_next): three consecutive sweeps'
+  // first launches at default / short / default depth (a linear drift of the
+  // sweep time cancels against the mean of the outer two), then the faster
+  // is kept for PROBE_HOLD sweeps; a probe costs one sweep at the slower
+  // depth and one host wait.  LDA_SB_RB=<n> at lda_create fixes the depth.
+  static constexpr int64_t PROBE_HOLD = 16;
   bool big_rb_auto = true;
   int big_rb = 0;
-  double big_rb_switch = 8.0;
-  unsigned long long* big_stats = nullptr;
-  unsigned long long* big_stats_pin = nullptr;
-  hipEvent_t big_stats_ev = nullptr;
-  bool big_stats_live = false;
+  int big_probe = 0;                 // probe launches issued so far (0..3)
+  int big_probe_slot = -1;           // the sweep being sampled is probe launch i (else -1)
+  int64_t big_hold = 0;              // sweeps left before the next probe
+  hipEvent_t big_ev[3][2] = {};
   bool rows_ready = false;
   int half = 0;    // dense K <= 128: 1 = the half-wave variant, 2 = the quarter-wave one (LDA_DENSE_HALF)
   // lda_infer: word totals of the snapshot (TopicInferencer's empty-row test),
@@ -427,9 +431,9 @@ struct lda_ctx {
     for (auto& g : graphs)
       if (g) (void)hipGraphExecDestroy(g);
     if (graph_ev) (void)hipEventDestroy(graph_ev);
-    if (big_stats) (void)hipFree(big_stats);
-    if (big_stats_pin) (void)hipHostFree(big_stats_pin);
-    if (big_stats_ev) (void)hipEventDestroy(big_stats_ev);
+    for (auto& e : big_ev)
+      for (hipEvent_t x : e)
+        if (x) (void)hipEventDestroy(x);
     if (switch_ev) (void)hipEventDestroy(switch_ev);
     if (state_dev) (void)hipFree(state_dev);
     if (zw) (void)hipFree(zw);
@@ -605,29 +609,7 @@ static lda_status apply_impl(lda_ctx* c) {
       lda_status s = build_row_capacity(c);
       if (s) return s;
     }
-    // the large-K sampler's ring depth for the next sweep: the rows'
-    // token-weighted mean rounds, copied back without a wait (the choice
-    // reads the copy of an earlier apply once it has landed)
-    const bool stats = c->C >= 32 && c->big_rb_auto;
-    if (stats) {
-      if (!c->big_stats) {
-        HIP_TRY(dalloc(&c->big_stats, 2));
-        HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&c->big_stats_pin), 2 * sizeof(unsigned long long)));
-        HIP_TRY(hipEventCreateWithFlags(&c->big_stats_ev, hipEventDisableTiming));
-      }
-      if (!c->big_stats_live) {
-        HIP_TRY(hipMemsetAsync(c->big_stats, 0, 2 * sizeof(unsigned long long), c->stream));
-      }
-    }
-    const bool take = stats && !c->big_stats_live;
-    HIP_TRY(lda::launch_build_sparse(c->nw, c->V, c->Kp, c->row_off, c->ent, c->row_nnz, c->stream,
-                                     take ? c->big_stats : nullptr));
-    if (take) {
-      HIP_TRY(hipMemcpyAsync(c->big_stats_pin, c->big_stats, 2 * sizeof(unsigned long long),
-                             hipMemcpyDeviceToHost, c->stream));
-      HIP_TRY(hipEventRecord(c->big_stats_ev, c->stream));
-      c->big_stats_live = true;
-    }
+    HIP_TRY(lda::launch_build_sparse(c->nw, c->V, c->Kp, c->row_off, c->ent, c->row_nnz, c->stream));
   } else {
     HIP_TRY(lda::launch_build_packed(c->nw, c->V, c->Kp, c->nw16, c->wide, c->stream));
   }
@@ -947,6 +929,35 @@ lda_status lda_apply(lda_ctx* c) {
   });
 }
 
+// The large-K sampler's ring depth for the sweep about to be sampled (see
+// lda_ctx::big_rb).  big_hold > 0: holding, a sweep counts it down; then
+// three probe launches (the sweeps' first parts) at default / short / default
+// depth; the sweep after them waits for the third (one host wait per probe:
+// a read-back that lagged the host's queue would choose by the rows of many
+// sweeps ago) and keeps the faster depth for the next PROBE_HOLD sweeps.
+static lda_status big_rb_next(lda_ctx* c) {
+  c->big_probe_slot = -1;
+  if (c->big_hold > 0) {
+    --c->big_hold;
+    return LDA_OK;
+  }
+  if (c->big_probe < 3) {                       // the next probe launch
+    if (!c->big_ev[0][0])
+      for (auto& e : c->big_ev)
+        for (hipEvent_t& x : e) HIP_TRY(hipEventCreate(&x));
+    c->big_rb = c->big_probe == 1 ? lda::SB_RB_SHORT_ROUNDS : 0;
+    c->big_probe_slot = c->big_probe++;
+    return LDA_OK;
+  }
+  HIP_TRY(hipEventSynchronize(c->big_ev[2][1]));
+  float ms[3];
+  for (int i = 0; i < 3; ++i) HIP_TRY(hipEventElapsedTime(&ms[i], c->big_ev[i][0], c->big_ev[i][1]));
+  c->big_rb = ms[1] < 0.5f * (ms[0] + ms[2]) ? lda::SB_RB_SHORT_ROUNDS : 0;
+  c->big_hold = lda_ctx::PROBE_HOLD;
+  c->big_probe = 0;
+  return LDA_OK;
+}
+
 // One launch of the sampler over part `part` of a (possibly split) sweep.
 static lda_status sample_part_impl(lda_ctx* c, int part) {
   if (part != c->next_part)
@@ -958,11 +969,9 @@ static lda_status sample_part_impl(lda_ctx* c, int part) {
   if (part == 0) {
     c->sweep_kind = next_sweep_kind(c);
     c->sweep_seq = c->sweep_kind != 0;
-    if (c->big_stats_live && hipEventQuery(c->big_stats_ev) == hipSuccess) {
-      const unsigned long long* h = c->big_stats_pin;
-      const double mean_rounds = h[1] ? (double)h[0] / (double)h[1] : 0.0;
-      c->big_rb = mean_rounds <= c->big_rb_switch ? lda::SB_RB_SHORT_ROUNDS : 0;
-      c->big_stats_live = false;
+    if (c->sampler == LDA_SAMPLER_SPARSE && c->C >= 32 && c->big_rb_auto) {
+      lda_status s = big_rb_next(c);
+      if (s) return s;
     }
     c->sweep_recount = next_sweep_recounts(c);
     if (c->sweep_recount && !c->perm && c->N > 0) {
@@ -1009,10 +1018,13 @@ static lda_status sample_part_impl(lda_ctx* c, int part) {
     const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>(cap, (r1 - r0 + wpb - 1) / wpb));
     const int slot = (int)(c->launches % lda_ctx::LDA_TIME_RING);
     HIP_TRY(hipEventRecord(c->ev0[slot], c->stream));
+    const int probe = part == 0 ? c->big_probe_slot : -1;
+    if (probe >= 0) HIP_TRY(hipEventRecord(c->big_ev[probe][0], c->stream));
     if (c->sampler == LDA_SAMPLER_SPARSE)
       HIP_TRY(lda::launch_sample_sparse(c->C, false, p, blocks, c->stream, c->big_rb));
     else
       HIP_TRY(lda::launch_sample(c->C, false, p, blocks, c->stream, c->half));
+    if (probe >= 0) HIP_TRY(hipEventRecord(c->big_ev[probe][1], c->stream));
     HIP_TRY(hipEventRecord(c->ev1[slot], c->stream));
     if (c->sweep_recount) {
       // this part's rows recounted into its exchange buffer (the apply left

@@ -115,8 +115,7 @@ int sample_sparse_blocks_per_cu(int C, bool frozen);
 // row totals of nw (saturating at Kp) -> host prefix -> capacity offsets
 hipError_t launch_row_caps(const int32_t* nw, int64_t V, int32_t Kp, int32_t* caps, hipStream_t st);
 hipError_t launch_build_sparse(const int32_t* nw, int64_t V, int32_t Kp, const int64_t* row_off,
-                               uint32_t* ent, int32_t* row_nnz, hipStream_t st,
-                               unsigned long long* stats = nullptr);
+                               uint32_t* ent, int32_t* row_nnz, hipStream_t st);
 hipError_t launch_build_packed(const int32_t* nw, int64_t V, int32_t Kp, uint16_t* nw16,
                                uint8_t* wide, hipStream_t st);
 // per-topic state refreshed by an apply (k_prepare_topics' arguments)

@@ -1843,9 +1843,9 @@ __global__ __launch_bounds__(256) void k_sample_sparse(SampleParams p) {
 #ifndef SB_RB
 #define SB_RB 10
 #endif
-// the ring's depth for short rows (round 4: after burn-in a C5 row is ~4-5
-// rounds; 8 register rounds were +2% there and -3% on the ~11-round rows
-// near init, so the launch picks by the rows' token-weighted mean rounds)
+// the ring's depth for short rows (round 4: 8 register rounds were +2% on
+// C5 after burn-in and -3% on its longer rows near init, so the host times
+// both depths from time to time and keeps the faster: lda_capi.cpp)
 #ifndef SB_RB_SHORT
 #define SB_RB_SHORT 8
 #endif
@@ -1923,6 +1923,14 @@ static_assert(SB_RB_SHORT == SB_RB_SHORT_ROUNDS, "lda_kernels.h names the short 
 #ifndef SB_DEFER
 #define SB_DEFER 1
 #endif
+// rows that fill the register rounds: the rounds as one straight-line
+// sequence whose LDS operands (document count, {alpha, inv}) are read one
+// round ahead by hand (inline ds_read + counted lgkmcnt waits), so two
+// rounds' reads are in flight where the compiler waited for each round's
+// own (A/B)
+#ifndef SB_PIPE
+#define SB_PIPE 0
+#endif
 // gfx9 buffer resource word 3 (raw 32-bit loads, bounds checked)
 [[maybe_unused]] constexpr int kBufWord3 = 0x00020000;
 static_assert(SB_RB % SB_GRP == 0 && (SB_DBUF || SB_BATCH % SB_GRP == 0), "round groups");
@@ -1961,6 +1969,12 @@ __global__ __launch_bounds__(64 * sb_waves<C>()) void k_sample_sparse_big(Sample
   for (int i = threadIdx.x; i < KP; i += 64 * WB) tab[i] = make_float2(p.alpha[i], p.inv[i]);
   for (int i = threadIdx.x; i < WB * (KP / 2); i += 64 * WB) smem[2 * KP + i] = 0;
   __syncthreads();
+#if SB_PIPE
+  // LDS byte addresses of the table and of this wave's document counts
+  typedef __attribute__((address_space(3))) int32_t lds_i32;
+  const uint32_t tab_lds = (uint32_t)(uintptr_t)(lds_i32*)smem;
+  const uint32_t nd_lds = (uint32_t)(uintptr_t)(lds_i32*)nd2;
+#endif
 
   const float beta = p.beta;
   const int last_lane = (p.K - 1) / C;
@@ -2289,7 +2303,50 @@ __global__ __launch_bounds__(64 * sb_waves<C>()) void k_sample_sparse_big(Sample
           // rounds in groups of SB_GRP under one uniform branch, so the
           // group's LDS reads are in flight together (a round past the row's
           // last one is evaluated and not added)
+#if SB_PIPE
+          // every register round of a row that fills them (no branch per
+          // round): round q+1's two LDS reads are issued before round q is
+          // summed, and the wait for round q leaves them in flight.  A
+          // read's destination stays live (an operand of the wait that
+          // retires it) until the data has landed.  The terms and their
+          // order are term_of's.
+          auto rounds_full = [&]() {
+            uint32_t ndv[2];
+            double tbv[2];
+            auto issue = [&](int b, uint32_t e) {
+              const uint32_t k = e & ENT_TOPIC_MASK;
+              const uint32_t a_nd = nd_lds + 2u * k, a_tb = tab_lds + 8u * k;
+              asm volatile("ds_read_u16 %0, %1" : "=v"(ndv[b]) : "v"(a_nd) : "memory");
+              asm volatile("ds_read_b64 %0, %1" : "=v"(tbv[b]) : "v"(a_tb) : "memory");
+            };
+            issue(0, ring[s][0]);
+#pragma unroll
+            for (int q = 0; q < RB; ++q) {
+              const int b = q & 1;
+              if (q + 1 < RB) {
+                issue(b ^ 1, ring[s][q + 1]);
+                asm volatile("s_waitcnt lgkmcnt(2)" : "+v"(ndv[b]), "+v"(tbv[b]));
+              } else {
+                asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(ndv[b]), "+v"(tbv[b]));
+              }
+              const uint32_t e = ring[s][q];
+              const int tq = (int)(e & ENT_TOPIC_MASK);
+              uint32_t cq = e >> ENT_TOPIC_BITS;
+              if (!FROZEN) cq = __builtin_elementwise_sub_sat(cq, (uint32_t)(tq == zc));
+              const float2 t = __builtin_bit_cast(float2, tbv[b]);
+              const float coef = ((float)(int)ndv[b] + t.x) * ((tq == zc) ? invc : t.y);
+              acc = acc + coef * (float)(int)cq;
+              accq[q] = acc;
+            }
+          };
+#endif
           auto rounds = [&](bool sat) {
+#if SB_PIPE
+            if (!sat && nr_all >= RB) {
+              rounds_full();
+              return;
+            }
+#endif
 #pragma unroll
             for (int q = 0; q < RB; q += SB_GRP) {
               if (q < nr_all) {
@@ -2553,33 +2610,22 @@ __global__ __launch_bounds__(256) void k_row_caps(const int32_t* __restrict__ nw
 
 // Compact every nw row into its sparse entries, topic ascending, zero-padded
 // to a whole number of 64-entry rounds (one wave per row).
-// stats (nullable): += {sum over rows of total * rounds, sum of totals}, the
-// token-weighted mean 64-entry rounds of a row (the large-K sampler's ring
-// depth choice)
 template <int C>
 __global__ __launch_bounds__(256) void k_build_sparse(const int32_t* __restrict__ nw, int64_t V,
                                                       const int64_t* __restrict__ row_off,
                                                       uint32_t* __restrict__ ent,
-                                                      int32_t* __restrict__ row_nnz,
-                                                      unsigned long long* __restrict__ stats) {
+                                                      int32_t* __restrict__ row_nnz) {
   constexpr int KP = C * 64;
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  unsigned long long wsum = 0, wtot = 0;
   for (int64_t w = (int64_t)blockIdx.x * 4 + wid; w < V; w += (int64_t)gridDim.x * 4) {
     int32_t c[C];
     load_row<C>(c, nw + w * KP + lane * C);
     int cnt = 0;
     bool sat = false;
-    unsigned long long tot = 0;
 #pragma unroll
     for (int j = 0; j < C; ++j) {
       cnt += c[j] > 0 ? 1 : 0;
       sat |= (uint32_t)c[j] >= ENT_COUNT_SAT;
-      tot += (unsigned long long)(uint32_t)c[j];
-    }
-    if (stats) {
-#pragma unroll
-      for (int o = 32; o > 0; o >>= 1) tot += __shfl_xor(tot, o);
     }
     const bool row_sat = __ballot(sat) != 0;
     const int incl = wave_incl_scan_i(cnt);
@@ -2602,14 +2648,6 @@ __global__ __launch_bounds__(256) void k_build_sparse(const int32_t* __restrict_
     // sign bit: the row holds a saturated count (the sampler then checks
     // entries for the escape; otherwise it skips that per-entry branch)
     if (lane == 63) row_nnz[w] = row_sat ? (int32_t)((uint32_t)incl | 0x80000000u) : incl;
-    if (stats) {
-      wsum += tot * (unsigned long long)((nnz + 63) >> 6);
-      wtot += tot;
-    }
-  }
-  if (stats && lane == 0 && wtot) {
-    atomicAdd(&stats[0], wsum);
-    atomicAdd(&stats[1], wtot);
   }
 }
 
@@ -3467,18 +3505,17 @@ hipError_t launch_row_caps(const int32_t* nw, int64_t V, int32_t Kp, int32_t* ca
 }
 
 hipError_t launch_build_sparse(const int32_t* nw, int64_t V, int32_t Kp, const int64_t* row_off,
-                               uint32_t* ent, int32_t* row_nnz, hipStream_t st,
-                               unsigned long long* stats) {
+                               uint32_t* ent, int32_t* row_nnz, hipStream_t st) {
   if (V <= 0) return hipSuccess;
   const int blocks = (int)std::min<int64_t>((V + 3) / 4, 16384);
   switch (Kp / 64) {
-    case 1: hipLaunchKernelGGL(k_build_sparse<1>, dim3(blocks), dim3(256), 0, st, nw, V, row_off, ent, row_nnz, stats); break;
-    case 2: hipLaunchKernelGGL(k_build_sparse<2>, dim3(blocks), dim3(256), 0, st, nw, V, row_off, ent, row_nnz, stats); break;
-    case 4: hipLaunchKernelGGL(k_build_sparse<4>, dim3(blocks), dim3(256), 0, st, nw, V, row_off, ent, row_nnz, stats); break;
-    case 8: hipLaunchKernelGGL(k_build_sparse<8>, dim3(blocks), dim3(256), 0, st, nw, V, row_off, ent, row_nnz, stats); break;
-    case 16: hipLaunchKernelGGL(k_build_sparse<16>, dim3(blocks), dim3(256), 0, st, nw, V, row_off, ent, row_nnz, stats); break;
-    case 32: hipLaunchKernelGGL(k_build_sparse<32>, dim3(blocks), dim3(256), 0, st, nw, V, row_off, ent, row_nnz, stats); break;
-    case 64: hipLaunchKernelGGL(k_build_sparse<64>, dim3(blocks), dim3(256), 0, st, nw, V, row_off, ent, row_nnz, stats); break;
+    case 1: hipLaunchKernelGGL(k_build_sparse<1>, dim3(blocks), dim3(256), 0, st, nw, V, row_off, ent, row_nnz); break;
+    case 2: hipLaunchKernelGGL(k_build_sparse<2>, dim3(blocks), dim3(256), 0, st, nw, V, row_off, ent, row_nnz); break;
+    case 4: hipLaunchKernelGGL(k_build_sparse<4>, dim3(blocks), dim3(256), 0, st, nw, V, row_off, ent, row_nnz); break;
+    case 8: hipLaunchKernelGGL(k_build_sparse<8>, dim3(blocks), dim3(256), 0, st, nw, V, row_off, ent, row_nnz); break;
+    case 16: hipLaunchKernelGGL(k_build_sparse<16>, dim3(blocks), dim3(256), 0, st, nw, V, row_off, ent, row_nnz); break;
+    case 32: hipLaunchKernelGGL(k_build_sparse<32>, dim3(blocks), dim3(256), 0, st, nw, V, row_off, ent, row_nnz); break;
+    case 64: hipLaunchKernelGGL(k_build_sparse<64>, dim3(blocks), dim3(256), 0, st, nw, V, row_off, ent, row_nnz); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();
