@@ -254,6 +254,12 @@ struct lda_ctx {
   // is kept for PROBE_HOLD sweeps; a probe costs one sweep at the slower
   // depth and one host wait.  LDA_SB_RB=<n> at lda_create fixes the depth.
   static constexpr int64_t PROBE_HOLD = 16;
+  // no probe in the context's first PROBE_FIRST sweeps: right after the
+  // random start the rows shrink fastest and the drift is far from linear
+  // (a probe over sweeps 0-2 picked the short ring, 3% slower there); the
+  // default depth is the right one near init
+  static constexpr int64_t PROBE_FIRST = 8;
+  int64_t big_sweeps = 0;            // sweeps sampled by the large-K sampler
   bool big_rb_auto = true;
   int big_rb = 0;
   int big_probe = 0;                 // probe launches issued so far (0..3)
@@ -930,13 +936,18 @@ lda_status lda_apply(lda_ctx* c) {
 }
 
 // The large-K sampler's ring depth for the sweep about to be sampled (see
-// lda_ctx::big_rb).  big_hold > 0: holding, a sweep counts it down; then
+// lda_ctx::big_rb).  The first PROBE_FIRST sweeps take the default depth;
+// big_hold > 0: holding, a sweep counts it down; then
 // three probe launches (the sweeps' first parts) at default / short / default
 // depth; the sweep after them waits for the third (one host wait per probe:
 // a read-back that lagged the host's queue would choose by the rows of many
 // sweeps ago) and keeps the faster depth for the next PROBE_HOLD sweeps.
 static lda_status big_rb_next(lda_ctx* c) {
   c->big_probe_slot = -1;
+  if (c->big_sweeps++ < lda_ctx::PROBE_FIRST) {
+    c->big_rb = 0;
+    return LDA_OK;
+  }
   if (c->big_hold > 0) {
     --c->big_hold;
     return LDA_OK;

@@ -106,11 +106,11 @@ hipError_t launch_sample(int C, bool frozen, const SampleParams& p, int blocks, 
 int sample_blocks_per_cu(int C, bool frozen, int K, int half = 0);
 int half_topics_per_lane(int K);
 int quarter_topics_per_lane(int K);
-// rb: register rounds of the large-K sampler (C >= 32): SB_RB_SHORT_ROUNDS
-// for short rows, anything else the default depth
+// rb: the large-K sampler's ring (C >= 32): 0 the default depth, nonzero
+// the short one for short rows (SB_RB_SHORT in lda_kernels.hip)
 hipError_t launch_sample_sparse(int C, bool frozen, const SampleParams& p, int blocks,
                                 hipStream_t st, int rb = 0);
-constexpr int SB_RB_SHORT_ROUNDS = 8;   // == SB_RB_SHORT in lda_kernels.hip
+constexpr int SB_RB_SHORT_ROUNDS = 8;   // the short depth's rounds (SB_RB_SHORT's default)
 int sample_sparse_blocks_per_cu(int C, bool frozen);
 // row totals of nw (saturating at Kp) -> host prefix -> capacity offsets
 hipError_t launch_row_caps(const int32_t* nw, int64_t V, int32_t Kp, int32_t* caps, hipStream_t st);

@@ -1849,7 +1849,10 @@ __global__ __launch_bounds__(256) void k_sample_sparse(SampleParams p) {
 #ifndef SB_RB_SHORT
 #define SB_RB_SHORT 8
 #endif
-static_assert(SB_RB_SHORT == SB_RB_SHORT_ROUNDS, "lda_kernels.h names the short depth");
+// the ring's slots at the short depth
+#ifndef SB_NS_SHORT
+#define SB_NS_SHORT SB_NS
+#endif
 #ifndef SB_BATCH
 #define SB_BATCH 4
 #endif
@@ -3414,36 +3417,36 @@ static int occupancy_sparse_t() {
     return 1;
   return nb > 0 ? nb : 1;
 }
-template <int C, int RB, bool FROZEN>
+template <int C, int NS, int RB, bool FROZEN>
 static size_t sparse_big_lds() {
   // {alpha, inv} table + per-wave 16-bit nd pairs; > 64 KiB at C = 64
   constexpr size_t lds = (2 * 64 * C + sb_waves<C>() * 32 * C) * sizeof(int32_t);
   static bool attr = [] {
-    return hipFuncSetAttribute(reinterpret_cast<const void*>(&k_sample_sparse_big<C, SB_NS, RB, FROZEN>),
+    return hipFuncSetAttribute(reinterpret_cast<const void*>(&k_sample_sparse_big<C, NS, RB, FROZEN>),
                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) == hipSuccess;
   }();
   (void)attr;
   return lds;
 }
-template <int C, int RB, bool FROZEN>
+template <int C, int NS, int RB, bool FROZEN>
 static hipError_t launch_sparse_big_rb(const SampleParams& p, int blocks, hipStream_t st) {
-  const size_t lds = sparse_big_lds<C, RB, FROZEN>();
-  hipLaunchKernelGGL((k_sample_sparse_big<C, SB_NS, RB, FROZEN>), dim3(blocks), dim3(64 * sb_waves<C>()),
+  const size_t lds = sparse_big_lds<C, NS, RB, FROZEN>();
+  hipLaunchKernelGGL((k_sample_sparse_big<C, NS, RB, FROZEN>), dim3(blocks), dim3(64 * sb_waves<C>()),
                      lds, st, p);
   return hipGetLastError();
 }
-// rb: the register rounds per token (the ring's depth); SB_RB_SHORT for
-// short rows (the caller's choice from the rows' token-weighted mean rounds),
-// SB_RB otherwise.  The same sums in the same order either way.
+// rb: 0 for the default ring (SB_NS slots of SB_RB register rounds), else
+// the short one (SB_NS_SHORT x SB_RB_SHORT) for short rows (the caller's
+// choice, by timing both).  The same sums in the same order either way.
 template <int C, bool FROZEN>
 static hipError_t launch_sparse_big_t(const SampleParams& p, int blocks, hipStream_t st, int rb) {
-  if (!FROZEN && rb == SB_RB_SHORT) return launch_sparse_big_rb<C, SB_RB_SHORT, FROZEN>(p, blocks, st);
-  return launch_sparse_big_rb<C, SB_RB, FROZEN>(p, blocks, st);
+  if (!FROZEN && rb != 0) return launch_sparse_big_rb<C, SB_NS_SHORT, SB_RB_SHORT, FROZEN>(p, blocks, st);
+  return launch_sparse_big_rb<C, SB_NS, SB_RB, FROZEN>(p, blocks, st);
 }
 template <int C, bool FROZEN>
 static int occupancy_sparse_big_t() {
   int nb = 0;
-  const size_t lds = sparse_big_lds<C, SB_RB, FROZEN>();
+  const size_t lds = sparse_big_lds<C, SB_NS, SB_RB, FROZEN>();
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_sample_sparse_big<C, SB_NS, SB_RB, FROZEN>,
                                                    64 * sb_waves<C>(), lds) != hipSuccess)
     return 1;

@@ -499,7 +499,7 @@ def test_large_k_sparse_very_long_rows(oracle, monkeypatch, ring):
     rounds = (nnz + 63) // 64
     assert rounds.max() > 10 + 8 * 3                 # past every kept batch
     assert ((rounds > 10) & (rounds <= 18)).any() and ((rounds > 18) & (rounds <= 26)).any()
-    if ring == "auto":          # more sweeps: the depth choice lands and may switch
-        g.sweep(4)
-        o.sweep(4)
+    if ring == "auto":          # sweeps 8-10 probe both depths, 11-13 take the faster
+        g.sweep(12)
+        o.sweep(12)
         _assert_same_state(g, o, with_nd=False)
