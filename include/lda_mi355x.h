@@ -103,7 +103,12 @@ lda_status lda_sweep(lda_ctx* ctx, int32_t n);
 
 /* One sampling pass over the shard against the current nw/nwsum snapshot
  * (one sweep of WorkerRunnable.run()); its result goes to the exchange
- * buffer below. */
+ * buffer below.  Asynchronous on the context's stream, except that the
+ * large-K sampler (K > 1024) times its two ring depths from the ninth sweep
+ * on, every 19 sweeps: the sweep after such a probe waits on the host for
+ * the probe's last launch (LDA_SB_RB=10 or 8 at
+ * lda_create fixes the depth and never waits).  Either depth gives the same
+ * draws. */
 lda_status lda_sample(lda_ctx* ctx);
 /* Device pointer to the pending exchange buffer: int32[V*Kp + Kp] (an nw part
  * row-major with padded row length Kp = lda_padded_topics(), then an nwsum

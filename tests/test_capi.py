@@ -195,3 +195,46 @@ def test_staleness_schedule_matches_mallet_threads(lib):
     # the quantised cuts are exact for equal parts
     assert O.quantise_fractions([1 / 3] * 3) == O.equal_cum(3)
     assert O.quantise_fractions([0.5, 0.5]) == O.equal_cum(2)
+
+
+def test_profile_summary_windows_the_bench_sweeps(tmp_path):
+    """tools/summarize_prof.py averages exactly the bench's timed sweeps: the
+    sampler's dispatches form one sequence whatever their template arguments
+    (the large-K sampler alternates two ring depths), the skipped warm-up /
+    burn-in sweeps and whatever follows the timed region (the estimate() side
+    figure's launches) stay out."""
+    import csv
+    import importlib.util
+    import json
+    import os
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    spec = importlib.util.spec_from_file_location("sp", os.path.join(root, "tools", "summarize_prof.py"))
+    sp = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(sp)
+    # 4 untimed sweeps, 3 timed, then 5 small "side figure" launches; sweep 1
+    # and timed sweep 5 use the other instantiation
+    names = ["k_sample_big<64, 3, 10, false>"] * 12
+    names[1] = names[5] = "k_sample_big<64, 3, 8, false>"
+    durs = [100, 90, 80, 70, 60, 50, 40, 1, 1, 1, 1, 1]
+    with open(tmp_path / "x_kernel_trace.csv", "w", newline="") as f:
+        w = csv.DictWriter(f, ["Kernel_Name", "Start_Timestamp", "End_Timestamp"])
+        w.writeheader()
+        for i, (n, d) in enumerate(zip(names, durs)):
+            w.writerow({"Kernel_Name": n, "Start_Timestamp": 1000 * i, "End_Timestamp": 1000 * i + d})
+            w.writerow({"Kernel_Name": "k_apply(int)", "Start_Timestamp": 1000 * i + 500,
+                        "End_Timestamp": 1000 * i + 510})
+    with open(tmp_path / "x_counter_collection.csv", "w", newline="") as f:
+        w = csv.DictWriter(f, ["Kernel_Name", "Dispatch_Id", "Counter_Name", "Counter_Value"])
+        w.writeheader()
+        for i, (n, d) in enumerate(zip(names, durs)):
+            for half in (0.5, 0.5):          # a counter reported per XCD-like slice
+                w.writerow({"Kernel_Name": n, "Dispatch_Id": 2 * i, "Counter_Name": "WRITE_SIZE",
+                            "Counter_Value": d * half})
+    out = tmp_path / "s.json"
+    sp.main(str(tmp_path), str(out), 4, 1, 3)
+    s = json.load(open(out))
+    k10, k8 = "k_sample_big<64, 3, 10, false>", "k_sample_big<64, 3, 8, false>"
+    assert s["kernels"][k10]["calls"] == 2 and s["kernels"][k10]["avg_ns"] == 50   # sweeps 4, 6
+    assert s["kernels"][k8]["calls"] == 1 and s["kernels"][k8]["avg_ns"] == 50     # sweep 5
+    assert s["counters"][k10]["WRITE_SIZE"]["avg_per_dispatch"] == 50
+    assert s["kernels"]["k_apply"]["calls"] == 3

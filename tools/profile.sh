@@ -2,21 +2,23 @@
 # usage: LABEL=x BENCH_ARGS="--config c5" bash tools/profile.sh
 # The command is the bench's own (its --steps / --warmup / --burnin, default
 # 10 / 3 / 0), and the summaries skip each kernel's first burnin + warmup
-# dispatches, so the counters and durations describe the bench's timed sweeps.
+# dispatches and keep the next --steps, so the counters and durations
+# describe the bench's timed sweeps (--no-estimate: the side figure's
+# estimate() runs after the timed region and would dilute the averages).
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
 P=gpurun_out/prof_${LABEL:-run}
 mkdir -p $P
 STEPS=${STEPS:-10}; WARMUP=${WARMUP:-3}; BURNIN=${BURNIN:-0}
-B="python3 bench.py --steps $STEPS --warmup $WARMUP --burnin $BURNIN --no-cpu-baseline ${BENCH_ARGS:-}"
+B="python3 bench.py --steps $STEPS --warmup $WARMUP --burnin $BURNIN --no-cpu-baseline --no-estimate ${BENCH_ARGS:-}"
 SKIP=$((WARMUP + BURNIN))
 PER_SWEEP=${PER_SWEEP:-1}   # sampler launches per sweep (--exchange-parts P: P)
 SEL='--kernel-include-regex k_sample|k_apply|k_prepare|k_count|k_build|k_recount'
 run() {  # name, rocprof args...
   local name=$1; shift
   timeout -k 10 600 rocprofv3 "$@" -d $P/$name -o $name --output-format csv -- $B > $P/$name.log 2>&1 || { echo "$name FAILED"; tail -20 $P/$name.log; return 1; }
-  python3 tools/summarize_prof.py $P/$name $P/summary_$name.json $SKIP $PER_SWEEP && cp $P/$name/*kernel_stats.csv $P/ 2>/dev/null; rm -rf $P/$name
+  python3 tools/summarize_prof.py $P/$name $P/summary_$name.json $SKIP $PER_SWEEP $STEPS && cp $P/$name/*kernel_stats.csv $P/ 2>/dev/null; rm -rf $P/$name
   echo "$name ok"
 }
 PASSES=${PASSES:-"kt fetch write sq lat tcc ea lds"}

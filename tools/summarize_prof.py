@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Condense rocprofv3 CSV output into small per-kernel summaries.
 
-  summarize_prof.py <prof_dir> <out.json> [skip_sweeps] [dispatches_per_sweep]
+  summarize_prof.py <prof_dir> <out.json> [skip_sweeps] [dispatches_per_sweep] [keep_sweeps]
 
 skip_sweeps: leave out each kernel's dispatches of the first `skip_sweeps`
 sweeps (in dispatch order), so that a profile of a bench command describes
@@ -10,6 +10,13 @@ command, tools/profile.sh).  dispatches_per_sweep (default 1): how many
 launches of a kernel one sweep makes -- the sampler launches once per part
 with --exchange-parts P (the skip had not been scaled, so split
 profiles kept near-init launches).  The summary records both.
+keep_sweeps (default 0 = all): keep only the next `keep_sweeps` sweeps'
+dispatches after the skipped ones -- the bench's --steps -- so work the
+bench command does after its timed region (the estimate() side figure) does
+not enter the averages.  The sampler kernels (k_sample*) are counted as ONE
+sequence in dispatch order, whatever their template arguments: the large-K
+sampler switches between two instantiations (ring depths) from sweep to
+sweep, and a per-name count would skip the wrong sweeps.
 
 Reads every *_kernel_stats.csv, *_kernel_trace.csv and
 *_counter_collection.csv under prof_dir and writes, per kernel name:
@@ -41,19 +48,42 @@ def short(name: str) -> str:
     return name.split("(")[0][:80]
 
 
-def main(prof_dir, out_path, skip=0, per_sweep=1):
-    skip_sweeps, per_sweep = int(skip), max(1, int(per_sweep))
-    skip = skip_sweeps * per_sweep
+def window(items, skip, keep):
+    """items: (order key, name, value); the kept (name, value) pairs: per
+    name, the dispatches past the first `skip` (and at most `keep`, 0 = all);
+    the sampler kernels form one sequence.  A name with nothing left keeps
+    all its dispatches (a kernel that runs only before the window)."""
+    out = defaultdict(list)
+    samp = sorted((o, n, v) for o, n, v in items if n.startswith("k_sample"))
+    rest = defaultdict(list)
+    for o, n, v in items:
+        if not n.startswith("k_sample"):
+            rest[n].append((o, v))
+    end = skip + keep if keep else None
+    sel = samp[skip:end]
+    for _, n, v in sel:
+        out[n].append(v)
+    for n in {n for _, n, _ in samp} - set(out):
+        out[n] = [v for o, nn, v in samp if nn == n]
+    for n, vs in rest.items():
+        vs = [v for _, v in sorted(vs)]
+        out[n] = vs[skip:end] or vs
+    return out
+
+
+def main(prof_dir, out_path, skip=0, per_sweep=1, keep=0):
+    skip_sweeps, per_sweep, keep_sweeps = int(skip), max(1, int(per_sweep)), int(keep)
+    skip, keep = skip_sweeps * per_sweep, keep_sweeps * per_sweep
     out = {"kernels": {}, "counters": {}, "skipped_sweeps": skip_sweeps,
-           "dispatches_per_sweep": per_sweep, "skipped_dispatches_per_kernel": skip}
+           "dispatches_per_sweep": per_sweep, "skipped_dispatches_per_kernel": skip,
+           "kept_sweeps": keep_sweeps}
     for path in glob.glob(os.path.join(prof_dir, "**", "*_kernel_trace.csv"), recursive=True):
-        agg = defaultdict(list)
+        items = []
         with open(path) as f:
             for row in csv.DictReader(f):
                 dur = int(row["End_Timestamp"]) - int(row["Start_Timestamp"])
-                agg[short(row["Kernel_Name"])].append((int(row["Start_Timestamp"]), dur))
-        for k, v in agg.items():
-            v = [d for _, d in sorted(v)[skip:]] or [d for _, d in sorted(v)]
+                items.append((int(row["Start_Timestamp"]), short(row["Kernel_Name"]), dur))
+        for k, v in window(items, skip, keep).items():
             v.sort()
             out["kernels"][k] = {
                 "calls": len(v),
@@ -71,14 +101,16 @@ def main(prof_dir, out_path, skip=0, per_sweep=1):
             for row in csv.DictReader(f):
                 agg[short(row["Kernel_Name"])][row["Counter_Name"]].append(
                     (int(row.get("Dispatch_Id", 0) or 0), float(row["Counter_Value"])))
+        by_counter = defaultdict(list)
         for k, ctrs in agg.items():
-            d = out["counters"].setdefault(k, {})
             for c, vals in ctrs.items():
                 per_dispatch = defaultdict(float)
                 for disp, v in vals:
                     per_dispatch[disp] += v
-                ids = sorted(per_dispatch)
-                xs = [per_dispatch[i] for i in (ids[skip:] or ids)]
+                by_counter[c] += [(i, k, x) for i, x in per_dispatch.items()]
+        for c, items in by_counter.items():
+            for k, xs in window(items, skip, keep).items():
+                d = out["counters"].setdefault(k, {})
                 d[c] = {"dispatches": len(xs), "avg_per_dispatch": sum(xs) / len(xs),
                         "min": min(xs), "max": max(xs)}
     for k, ctrs in out["counters"].items():
@@ -92,4 +124,4 @@ def main(prof_dir, out_path, skip=0, per_sweep=1):
 
 
 if __name__ == "__main__":
-    main(*sys.argv[1:5])
+    main(*sys.argv[1:6])
