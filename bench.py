@@ -323,6 +323,10 @@ def main():
     ap.add_argument("--int32-exchange", action="store_true",
                     help="N > 1: all-reduce the int32 exchange buffer instead of the compact "
                          "packed form (A/B)")
+    ap.add_argument("--force-exchange", action="store_true",
+                    help="N = 1: run the exchange anyway (an RCCL process group of one rank: the "
+                         "pack, the in-place all-reduce, the all-gather and the unpack, whose sum "
+                         "is the identity) to price the exchange's on-GPU cost; never the default")
     ap.add_argument("--reserve-cus", type=int, default=-1,
                     help="split sweeps: CUs' worth of sampler blocks left free for RCCL (-1: the library default, 1/32 of the CUs)")
     args = ap.parse_args()
@@ -347,6 +351,15 @@ def main():
             dist.init_process_group("nccl", device_id=torch.device("cuda", device))
         else:
             dist.init_process_group("gloo")
+    elif args.force_exchange:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        if "MASTER_PORT" not in os.environ:
+            import socket
+            with socket.socket() as so:
+                so.bind(("127.0.0.1", 0))
+                os.environ["MASTER_PORT"] = str(so.getsockname()[1])
+        dist.init_process_group(args.backend, rank=0, world_size=1,
+                                device_id=torch.device("cuda", device) if args.backend == "nccl" else None)
 
     from ldagibbssampling_amd.corpus import synthetic_lda_torch
     from ldagibbssampling_amd.distributed import ADLDATrainer
@@ -417,7 +430,8 @@ def main():
     if args.exchange_parts > 1:
         sampler.set_exchange_parts(args.exchange_parts, args.reserve_cus)
     trainer = ADLDATrainer(sampler, sync_before_reduce=False, time_reduce=True,
-                           compact=not args.int32_exchange)
+                           compact=not args.int32_exchange,
+                           exchange=True if args.force_exchange else None)
     trainer.init_counts()
 
     def step():
@@ -510,7 +524,7 @@ def main():
             bound_detail = ("word rows streamed from HBM (table larger than the Infinity Cache) "
                             "plus the token's dependency chain")
         coll = None
-        if world > 1:
+        if trainer.exchange:
             xb = trainer.exchange_bytes()
             nbytes = xb["allreduce_bytes"] + xb["allgather_bytes"]
             int32_bytes = 4 * (V * sampler.Kp + sampler.Kp)
@@ -540,6 +554,10 @@ def main():
                     # the last part's sampling
                     "ms_per_sweep": trainer.reduce_ms(args.steps),
                     "ms_kind": "collective" if parts == 1 else "exposed (after the last part)"}
+            if world == 1:
+                coll["forced_one_rank"] = ("--force-exchange: one RCCL rank, so ms_per_sweep is the "
+                                           "pack + unpack kernels and RCCL's one-rank calls, not a "
+                                           "transfer")
         result = {
             "metric": f"Gibbs tokens sampled/sec at K={K}",
             "value": value,
@@ -630,7 +648,7 @@ def main():
             result["cpu_baseline"] = cpu_baseline(corpus, K, alpha_sum, beta, args.cpu_budget)
         print(json.dumps(result), flush=True)
     sampler.close()
-    if world > 1:
+    if dist.is_initialized():
         dist.destroy_process_group()
 
 

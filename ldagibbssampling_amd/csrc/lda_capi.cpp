@@ -1151,7 +1151,8 @@ lda_status lda_delta_buffer_part(lda_ctx* c, int32_t part, void** dev_ptr, size_
 // ---- compact exchange
 static lda_status exchange_dims(lda_ctx* c, int32_t world, int64_t max_tokens, size_t* packed_count,
                                 size_t* escape_count, int32_t* cap) {
-  if (world < 2 || world > 16384) return fail(LDA_ERR_INVALID_ARG, "world must be in [2, 16384]");
+  // world 1: the sum is the identity (a one-rank run with the exchange forced on, to exercise it)
+  if (world < 1 || world > 16384) return fail(LDA_ERR_INVALID_ARG, "world must be in [1, 16384]");
   if (max_tokens < c->N) return fail(LDA_ERR_INVALID_ARG, "max_shard_tokens below this shard's tokens");
   // sum |cell| of one rank's buffer <= 2 x its tokens, so at most that over
   // the smaller bias can escape

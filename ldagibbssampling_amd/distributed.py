@@ -70,12 +70,17 @@ class ADLDATrainer:
     """
 
     def __init__(self, engine, group=None, sync_before_reduce: bool = True,
-                 time_reduce: bool = False, compact: bool = True):
+                 time_reduce: bool = False, compact: bool = True, exchange=None):
         """sync_before_reduce=False when the engine already launches on the
         stream the collective runs behind (GibbsSampler.set_stream(torch's
         current stream)): then no host synchronisation per sweep is needed.
         time_reduce: record CUDA events around every all-reduce on torch's
-        current stream (reduce_ms reads them after a synchronize)."""
+        current stream (reduce_ms reads them after a synchronize).
+        exchange: run the collectives (default: with more than one rank);
+        True on one rank puts the real backend's calls -- RCCL's in-place
+        all-reduce on the library's buffers, the all-gather, the pack and
+        unpack -- on the path of a one-GPU run, whose sums are then the
+        identity (tests/test_distributed_gpu.py)."""
         import torch.distributed as dist
 
         self.engine = engine
@@ -85,15 +90,16 @@ class ADLDATrainer:
         self.group = group
         self.dist = dist
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
-        self._delta = engine.delta_tensor() if self.world > 1 else None
+        self.exchange = self.world > 1 if exchange is None else bool(exchange and dist.is_initialized())
+        self._delta = engine.delta_tensor() if self.exchange else None
         self._part_deltas = {}
         self._initialised = False
         # the compact exchange needs engine.exchange_pack / exchange_unpack and
         # the largest shard's tokens (every rank sizes its escape list alike)
-        self.compact = bool(compact and self.world > 1 and hasattr(engine, "exchange_pack"))
+        self.compact = bool(compact and self.exchange and hasattr(engine, "exchange_pack"))
         self._esc_all = {}
         self.max_tokens = self._max_tokens() if self.compact else 0
-        if self.world > 1 and not sync_before_reduce:
+        if self.exchange and not sync_before_reduce:
             self._check_stream_order()
 
     def _check_stream_order(self):
@@ -180,7 +186,7 @@ class ADLDATrainer:
             torch.cuda.current_stream(self._delta.device).synchronize()
 
     def _reduce(self):
-        if self.world > 1:
+        if self.exchange:
             ev = None
             if self.time_reduce and self._delta.device.type == "cuda":
                 import torch
@@ -208,7 +214,7 @@ class ADLDATrainer:
         """Every rank must recount or keep a delta in the same sweeps (the
         buffers they sum hold counts or changes accordingly): the same mode,
         and for AUTO the smallest recount_sweeps of any rank."""
-        if self.world < 2 or not hasattr(self.engine, "count_update"):
+        if not self.exchange or not hasattr(self.engine, "count_update"):
             return
         import torch
         from . import capi
@@ -291,7 +297,7 @@ class ADLDATrainer:
             if seq:
                 self._sequential_sweep(parts)
                 continue
-            if self.world < 2:
+            if not self.exchange:
                 self.engine.sample()
             elif parts > 1:
                 self._split_sweep(parts)
@@ -306,7 +312,7 @@ class ADLDATrainer:
         import torch
 
         doc, word = self.engine.log_likelihood_parts()
-        if self.world > 1:
+        if self.exchange:
             dev = self._delta.device if self.dist.get_backend(self.group) == "nccl" else "cpu"
             t = torch.tensor([doc], dtype=torch.float64, device=dev)
             self.dist.all_reduce(t, op=self.dist.ReduceOp.SUM, group=self.group)

@@ -144,7 +144,7 @@ def test_default_mode_waits_for_async_collective(compact):
     ref = GibbsSampler(16, c.num_types, c.doc_off, c.words, 0.1, 0.01, seed=4)
     ref.sweep(0)
     tr = ADLDATrainer(g)                       # default: sync_before_reduce=True
-    tr.world = 2                               # as if sharded: reduce, then apply
+    tr.world, tr.exchange = 2, True            # as if sharded: reduce, then apply
     tr._delta = g.delta_tensor()
     Kp = g.Kp
     if compact:
@@ -165,3 +165,67 @@ def test_default_mode_waits_for_async_collective(compact):
     np.testing.assert_array_equal(nwsum, rnwsum)
     g.synchronize()
     assert int(g.delta_tensor().abs().sum()) == 0      # nothing landed after the apply
+
+
+def _rccl_worker(rank, port, outdir, stream_ordered, parts, compact):
+    sys.path.insert(0, ROOT)
+    import torch
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    from ldagibbssampling_amd.distributed import ADLDATrainer
+    from ldagibbssampling_amd.sampler import GibbsSampler
+    c = _corpus()
+    g = GibbsSampler(K, c.num_types, c.doc_off, c.words, 0.1, 0.01, seed=SEED)
+    if parts > 1:
+        g.set_exchange_parts(parts, reserve_cus=8)
+    if stream_ordered:
+        st = torch.cuda.Stream()
+        torch.cuda.set_stream(st)
+        g.set_stream(st.cuda_stream)
+    tr = ADLDATrainer(g, sync_before_reduce=not stream_ordered, compact=compact, exchange=True,
+                      time_reduce=True)
+    assert tr.exchange and tr.compact == compact
+    tr.sweep(SWEEPS)
+    ll = tr.log_likelihood()
+    torch.cuda.synchronize()
+    assert tr.reduce_ms(SWEEPS) is not None          # the collectives ran
+    nw, nwsum, _, _ = g.counts()
+    np.savez(os.path.join(outdir, "r0.npz"), z=g.z(), nw=nw, nwsum=nwsum, ll=ll,
+             bytes=tr.exchange_bytes()["allreduce_bytes"])
+    g.close()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("stream_ordered,parts,compact", [(True, 1, True), (False, 1, True), (True, 2, True),
+                                                          (True, 1, False)])
+def test_rccl_exchange_one_rank(oracle, stream_ordered, parts, compact):
+    """The RCCL path bench.py takes at N > 1 (torch.distributed "nccl"),
+    exercised on the one-GPU box with one rank and the exchange forced on:
+    process-group init on the device, the in-place SUM all-reduce of the
+    library's packed (or int32) buffer, the all-gather of the escape lists,
+    the pack / unpack kernels, stream-ordered and host-synchronised, split
+    sweeps.  One rank's sum is the identity, so the chain must equal the
+    oracle bit for bit -- a wrong stream order, size or dtype at the RCCL
+    boundary shows up as a difference."""
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    with tempfile.TemporaryDirectory() as d:
+        mp.start_processes(_rccl_worker, args=(port, d, stream_ordered, parts, compact), nprocs=1,
+                           start_method="spawn")
+        r = np.load(os.path.join(d, "r0.npz"))
+    c = _corpus()
+    o = oracle.ExactSampler(K, c.num_types, c.doc_off, c.words, 0.1, 0.01, SEED)
+    o.sweep(SWEEPS)
+    np.testing.assert_array_equal(r["z"], o.z())
+    nw, nwsum, _, _ = o.counts()
+    np.testing.assert_array_equal(r["nw"], nw)
+    np.testing.assert_array_equal(r["nwsum"], nwsum)
+    assert abs(float(r["ll"]) - o.log_likelihood()) < 1e-9 * abs(o.log_likelihood())
+    vk, kp = c.num_types * 128, 128
+    # compact: two nw cells per int32 word, the nwsum part as raw int32
+    assert int(r["bytes"]) == (4 * (vk // 2 + kp) if compact else 4 * (vk + kp))
