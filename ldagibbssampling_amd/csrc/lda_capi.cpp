@@ -267,6 +267,7 @@ struct lda_ctx {
   int64_t big_hold = 0;              // sweeps left before the next probe
   hipEvent_t big_ev[3][2] = {};
   bool rows_ready = false;
+  bool fused_apply = true;   // k_apply_build (LDA_FUSED_APPLY=0: k_apply_cols + k_build_sparse, A/B)
   int half = 0;    // dense K <= 128: 1 = the half-wave variant, 2 = the quarter-wave one (LDA_DENSE_HALF)
   // lda_infer: word totals of the snapshot (TopicInferencer's empty-row test),
   // valid while apply_gen == totals_gen, and grow-only scratch buffers, so a
@@ -606,6 +607,17 @@ static lda_status apply_impl(lda_ctx* c) {
   // initial counts of k_count, an exchange's sum) is the same column sum, so
   // it is dropped and recomputed
   HIP_TRY(hipMemsetAsync(c->delta + (int64_t)c->V * c->Kp, 0, sizeof(int32_t) * c->Kp, c->stream));
+  if (c->sampler == LDA_SAMPLER_SPARSE && c->rows_ready && c->fused_apply) {
+    // one pass: apply, column sums, sparse rows (k_apply_build); then the
+    // topic tables from the column sums
+    HIP_TRY(lda::launch_apply_build(c->nw, c->delta, c->V, c->Kp, c->row_off, c->ent, c->row_nnz,
+                                    c->delta + (int64_t)c->V * c->Kp, c->stream));
+    HIP_TRY(lda::launch_prepare_topics(c->nwsum, c->delta + (int64_t)c->V * c->Kp, c->alpha_d,
+                                       c->beta, (double)c->V * c->beta, c->K, c->Kp, c->alpha_f,
+                                       c->inv, c->inv_m1, c->stream));
+    c->pending = false;
+    return LDA_OK;
+  }
   HIP_TRY(lda::launch_apply_cols(c->nw, c->delta, c->V, c->Kp, c->delta + (int64_t)c->V * c->Kp, c->stream));
   HIP_TRY(lda::launch_prepare_topics(c->nwsum, c->delta + (int64_t)c->V * c->Kp, c->alpha_d,
                                      c->beta, (double)c->V * c->beta, c->K, c->Kp, c->alpha_f,
@@ -823,6 +835,8 @@ lda_status lda_create(lda_ctx** out, const lda_config* cfg, const int64_t* doc_o
   {
     const char* gv = std::getenv("LDA_GRAPHS");
     c->use_graphs = !(gv && gv[0] == '0');
+    const char* fav = std::getenv("LDA_FUSED_APPLY");
+    c->fused_apply = !(fav && fav[0] == '0');
     const char* rbv = std::getenv("LDA_SB_RB");
     if (rbv && rbv[0]) {
       c->big_rb_auto = false;

@@ -116,6 +116,11 @@ int sample_sparse_blocks_per_cu(int C, bool frozen);
 hipError_t launch_row_caps(const int32_t* nw, int64_t V, int32_t Kp, int32_t* caps, hipStream_t st);
 hipError_t launch_build_sparse(const int32_t* nw, int64_t V, int32_t Kp, const int64_t* row_off,
                                uint32_t* ent, int32_t* row_nnz, hipStream_t st);
+// the sparse samplers' apply + row build in one pass (rows already sized:
+// build_row_capacity): nw += delta, delta = 0, dsum += the delta's column
+// sums, the sparse entries and row_nnz of every row
+hipError_t launch_apply_build(int32_t* nw, int32_t* delta, int64_t V, int32_t Kp, const int64_t* row_off,
+                              uint32_t* ent, int32_t* row_nnz, int32_t* dsum, hipStream_t st);
 hipError_t launch_build_packed(const int32_t* nw, int64_t V, int32_t Kp, uint16_t* nw16,
                                uint8_t* wide, hipStream_t st);
 // per-topic state refreshed by an apply (k_prepare_topics' arguments)

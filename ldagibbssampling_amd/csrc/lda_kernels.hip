@@ -2743,6 +2743,78 @@ __global__ __launch_bounds__(256) void k_apply_cols(int4* __restrict__ nw, int4*
   if (acc.w) atomicAdd(ds + 3, acc.w);
 }
 
+// The sparse samplers' apply fused with the row build (round 4): one wave per
+// word row reads its nw and delta rows once, writes nw += delta and delta = 0
+// for the int4 groups that changed, accumulates the column sums of the delta
+// (the nwsum delta) in lane-private LDS words, and builds the row's sparse
+// entries from the updated counts still in registers -- k_apply_cols +
+// k_build_sparse without the second full read of nw.  Lane l owns topics
+// [l*C, l*C+C), as k_build_sparse.  At the end the block's waves add their
+// column sums and one atomic per nonzero column goes to dsum.
+template <int C>
+__global__ __launch_bounds__(256) void k_apply_build(int32_t* __restrict__ nw, int32_t* __restrict__ delta,
+                                                     int64_t V, const int64_t* __restrict__ row_off,
+                                                     uint32_t* __restrict__ ent, int32_t* __restrict__ row_nnz,
+                                                     int32_t* __restrict__ dsum) {
+  constexpr int KP = C * 64;
+  extern __shared__ __attribute__((aligned(16))) int32_t smem[];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  int32_t* cs = smem + wid * KP + lane * C;          // this lane's column sums
+#pragma unroll
+  for (int j = 0; j < C; ++j) cs[j] = 0;
+  for (int64_t w = (int64_t)blockIdx.x * 4 + wid; w < V; w += (int64_t)gridDim.x * 4) {
+    int32_t c[C], d[C];
+    int32_t* nrow = nw + w * KP + lane * C;
+    int32_t* drow = delta + w * KP + lane * C;
+    load_row<C>(c, nrow);
+    load_row<C>(d, drow);
+#pragma unroll
+    for (int q = 0; q < (C + 3) / 4; ++q) {
+      const int n = C < 4 ? C : 4;
+      bool ch = false;
+#pragma unroll
+      for (int i = 0; i < n; ++i) ch |= d[4 * q + i] != 0;
+      if (ch) {
+#pragma unroll
+        for (int i = 0; i < n; ++i) {
+          c[4 * q + i] += d[4 * q + i];
+          nrow[4 * q + i] = c[4 * q + i];
+          drow[4 * q + i] = 0;
+          cs[4 * q + i] += d[4 * q + i];
+        }
+      }
+    }
+    int cnt = 0;
+    bool sat = false;
+#pragma unroll
+    for (int j = 0; j < C; ++j) {
+      cnt += c[j] > 0 ? 1 : 0;
+      sat |= (uint32_t)c[j] >= ENT_COUNT_SAT;
+    }
+    const bool row_sat = __ballot(sat) != 0;
+    const int incl = wave_incl_scan_i(cnt);
+    int pos = incl - cnt;
+    const int64_t o = row_off[w];
+#pragma unroll
+    for (int j = 0; j < C; ++j) {
+      if (c[j] > 0) {
+        const uint32_t cc = (uint32_t)c[j] >= ENT_COUNT_SAT ? ENT_COUNT_SAT : (uint32_t)c[j];
+        ent[o + pos] = (cc << ENT_TOPIC_BITS) | (uint32_t)(lane * C + j);
+        ++pos;
+      }
+    }
+    const int nnz = __shfl(incl, 63);
+    const int pad_end = (nnz + 63) & ~63;
+    if (nnz + lane < pad_end) ent[o + nnz + lane] = 0u;
+    if (lane == 63) row_nnz[w] = row_sat ? (int32_t)((uint32_t)incl | 0x80000000u) : incl;
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < KP; i += 256) {
+    const int v = smem[i] + smem[KP + i] + smem[2 * KP + i] + smem[3 * KP + i];
+    if (v != 0) atomicAdd(&dsum[i], v);
+  }
+}
+
 // ---- compact exchange (lda_exchange_pack / lda_exchange_unpack)
 // Two exchange cells per int32 word, biased so that the SUM over `world`
 // ranks cannot carry between the halves: cell 2i as d + b0 in bits 0..15
@@ -3592,6 +3664,35 @@ hipError_t launch_apply_cols(int32_t* nw, int32_t* delta, int64_t V, int32_t Kp,
   hipLaunchKernelGGL(k_apply_cols, dim3(blocks), dim3(256), 0, st, reinterpret_cast<int4*>(nw),
                      reinterpret_cast<int4*>(delta), n4, dsum, kp4);
   return hipGetLastError();
+}
+
+template <int C>
+static hipError_t launch_apply_build_t(int32_t* nw, int32_t* delta, int64_t V, const int64_t* row_off,
+                                       uint32_t* ent, int32_t* row_nnz, int32_t* dsum, hipStream_t st) {
+  constexpr size_t lds = 4 * 64 * C * sizeof(int32_t);
+  static bool attr = [] {
+    return hipFuncSetAttribute(reinterpret_cast<const void*>(&k_apply_build<C>),
+                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) == hipSuccess;
+  }();
+  (void)attr;
+  const int blocks = (int)std::min<int64_t>((V + 3) / 4, 2048);
+  hipLaunchKernelGGL(k_apply_build<C>, dim3(blocks), dim3(256), lds, st, nw, delta, V, row_off, ent, row_nnz,
+                     dsum);
+  return hipGetLastError();
+}
+hipError_t launch_apply_build(int32_t* nw, int32_t* delta, int64_t V, int32_t Kp, const int64_t* row_off,
+                              uint32_t* ent, int32_t* row_nnz, int32_t* dsum, hipStream_t st) {
+  if (V <= 0) return hipSuccess;
+  switch (Kp / 64) {
+    case 1: return launch_apply_build_t<1>(nw, delta, V, row_off, ent, row_nnz, dsum, st);
+    case 2: return launch_apply_build_t<2>(nw, delta, V, row_off, ent, row_nnz, dsum, st);
+    case 4: return launch_apply_build_t<4>(nw, delta, V, row_off, ent, row_nnz, dsum, st);
+    case 8: return launch_apply_build_t<8>(nw, delta, V, row_off, ent, row_nnz, dsum, st);
+    case 16: return launch_apply_build_t<16>(nw, delta, V, row_off, ent, row_nnz, dsum, st);
+    case 32: return launch_apply_build_t<32>(nw, delta, V, row_off, ent, row_nnz, dsum, st);
+    case 64: return launch_apply_build_t<64>(nw, delta, V, row_off, ent, row_nnz, dsum, st);
+    default: return hipErrorInvalidValue;
+  }
 }
 
 hipError_t launch_exch_pack(const int32_t* buf, int64_t cells, int32_t* packed, int32_t world,
