@@ -106,8 +106,8 @@ lda_status lda_sweep(lda_ctx* ctx, int32_t n);
  * buffer below.  Asynchronous on the context's stream, except that the
  * large-K sampler (K > 1024) times its two ring depths from the ninth sweep
  * on, every 19 sweeps: the sweep after such a probe waits on the host for
- * the probe's last launch (LDA_SB_RB=10 or 8 at
- * lda_create fixes the depth and never waits).  Either depth gives the same
+ * the probe's last launch (LDA_SB_RB=short or default at
+ * lda_create fixes the ring and never waits).  Either ring gives the same
  * draws. */
 lda_status lda_sample(lda_ctx* ctx);
 /* Device pointer to the pending exchange buffer: int32[V*Kp + Kp] (an nw part

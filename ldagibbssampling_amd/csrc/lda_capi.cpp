@@ -837,10 +837,13 @@ lda_status lda_create(lda_ctx** out, const lda_config* cfg, const int64_t* doc_o
     c->use_graphs = !(gv && gv[0] == '0');
     const char* fav = std::getenv("LDA_FUSED_APPLY");
     c->fused_apply = !(fav && fav[0] == '0');
+    // LDA_SB_RB=short (or the short ring's rounds) / default (or any other
+    // number): the large-K ring fixed instead of timed
     const char* rbv = std::getenv("LDA_SB_RB");
     if (rbv && rbv[0]) {
       c->big_rb_auto = false;
-      c->big_rb = std::atoi(rbv) == lda::SB_RB_SHORT_ROUNDS ? lda::SB_RB_SHORT_ROUNDS : 0;
+      const bool shrt = std::strcmp(rbv, "short") == 0 || std::atoi(rbv) == lda::SB_RB_SHORT_ROUNDS;
+      c->big_rb = shrt ? lda::SB_RB_SHORT_ROUNDS : 0;
     }
     const char* zv = std::getenv("LDA_ZW");
     c->use_zw = !(zv && zv[0] == '0');

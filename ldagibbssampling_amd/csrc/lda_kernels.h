@@ -110,7 +110,7 @@ int quarter_topics_per_lane(int K);
 // the short one for short rows (SB_RB_SHORT in lda_kernels.hip)
 hipError_t launch_sample_sparse(int C, bool frozen, const SampleParams& p, int blocks,
                                 hipStream_t st, int rb = 0);
-constexpr int SB_RB_SHORT_ROUNDS = 8;   // the short depth's rounds (SB_RB_SHORT's default)
+constexpr int SB_RB_SHORT_ROUNDS = 6;   // the short ring's rounds (SB_RB_SHORT's default)
 int sample_sparse_blocks_per_cu(int C, bool frozen);
 // row totals of nw (saturating at Kp) -> host prefix -> capacity offsets
 hipError_t launch_row_caps(const int32_t* nw, int64_t V, int32_t Kp, int32_t* caps, hipStream_t st);

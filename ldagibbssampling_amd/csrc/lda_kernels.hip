@@ -1843,15 +1843,16 @@ __global__ __launch_bounds__(256) void k_sample_sparse(SampleParams p) {
 #ifndef SB_RB
 #define SB_RB 10
 #endif
-// the ring's depth for short rows (round 4: 8 register rounds were +2% on
-// C5 after burn-in and -3% on its longer rows near init, so the host times
-// both depths from time to time and keeps the faster: lda_capi.cpp)
+// the ring for short rows (round 4): 6 register rounds in 4 slots (the
+// same 24 VGPRs as 8 x 3, one token deeper) was +0.7% over 8 x 3 on C5 after
+// burn-in (profiles/r04/c5_short_ring/), and 8 x 3 +2% over the default
+// 10 x 3 there, -3% on the longer rows near init: the host times both rings
+// from time to time and keeps the faster (lda_capi.cpp)
 #ifndef SB_RB_SHORT
-#define SB_RB_SHORT 8
+#define SB_RB_SHORT 6
 #endif
-// the ring's slots at the short depth
 #ifndef SB_NS_SHORT
-#define SB_NS_SHORT SB_NS
+#define SB_NS_SHORT 4
 #endif
 #ifndef SB_BATCH
 #define SB_BATCH 4

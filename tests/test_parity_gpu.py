@@ -471,15 +471,15 @@ def test_dense_half_wave_variant(oracle, K, variant, monkeypatch):
     np.testing.assert_allclose(tg, to, rtol=0, atol=1e-12)
 
 
-@pytest.mark.parametrize("ring", ["8", "10", "auto"])
+@pytest.mark.parametrize("ring", ["short", "default", "auto"])
 def test_large_k_sparse_very_long_rows(oracle, monkeypatch, ring):
     """Word rows far longer than the register rounds (K = 4096): rows of up
     to ~3500 entries, so a draw can land in the register rounds, in either of
     the batches whose running sums are kept, or past them (the re-read of
     the rest of the selected lane), and the sparse rows are padded to whole
-    64-entry rounds.  ring: the sampler's register rounds, fixed at 8 or 10
-    (LDA_SB_RB) or chosen per sweep from the rows' mean rounds (round 4):
-    the same sums in the same order, so the same draws."""
+    64-entry rounds.  ring: the sampler's ring, fixed at the short (6 rounds
+    x 4 slots) or the default (10 x 3) one (LDA_SB_RB) or chosen by timing
+    both (round 4): the same sums in the same order, so the same draws."""
     if ring != "auto":
         monkeypatch.setenv("LDA_SB_RB", ring)
     from ldagibbssampling_amd.corpus import Corpus
