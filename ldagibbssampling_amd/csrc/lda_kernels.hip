@@ -1840,8 +1840,11 @@ __global__ __launch_bounds__(256) void k_sample_sparse(SampleParams p) {
 // so the selected lane's prefix search over them is one compare per round
 // (no re-walk); only rounds >= SB_RB of long rows are re-read, one per lane.
 // The sums and their order are those of oracle exact_draw_sparse.
+// the long-row ring: 12 register rounds in 2 slots (round 4: +0.6% near
+// init over 10 x 3 with the fused apply, profiles/r04/c5_long_ring/; 14 x 2
+// the same, 11 x 2 -0.4%, 9 x 3 -2.5%)
 #ifndef SB_RB
-#define SB_RB 10
+#define SB_RB 12
 #endif
 // the ring for short rows (round 4): 6 register rounds in 4 slots (the
 // same 24 VGPRs as 8 x 3, one token deeper) was +0.7% over 8 x 3 on C5 after
@@ -1858,7 +1861,7 @@ __global__ __launch_bounds__(256) void k_sample_sparse(SampleParams p) {
 #define SB_BATCH 4
 #endif
 #ifndef SB_NS
-#define SB_NS 3
+#define SB_NS 2
 #endif
 #ifndef SB_GRP
 #define SB_GRP 1
