@@ -478,7 +478,7 @@ def test_large_k_sparse_very_long_rows(oracle, monkeypatch, ring):
     the batches whose running sums are kept, or past them (the re-read of
     the rest of the selected lane), and the sparse rows are padded to whole
     64-entry rounds.  ring: the sampler's ring, fixed at the short (6 rounds
-    x 4 slots) or the default (10 x 3) one (LDA_SB_RB) or chosen by timing
+    x 4 slots) or the default (12 x 2) one (LDA_SB_RB) or chosen by timing
     both (round 4): the same sums in the same order, so the same draws."""
     if ring != "auto":
         monkeypatch.setenv("LDA_SB_RB", ring)
