@@ -182,12 +182,17 @@ def cpu_share() -> int:
         return os.cpu_count() or 1
 
 
-def cpu_baseline(corpus, K, alpha_sum, beta, budget_s=15.0, threads=4):
+def cpu_baseline(corpus, K, alpha_sum, beta, budget_s=15.0, threads=4, runs=3):
     """cpu_mallet (oracle/, the Mallet 2.0.7 SparseLDA restatement) timed on a
     bounded sample of the same workload on this host's cores (SURVEY.md §8d,
     BASELINE.md: T = 1 and T = nproc): `threads` workers (the reference's
-    setNumThreads(4)) for ~budget_s, a single-thread run, and a run on every
-    core of this job's CPU share."""
+    setNumThreads(4)), a single thread, and every core of this job's CPU share.
+    Each leg is `runs` separate timed runs of ~budget_s / runs seconds, worker
+    t pinned to the t-th CPU of the job's affinity mask; a leg reports the
+    median and the spread (min, max) of its runs, and the multi-thread legs the
+    split of their time between the workers' sampling and Mallet's
+    single-threaded sumTypeTopicCounts merge (the share that caps their
+    speed-up over one thread)."""
     from oracle import oracle as O
     O.build()
     ndocs = min(corpus.num_docs, 20_000)
@@ -196,7 +201,9 @@ def cpu_baseline(corpus, K, alpha_sum, beta, budget_s=15.0, threads=4):
     def timed(T, budget, max_sweeps):
         m = O.MalletModel(K, alpha_sum, beta, corpus.num_types, sub.doc_off, sub.words, seed=1,
                           num_threads=T)
+        m.set_pin_threads(True)
         m.estimate(2)                                    # warm-up sweeps
+        m.timing(reset=True)
         t0 = time.perf_counter()
         sweeps = 0
         while True:
@@ -204,27 +211,42 @@ def cpu_baseline(corpus, K, alpha_sum, beta, budget_s=15.0, threads=4):
             sweeps += 1
             if time.perf_counter() - t0 >= budget or sweeps >= max_sweeps:
                 break
-        return sub.num_tokens * sweeps / (time.perf_counter() - t0), sweeps
+        dt = time.perf_counter() - t0
+        ts, tm = m.timing()
+        return sub.num_tokens * sweeps / dt, sweeps, tm / dt
 
-    v, sweeps = timed(threads, budget_s, 50)
-    v1, sweeps1 = timed(1, budget_s / 3, 20)
+    def leg(T, budget, max_sweeps):
+        r = [timed(T, budget / runs, max_sweeps) for _ in range(runs)]
+        v = sorted(x[0] for x in r)
+        return {"median": float(np.median(v)), "min": v[0], "max": v[-1], "runs": runs,
+                "sweeps": [x[1] for x in r], "merge_share": float(np.median([x[2] for x in r]))}
+
+    l4 = leg(threads, budget_s, 50)
+    l1 = leg(1, budget_s / 2, 20)
     tn = cpu_share()
-    vn, sweepsn = timed(tn, budget_s / 2, 50)
+    ln = leg(tn, budget_s / 2, 50)
     return {
-        "value": v,
+        "value": l4["median"],
         "unit": "tokens/s",
         "cores": threads,
         "kind": "port",
-        "t1_value": v1,
-        "tnproc_value": vn,
+        "spread": [l4["min"], l4["max"]],
+        "merge_share": l4["merge_share"],
+        "t1_value": l1["median"],
+        "t1_spread": [l1["min"], l1["max"]],
+        "tnproc_value": ln["median"],
+        "tnproc_spread": [ln["min"], ln["max"]],
+        "tnproc_merge_share": ln["merge_share"],
         "tnproc_cores": tn,
         "sample": (f"cpu_mallet (Mallet 2.0.7 SparseLDA restatement, oracle/lda_oracle.c), "
                    f"{threads} threads (= setNumThreads(4), src/cmu_ron/TrainAndPredict.java:164), "
-                   f"first {ndocs} docs ({sub.num_tokens} tokens) of this workload, "
-                   f"{sweeps} timed sweeps after 2 warm-up; t1_value: 1 thread, {sweeps1} sweeps; "
-                   f"tnproc_value: {tn} threads = this job's CPU share (OMP_NUM_THREADS, else the "
-                   f"affinity mask), {sweepsn} sweeps; host {_cpu_model()}, "
-                   f"{os.cpu_count()} logical CPUs visible"),
+                   f"first {ndocs} docs ({sub.num_tokens} tokens) of this workload; each leg {runs} runs "
+                   f"(2 warm-up sweeps, then timed sweeps: {l4['sweeps']} / 1 thread {l1['sweeps']} / "
+                   f"{tn} threads {ln['sweeps']}), median reported with [min, max] spread, worker t pinned "
+                   f"to the t-th CPU of the job's affinity mask; merge_share = the fraction of the timed wall "
+                   f"time in Mallet's single-threaded sumTypeTopicCounts merge after each sweep; "
+                   f"tnproc: {tn} threads = this job's CPU share (OMP_NUM_THREADS, else the affinity mask); "
+                   f"host {_cpu_model()}, {os.cpu_count()} logical CPUs visible"),
     }
 
 

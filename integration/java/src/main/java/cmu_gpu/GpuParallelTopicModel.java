@@ -37,7 +37,18 @@ import cc.mallet.types.FeatureSequence;
 public class GpuParallelTopicModel extends ParallelTopicModel {
   private static final long serialVersionUID = 1L;
   private static final Logger logger = Logger.getLogger(GpuParallelTopicModel.class.getName());
-  static { System.loadLibrary("lda_mi355x_jni"); }
+
+  /**
+   * The native library, loaded on the first estimate() only: initialising
+   * this class (Java deserialization in the reference's load(),
+   * src/cmu_ron/TrainAndPredict.java:191-196, which predict() calls at :246)
+   * must work on a host without liblda_mi355x_jni.so, since prediction needs
+   * no GPU.  The JVM links the native method when it is first called.
+   */
+  private static final class NativeLibrary {
+    static { System.loadLibrary("lda_mi355x_jni"); }
+    static void load() {}
+  }
 
   private int gpuShards = 1;        // setNumThreads
   private long gpuSeed = -1;        // setRandomSeed (-1: time-seeded, as Mallet)
@@ -74,6 +85,7 @@ public class GpuParallelTopicModel extends ParallelTopicModel {
 
   @Override
   public void estimate() throws IOException {
+    NativeLibrary.load();
     final int D = data.size();
     long[] docOff = new long[D + 1];
     for (int d = 0; d < D; d++) {

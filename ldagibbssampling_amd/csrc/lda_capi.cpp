@@ -348,6 +348,8 @@ struct lda_ctx {
   float* alpha_f = nullptr;
   float* inv = nullptr;
   float* inv_m1 = nullptr;
+  // the large-K sampler's per-sweep tables (k_big_tables; C >= 32 sparse only)
+  lda::BigTables big{};
   double* partial = nullptr;
   unsigned long long* nonzero = nullptr;
   int partial_blocks = 1024;
@@ -420,7 +422,8 @@ struct lda_ctx {
                     (void*)inv, (void*)inv_m1, (void*)partial, (void*)nonzero, (void*)ent,
                     (void*)row_off, (void*)row_nnz, (void*)row_rnd, (void*)nw16, (void*)wide, (void*)inf_words,
                     (void*)inf_z, (void*)inf_acc, (void*)inf_q, (void*)inf_doff, (void*)inf_range,
-                    (void*)perm, (void*)items, (void*)warm.range_doc, (void*)steady.range_doc})
+                    (void*)perm, (void*)items, (void*)warm.range_doc, (void*)steady.range_doc,
+                    (void*)big.tab, (void*)big.tab_m1, (void*)big.F, (void*)big.pfx, (void*)big.scal})
       if (p) (void)hipFree(p);
     for (int i = 1; i < LDA_MAX_EXCHANGE_PARTS; ++i)
       if (delta_part[i]) (void)hipFree(delta_part[i]);
@@ -484,6 +487,7 @@ struct lda_ctx {
     p.row_rnd = row_rnd;
     p.nw16 = nw16;
     p.wide = wide;
+    p.big = big;
     (void)frozen;
     return p;
   }
@@ -584,6 +588,18 @@ static lda_status build_recount_index(lda_ctx* c) {
   return LDA_OK;
 }
 
+// nwsum += its pending delta and the per-topic tables (k_prepare_topics),
+// then the large-K sampler's fixed-point tables from them
+static hipError_t prepare_tables(lda_ctx* c) {
+  hipError_t e = lda::launch_prepare_topics(c->nwsum, c->delta + (int64_t)c->V * c->Kp, c->alpha_d, c->beta,
+                                            (double)c->V * c->beta, c->K, c->Kp, c->alpha_f, c->inv,
+                                            c->inv_m1, c->stream);
+  if (e == hipSuccess && c->big.tab)
+    e = lda::launch_big_tables(c->nwsum, c->alpha_f, c->inv, c->inv_m1, c->K, c->Kp, (float)c->beta, c->big,
+                               c->stream);
+  return e;
+}
+
 static lda_status apply_impl(lda_ctx* c) {
   if (c->next_part != 0 && !c->sweep_seq)
     return fail(LDA_ERR_STATE, "lda_apply inside a split sweep: sample every part first");
@@ -612,16 +628,12 @@ static lda_status apply_impl(lda_ctx* c) {
     // topic tables from the column sums
     HIP_TRY(lda::launch_apply_build(c->nw, c->delta, c->V, c->Kp, c->row_off, c->ent, c->row_nnz,
                                     c->delta + (int64_t)c->V * c->Kp, c->stream));
-    HIP_TRY(lda::launch_prepare_topics(c->nwsum, c->delta + (int64_t)c->V * c->Kp, c->alpha_d,
-                                       c->beta, (double)c->V * c->beta, c->K, c->Kp, c->alpha_f,
-                                       c->inv, c->inv_m1, c->stream));
+    HIP_TRY(prepare_tables(c));
     c->pending = false;
     return LDA_OK;
   }
   HIP_TRY(lda::launch_apply_cols(c->nw, c->delta, c->V, c->Kp, c->delta + (int64_t)c->V * c->Kp, c->stream));
-  HIP_TRY(lda::launch_prepare_topics(c->nwsum, c->delta + (int64_t)c->V * c->Kp, c->alpha_d,
-                                     c->beta, (double)c->V * c->beta, c->K, c->Kp, c->alpha_f,
-                                     c->inv, c->inv_m1, c->stream));
+  HIP_TRY(prepare_tables(c));
   if (c->sampler == LDA_SAMPLER_SPARSE) {
     if (!c->rows_ready) {
       lda_status s = build_row_capacity(c);
@@ -830,6 +842,13 @@ lda_status lda_create(lda_ctx** out, const lda_config* cfg, const int64_t* doc_o
   CT(dalloc(&c->alpha_f, c->Kp));
   CT(dalloc(&c->inv, c->Kp));
   CT(dalloc(&c->inv_m1, c->Kp));
+  if (c->sampler == LDA_SAMPLER_SPARSE && c->C >= 32) {
+    CT(dalloc(&c->big.tab, c->Kp));
+    CT(dalloc(&c->big.tab_m1, c->Kp));
+    CT(dalloc(&c->big.F, c->Kp));
+    CT(dalloc(&c->big.pfx, c->Kp));
+    CT(dalloc(&c->big.scal, 1));
+  }
   CT(dalloc(&c->partial, c->partial_blocks));
   CT(dalloc(&c->state_dev, 4));
   {
@@ -1721,9 +1740,7 @@ lda_status lda_set_alpha_beta(lda_ctx* c, const double* alpha, double beta) {
   c->alpha_ev_live = true;
   // refresh the fp32 tables (the nwsum delta part is zero unless pending)
   if (!c->pending) {
-    HIP_TRY(lda::launch_prepare_topics(c->nwsum, c->delta + (int64_t)c->V * c->Kp, c->alpha_d,
-                                       c->beta, (double)c->V * c->beta, c->K, c->Kp, c->alpha_f,
-                                       c->inv, c->inv_m1, c->stream));
+    HIP_TRY(prepare_tables(c));
   }
   return LDA_OK;
   });

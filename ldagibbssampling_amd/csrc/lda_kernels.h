@@ -45,6 +45,25 @@ constexpr uint32_t STREAM_INFER = 2u;
 #define SPARSE_R0 2
 #endif
 
+// Per-sweep tables of the large-K sampler (k_big_tables, oracle
+// exact_big_tables): the fixed-point exponent S, sum_k G_k, beta 2^-S, 2^S / beta.
+struct BigScal {
+  int32_t S;
+  float bsig;               // beta 2^-S
+  uint64_t S0;
+  float bsig_hi;            // beta 2^(32-S)
+  int32_t pad;
+  double isig;              // 2^S / beta
+};
+struct BigTables {
+  float2* tab;              // [Kp] {inv, ainv = alpha * inv}
+  float4* tab_m1;           // [Kp] {inv_m1, alpha * inv_m1, bits of big_fix(inv_m1), bits of
+                            //  big_fix(alpha inv_m1) - big_fix(alpha inv)} (0 for a topic with no tokens)
+  uint32_t* F;              // [Kp] big_fix(inv)
+  uint64_t* pfx;            // [Kp] inclusive prefix of big_fix(ainv)
+  BigScal* scal;
+};
+
 struct SampleParams {
   const int32_t* words;     // [N] token stream (doc-contiguous)
   int32_t* z;               // [N] topic of each token (read old, write new)
@@ -82,6 +101,8 @@ struct SampleParams {
   // sampler, so the recount streams it instead of gathering z through perm
   int32_t* zw;
   const uint32_t* zpos;
+  // the large-K sampler's per-sweep tables (k_sample_big)
+  BigTables big;
 };
 
 // Tokens [tok[i], tok[i+1]) of a shard belong to exchange part i.
@@ -121,6 +142,9 @@ hipError_t launch_build_sparse(const int32_t* nw, int64_t V, int32_t Kp, const i
 // sums, the sparse entries and row_nnz of every row
 hipError_t launch_apply_build(int32_t* nw, int32_t* delta, int64_t V, int32_t Kp, const int64_t* row_off,
                               uint32_t* ent, int32_t* row_nnz, int32_t* dsum, hipStream_t st);
+// the large-K sampler's tables from the topic tables (after every k_prepare_topics)
+hipError_t launch_big_tables(const int32_t* nwsum, const float* alpha_f, const float* inv, const float* inv_m1,
+                             int32_t K, int32_t Kp, float beta, const BigTables& t, hipStream_t st);
 hipError_t launch_build_packed(const int32_t* nw, int64_t V, int32_t Kp, uint16_t* nw16,
                                uint8_t* wide, hipStream_t st);
 // per-topic state refreshed by an apply (k_prepare_topics' arguments)

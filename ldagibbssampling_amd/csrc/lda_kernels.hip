@@ -28,6 +28,7 @@
 // explicit __builtin_fmaf below.
 #include <hip/hip_runtime.h>
 
+#include <cstddef>
 #include <cstdint>
 
 #include "lda_kernels.h"
@@ -108,8 +109,9 @@ __device__ __forceinline__ float dpp_mov(float v) {
 #ifndef LDA_WORD_FLAG
 #define LDA_WORD_FLAG 1
 #endif
-// s_waitcnt vmcnt(0) (gfx9 encoding: expcnt and lgkmcnt left at their maxima)
+// s_waitcnt vmcnt(0) / vmcnt(1) (gfx9 encoding: expcnt and lgkmcnt left at their maxima)
 constexpr int kVmcnt0 = 0x0F70;
+constexpr int kVmcnt1 = 0x0F71;
 // (a != b) ? m : 0 as s_cmp + s_cselect_b64
 __device__ __forceinline__ uint64_t select_mask_ne(int a, int b, uint64_t m) {
   uint64_t r;
@@ -1815,269 +1817,280 @@ __global__ __launch_bounds__(256) void k_sample_sparse(SampleParams p) {
 }
 
 // ------------------------------------------- the large-K sparse sampler
-// K up to 4096 (C = 32, 64): the draw of k_sample_sparse with the doc part's
-// lane partials split into groups of 16 topics.  A group's partial is the
-// Hillis-Steele inclusive scan of coef*beta across one 16-lane DPP row
-// (oracle/lda_oracle.c:group_rowscan16), so re-evaluating a changed group is
-// one row pass for the whole wave, and the A-part search over the selected
-// lane's C topics is one pass over NG rows plus a ballot.  LDS holds a
-// per-block float2 {alpha, inv} table and per-wave 16-bit document counts
-// (documents < 65536 tokens); coefficients are recomputed where used, which
-// keeps 16 waves per CU resident.
+// K up to 4096 (C = 32, 64), round 5 (v9).  The draw (oracle/lda_oracle.c:
+// exact_draw_big) splits p_k = (nd_k + a_k)(nw_k + b) inv_k into
+//   B, the word part, over the word's nonzero entries (lane l holds entries
+//     l, l+64, ...): coef_t = fma(nd_t, inv_t, ainv_t), acc = fma(c, coef, acc)
+//     -- one fma chain per entry and no own-token test per entry: the
+//     token's own entry enters B uncorrected and is corrected afterwards by
+//     an exact accept / re-draw step (below);
+//   A, the doc part beta * sum_k (nd_k + a_k) inv'_k, held EXACTLY as a
+//     64-bit fixed-point sum: sum_k G'_k (per sweep, k_big_tables) plus
+//     R = sum_k nd_k F_k, which a token updates with two integer adds (the
+//     previous token's new topic in, this token's old topic out).
+// So a token's fixed work is a handful of scalar-ish operations where v8
+// re-evaluated and re-scanned three 16-topic groups of the doc part per token
+// (~60 VALU), and a word entry costs ~8 VALU + 2 LDS reads instead of ~14.
 //
-// The word part streams its rounds of 64 entries.  Rows are padded with zero
-// entries to whole rounds (k_build_sparse), so every round is one full-wave
-// load and a padding entry adds +0 (its count is 0; the own-token correction
-// saturates at 0, and a real entry of topic z_old always has a count >= 1).
-// The first SB_RB rounds of the next tokens sit in a ring of SB_NS slots.  The
-// slot of token t-1 is refilled with token t+SB_NS-1 right AFTER token t has
-// consumed its own rounds: vmcnt counts loads in issue order, so every wait in
-// token t then covers loads issued at least one token earlier (refilling at
-// the end of a token, the first use in the next token waited for the load
-// just issued).  Count changes go out per 64-token chunk (lane i: token i),
-// not per token, so no atomics sit between a refill and the next wait.
-// Each lane keeps its running B sum after each of the SB_RB register rounds,
-// so the selected lane's prefix search over them is one compare per round
-// (no re-walk); only rounds >= SB_RB of long rows are re-read, one per lane.
-// The sums and their order are those of oracle exact_draw_sparse.
-// the long-row ring: 12 register rounds in 2 slots (round 4: +0.6% near
-// init over 10 x 3 with the fused apply, profiles/r04/c5_long_ring/; 14 x 2
-// the same, 11 x 2 -0.4%, 9 x 3 -2.5%)
+// The own token.  B holds its entry as x = c * coef_zo; the exact weight of
+// that entry is O = (c - 1) * fma(nd_zo, inv_m1_zo, ainv_m1_zo) <= x (c <=
+// nwsum).  A draw that lands in the entry keeps zo with probability O / w
+// (w = the entry's width in its lane's running sums); otherwise the draw is
+// repeated once over the same sums with the entry's width replaced by O
+// (the second uniform mapped around the entry).  Together that is exactly
+// the corrected distribution; only draws that hit the own entry pay for it.
+//
+// Work distribution and LDS are v8's: 16-wave blocks, a block-wide float2
+// {inv, ainv} table and per-wave 16-bit document counts (documents < 65536
+// tokens).  The word part streams rounds of 64 entries: the first RB rounds
+// of the next tokens sit in a ring of NS slots (refilled right after a token
+// has used its own rounds, so every wait covers loads issued at least one
+// token earlier), as bounded buffer loads whose range ends at the row's last
+// entry: the zero padding of a row's last round (k_build_sparse) is never
+// fetched.  Count changes go out per 64-token chunk (lane i: token i).
 #ifndef SB_RB
 #define SB_RB 12
 #endif
-// the ring for short rows (round 4): 6 register rounds in 4 slots (the
-// same 24 VGPRs as 8 x 3, one token deeper) was +0.7% over 8 x 3 on C5 after
-// burn-in (profiles/r04/c5_short_ring/), and 8 x 3 +2% over the default
-// 10 x 3 there, -3% on the longer rows near init: the host times both rings
-// from time to time and keeps the faster (lda_capi.cpp)
+#ifndef SB_NS
+#define SB_NS 2
+#endif
 #ifndef SB_RB_SHORT
 #define SB_RB_SHORT 6
 #endif
 #ifndef SB_NS_SHORT
 #define SB_NS_SHORT 4
 #endif
+// rows past the register rounds: batches of SB_BATCH rounds, double-buffered;
+// each lane keeps its running sum after each of the first SB_NB batches so a
+// draw in a long row re-reads one batch of the selected lane
 #ifndef SB_BATCH
 #define SB_BATCH 4
 #endif
-#ifndef SB_NS
-#define SB_NS 2
-#endif
-#ifndef SB_GRP
-#define SB_GRP 1
-#endif
-// batches whose per-lane end sums are kept for the draw's re-read
 #ifndef SB_NB
 #define SB_NB 2
 #endif
-// the batch loop specialised on the row's saturation flag (0: A/B baseline)
-#ifndef SB_SAT_SPLIT
-#define SB_SAT_SPLIT 1
+// 1: the ring refill of token t+NS-1 issued last in token t, after the
+// long-row batches and the draw's rare paths, whose loads are waited for
+// right after they are issued (in-order vmcnt: such a wait drains every older
+// load, the refill included when it was issued before them)
+#ifndef SB_REFILL_LAST
+#define SB_REFILL_LAST 0
 #endif
-// topic -> (lane, group) with unsigned shifts (signed / and % on the scalar
-// unit cost ~12 instructions per split)
-#ifndef SB_UDIV
-#define SB_UDIV 1
-#endif
-// the selected lane's round count as a per-lane vector count + one readlane
-// (a ballot + bit test + add per round on the scalar unit otherwise)
-#ifndef SB_VCOUNT
-#define SB_VCOUNT 1
-#endif
-// group-sum selects keyed by lane*NG + g in VGPRs (a scalar compare and
-// select per group element otherwise)
-#ifndef SB_TGKEY
-#define SB_TGKEY 1
-#endif
-// group-sum updates as one select under a scalar lane mask, the group by a
-// uniform switch (A/B: NG <= 4)
-#ifndef SB_TGMASK
-#define SB_TGMASK 0
-#endif
-// word-row loads as buffer loads bounded by the row (a load past it returns
-// 0 without a memory access): the ring prefetch is issued for every token
-// slot without a per-round branch, so every path round the loop issues the
-// same loads and the first round's wait need not drain the next token's
-// prefetch; the batches past the register rounds are double-buffered
-#ifndef SB_BUF
-#define SB_BUF 1
-#endif
-#ifndef SB_DBUF
-#define SB_DBUF SB_BUF
-#endif
-// the double-buffered batch loop runs whole batches only and sums the row's
-// last partial batch round by round (no zero rounds past the row's end)
-#ifndef SB_REM
-#define SB_REM 0
-#endif
-// row starts read as 32-bit round counts (row_rnd) instead of 64-bit offsets
-#ifndef SB_OFF32
-#define SB_OFF32 1
-#endif
-// A/B only: keep round 3's two per-token nwsum atomics (into a scratch
-// region: the sparse apply derives the nwsum delta itself)
-#ifndef SB_DSUM_ATOMICS
-#define SB_DSUM_ATOMICS 0
-#endif
-// the per-token document-count updates as no-return LDS atomics
-#ifndef SB_NDATOM
-#define SB_NDATOM 1
-#endif
-// the add-back of a token's new topic deferred to the next token of its
-// document and folded into that token's removal: one LDS update block and one
-// row pass per token (rows: the previous token's old and new groups, this
-// token's group) instead of two
-#ifndef SB_DEFER
-#define SB_DEFER 1
-#endif
-// rows that fill the register rounds: the rounds as one straight-line
-// sequence whose LDS operands (document count, {alpha, inv}) are read one
-// round ahead by hand (inline ds_read + counted lgkmcnt waits), so two
-// rounds' reads are in flight where the compiler waited for each round's
-// own (A/B)
-#ifndef SB_PIPE
-#define SB_PIPE 0
+// register rounds evaluated without a branch (the rest: one uniform branch
+// each); they share a basic block with the doc part's fixed-point chain
+#ifndef SB_RU
+#define SB_RU 2
 #endif
 // gfx9 buffer resource word 3 (raw 32-bit loads, bounds checked)
-[[maybe_unused]] constexpr int kBufWord3 = 0x00020000;
-static_assert(SB_RB % SB_GRP == 0 && (SB_DBUF || SB_BATCH % SB_GRP == 0), "round groups");
+constexpr int kBufWord3 = 0x00020000;
 #ifndef SB_WAVES
 #define SB_WAVES 16
 #endif
 template <int C>
 constexpr int sb_waves() { return SB_WAVES; }
 
+// Philox words x0, x1, x2 of a token's block, lane-parallel per 64-token
+// chunk (the large-K draw: x0 the draw, x1 the own-entry accept test, x2 the
+// rare re-draw; computed per token inside the re-draw branch, the compiler
+// hoisted the whole block into every token's scalar path)
+__device__ __forceinline__ void philox_x012(uint64_t gtok, uint32_t c2, uint32_t c3, uint32_t k0, uint32_t k1,
+                                            uint32_t& x0, uint32_t& x1, uint32_t& x2) {
+  uint32_t c0 = (uint32_t)gtok, c1 = (uint32_t)(gtok >> 32);
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    if (r > 0) {
+      k0 += PHILOX_W0;
+      k1 += PHILOX_W1;
+    }
+    const uint32_t hi0 = __umulhi(PHILOX_M0, c0), lo0 = PHILOX_M0 * c0;
+    const uint32_t hi1 = __umulhi(PHILOX_M1, c2), lo1 = PHILOX_M1 * c2;
+    const uint32_t n0 = hi1 ^ c1 ^ k0;
+    const uint32_t n2 = hi0 ^ c3 ^ k1;
+    c0 = n0;
+    c1 = lo1;
+    c2 = n2;
+    c3 = lo0;
+  }
+  x0 = c0;
+  x1 = c1;
+  x2 = c2;
+}
+__device__ __forceinline__ void philox_x01(uint64_t gtok, uint32_t c2, uint32_t c3, uint32_t k0, uint32_t k1,
+                                           uint32_t& x0, uint32_t& x1) {
+  uint32_t x2;
+  philox_x012(gtok, c2, c3, k0, k1, x0, x1, x2);
+}
+__device__ __forceinline__ float uniform_f(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, v)));
+}
+
+// floor(x) for 0 <= x < 2^64 (C's (uint64_t)x): both conversions truncate,
+// x - hi 2^32 is exact
+__device__ __forceinline__ uint64_t d2u64(double x) {
+  const uint32_t hi = (uint32_t)(x * 0x1p-32);
+  const uint32_t lo = (uint32_t)(x - (double)hi * 0x1p32);
+  return ((uint64_t)hi << 32) | lo;
+}
+__device__ __forceinline__ uint64_t uniform_u64(uint64_t v) { return (uint64_t)uniform_l((int64_t)v); }
+__device__ __forceinline__ uint64_t shfl_up_u64(uint64_t v, int d) {
+  const int lane = threadIdx.x & 63;
+  const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)v, lane - d < 0 ? lane : lane - d);
+  const uint32_t hi = (uint32_t)__shfl((int)(uint32_t)(v >> 32), lane - d < 0 ? lane : lane - d);
+  return lane >= d ? (((uint64_t)hi << 32) | lo) : 0ull;
+}
+// inclusive wave scan of 64-bit integers (exact in any order)
+__device__ __forceinline__ uint64_t wave_incl_scan_u64(uint64_t v) {
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) v += shfl_up_u64(v, d);
+  return v;
+}
+__device__ __forceinline__ uint64_t wave_sum_u64(uint64_t v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)v, o);
+    const uint32_t hi = (uint32_t)__shfl_xor((int)(uint32_t)(v >> 32), o);
+    v += ((uint64_t)hi << 32) | lo;
+  }
+  return v;
+}
+
+// Per-sweep tables of the large-K draw (oracle exact_big_tables), one block
+// of 1024 threads (Kp <= 4096): m = the largest table value (inv, ainv and,
+// for topics holding tokens, inv_m1, ainv_m1), S = 31 - exponent(m), the
+// fixed-point values big_fix(x) = (uint32) ldexp(x, S) < 2^31, the prefix of
+// G = big_fix(ainv) and the scalars bsig = beta 2^-S, isig = 2^S / beta.
+__device__ __forceinline__ uint32_t big_fix(float x, int S) { return (uint32_t)ldexpf(x, S); }
+
+__global__ __launch_bounds__(1024) void k_big_tables(const int32_t* __restrict__ nwsum,
+                                                     const float* __restrict__ alpha_f,
+                                                     const float* __restrict__ inv,
+                                                     const float* __restrict__ inv_m1, int32_t K, int32_t Kp,
+                                                     float beta, BigTables t) {
+  __shared__ float smax[16];
+  __shared__ uint64_t ssum[1024];
+  const int tid = threadIdx.x;
+  const int per = (Kp + 1023) / 1024;   // <= 4
+  float m = 0.0f;
+  float vi[4], va[4], vim[4], vam[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int k = tid * per + j;
+    vi[j] = va[j] = vim[j] = vam[j] = 0.0f;
+    if (j >= per || k >= Kp) continue;
+    const bool live = k < K && nwsum[k] >= 1;
+    vi[j] = inv[k];
+    va[j] = alpha_f[k] * vi[j];
+    vim[j] = live ? inv_m1[k] : 0.0f;
+    vam[j] = live ? alpha_f[k] * inv_m1[k] : 0.0f;
+    t.tab[k] = make_float2(vi[j], va[j]);
+    m = fmaxf(m, fmaxf(fmaxf(vi[j], va[j]), fmaxf(vim[j], vam[j])));
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+  if ((tid & 63) == 0) smax[tid >> 6] = m;
+  __syncthreads();
+  float mm = 0.0f;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) mm = fmaxf(mm, smax[i]);
+  int e = 0;
+  (void)frexpf(mm, &e);
+  const int S = mm > 0.0f ? 31 - e : 0;
+  uint64_t loc = 0;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int k = tid * per + j;
+    if (j >= per || k >= Kp) continue;
+    const uint32_t G = big_fix(va[j], S);
+    t.F[k] = big_fix(vi[j], S);
+    t.tab_m1[k] = make_float4(vim[j], vam[j], __builtin_bit_cast(float, big_fix(vim[j], S)),
+                              __builtin_bit_cast(float, (int32_t)big_fix(vam[j], S) - (int32_t)G));
+    loc += G;
+  }
+  ssum[tid] = loc;
+  __syncthreads();
+  for (int d = 1; d < 1024; d <<= 1) {
+    const uint64_t v = tid >= d ? ssum[tid - d] : 0ull;
+    __syncthreads();
+    ssum[tid] += v;
+    __syncthreads();
+  }
+  uint64_t acc = ssum[tid] - loc;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int k = tid * per + j;
+    if (j >= per || k >= Kp) continue;
+    acc += big_fix(va[j], S);
+    t.pfx[k] = acc;
+  }
+  if (tid == 0) {
+    BigScal s;
+    s.S = S;
+    s.pad = 0;
+    s.S0 = ssum[1023];
+    s.bsig = ldexpf(beta, -S);
+    s.bsig_hi = ldexpf(beta, 32 - S);
+    s.isig = ldexp(1.0, S) / (double)beta;
+    *t.scal = s;
+  }
+}
+
 __device__ __forceinline__ int nd16_get(const uint32_t* nd2, int k) {
   return (int)reinterpret_cast<const uint16_t*>(nd2)[k];
 }
 
-// inclusive scan inside each 16-lane row (sources outside the row add 0)
-__device__ __forceinline__ float row_scan16(float x) {
-  x = dpp_mov<0x111, 0xf, true>(x) + x;
-  x = dpp_mov<0x112, 0xf, true>(x) + x;
-  x = dpp_mov<0x114, 0xf, true>(x) + x;
-  x = dpp_mov<0x118, 0xf, true>(x) + x;
-  return x;
-}
-
+// A SampleParams field read from the kernel-argument segment where it is used
+// (the kernel's only argument sits at offset 0).  The large-K sampler runs
+// out of SGPRs (36 spilled into VGPR lanes with every pointer held live);
+// pointers of rare paths (chunk and document switches, the doc-part search,
+// saturated rows) are re-read from the segment instead of held.
+#define KARG(field)                                                                                   \
+  (*reinterpret_cast<const volatile decltype(SampleParams::field)*>(                                  \
+      (const char*)(__builtin_amdgcn_kernarg_segment_ptr()) + offsetof(SampleParams, field)))
 template <int C, int NS, int RB, bool FROZEN>
-__global__ __launch_bounds__(64 * sb_waves<C>()) void k_sample_sparse_big(SampleParams p) {
+__global__ __launch_bounds__(64 * sb_waves<C>()) void k_sample_big(SampleParams p) {
   extern __shared__ __attribute__((aligned(16))) int32_t smem[];
   constexpr int KP = C * 64;
-  constexpr int NG = C / 16;
   constexpr int WB = sb_waves<C>();
   static_assert(NS >= 2 && NS <= 8, "ring slots");
   const int lane = threadIdx.x & 63;
   const int wid = threadIdx.x >> 6;
-  const int row = lane >> 4, col = lane & 15;
-  float2* tab = reinterpret_cast<float2*>(smem);                              // [KP] {alpha, inv}
+  float2* tab = reinterpret_cast<float2*>(smem);                              // [KP] {inv, ainv}
   uint32_t* nd2 = reinterpret_cast<uint32_t*>(smem + 2 * KP) + wid * (KP / 2); // [KP/2]
 
-  for (int i = threadIdx.x; i < KP; i += 64 * WB) tab[i] = make_float2(p.alpha[i], p.inv[i]);
+  for (int i = threadIdx.x; i < KP; i += 64 * WB) tab[i] = p.big.tab[i];
   for (int i = threadIdx.x; i < WB * (KP / 2); i += 64 * WB) smem[2 * KP + i] = 0;
   __syncthreads();
-#if SB_PIPE
-  // LDS byte addresses of the table and of this wave's document counts
-  typedef __attribute__((address_space(3))) int32_t lds_i32;
-  const uint32_t tab_lds = (uint32_t)(uintptr_t)(lds_i32*)smem;
-  const uint32_t nd_lds = (uint32_t)(uintptr_t)(lds_i32*)nd2;
-#endif
 
-  const float beta = p.beta;
-  const int last_lane = (p.K - 1) / C;
-  const int32_t* __restrict__ nw = p.nw;
+  const int S = uniform_i(p.big.scal->S);
+  const uint64_t S0 = uniform_u64(p.big.scal->S0);
+  const float bsig = p.big.scal->bsig, bsig_hi = p.big.scal->bsig_hi;
+  const double isig = p.big.scal->isig;
+  const int last_topic = p.K - 1;
   const uint32_t* __restrict__ ent = p.ent;
-#if SB_OFF32
-  // a row's start as a 32-bit count of whole 64-entry rounds: one VGPR and one
-  // readlane per row offset instead of two
-  const uint32_t* __restrict__ row_off = p.row_rnd;
-  typedef uint32_t roff_t;
-  auto row_ptr = [&](roff_t o) -> const uint32_t* { return ent + ((uint64_t)o << 6); };
-  auto readlane_o = [&](roff_t v, int l) -> roff_t { return (roff_t)readlane_i((int)v, l); };
-#else
-  const int64_t* __restrict__ row_off = p.row_off;
-  typedef int64_t roff_t;
-  auto row_ptr = [&](roff_t o) -> const uint32_t* { return ent + o; };
-  auto readlane_o = [&](roff_t v, int l) -> roff_t {
-    return ((int64_t)readlane_i((int)(v >> 32), l) << 32) | (uint32_t)readlane_i((int)v, l);
-  };
-#endif
+  const uint32_t* __restrict__ row_off = p.row_rnd;   // a row's start in whole 64-entry rounds
+  auto row_ptr = [&](uint32_t o) -> const uint32_t* { return ent + ((uint64_t)o << 6); };
   const int32_t* __restrict__ row_nnz = p.row_nnz;
-  const float* __restrict__ inv_m1 = p.inv_m1;
+  const float4* __restrict__ tab_m1 = p.big.tab_m1;
 
-  auto coef_at = [&](int k, int zc, float invc) -> float {
-    const float2 t = tab[k];
-    return ((float)nd16_get(nd2, k) + t.x) * ((k == zc) ? invc : t.y);
+  auto fixp = [&](float x) -> uint32_t { return big_fix(x, S); };
+  // one B term into the lane's running sum (SAT: the row holds a saturated
+  // count field, read the exact count from nw)
+  auto term_acc = [&](uint32_t e, int w, bool sat, float acc) -> float {
+    const int t = (int)(e & ENT_TOPIC_MASK);
+    uint32_t c = e >> ENT_TOPIC_BITS;
+    if (sat && c == ENT_COUNT_SAT) c = (uint32_t)KARG(nw)[(int64_t)w * KP + t];
+    const float2 tb = tab[t];
+    const float coef = __builtin_fmaf((float)nd16_get(nd2, t), tb.x, tb.y);
+    return __builtin_fmaf((float)c, coef, acc);
   };
-  // one word-part term: coef[t] * float(c - [t == z_old]); SAT: the row holds
-  // a saturated count field, read the exact count from nw
-  auto term_of = [&](uint32_t e, int w, int zc, float invc, bool sat) -> float {
-    const int tq = (int)(e & ENT_TOPIC_MASK);
-    uint32_t cq = e >> ENT_TOPIC_BITS;
-    if (sat && cq == ENT_COUNT_SAT) cq = (uint32_t)nw[(int64_t)w * KP + tq];
-    if (!FROZEN) cq = __builtin_elementwise_sub_sat(cq, (uint32_t)(tq == zc));
-    return coef_at(tq, zc, invc) * (float)(int)cq;
-  };
-  // one row pass: lane (row r, col j) evaluates topic owner*C + g*16 + j of
-  // the (owner, g) its row was given; returns the in-row inclusive scan
-  auto row_pass = [&](int owner, int g, int zc, float invc) -> float {
-    return row_scan16(coef_at(owner * C + g * 16 + col, zc, invc) * beta);
-  };
-  // the lane's NG group sums as one register vector: a wave-uniform group
-  // index becomes an indexed register move (an array was placed in scratch)
-  typedef float tg_t __attribute__((ext_vector_type(NG)));
-#if SB_TGMASK
-  // lane `owner` writes group g: the lane as a scalar mask (s_lshl_b64, an
-  // inverse ballot) and the uniform g as a uniform switch, so one update is
-  // one VALU select (the keyed form is NG compares + NG selects; the scalar
-  // unit has the headroom since v8.4 moved work off it)
-  auto set_tg = [&](tg_t& TG, int owner, int g, float v) {
-    const bool me = __builtin_amdgcn_inverse_ballot_w64(1ull << (uint32_t)owner);
-    switch (uniform_i(g)) {
-      default:
-        break;
-      case 0: TG[0] = me ? v : TG[0]; break;
-      case 1: if (NG > 1) TG[1 % NG] = me ? v : TG[1 % NG]; break;
-      case 2: if (NG > 2) TG[2 % NG] = me ? v : TG[2 % NG]; break;
-      case 3: if (NG > 3) TG[3 % NG] = me ? v : TG[3 % NG]; break;
-    }
-  };
-  [[maybe_unused]] auto tg_at = [&](const tg_t& TG, int owner, int g) -> float { return readlane_f(TG[g], owner); };
-#elif SB_TGKEY
-  // lane*NG + q per element; the asm keeps them opaque VGPRs, so the
-  // compare against a uniform key stays one VALU compare per element
-  int tkey[NG];
-#pragma unroll
-  for (int q = 0; q < NG; ++q) {
-    int v = lane * NG + q;
-    asm volatile("" : "+v"(v));
-    tkey[q] = v;
-  }
-  auto set_tg = [&](tg_t& TG, int owner, int g, float v) {
-    const int key = owner * NG + g;
-#pragma unroll
-    for (int q = 0; q < NG; ++q) TG[q] = (tkey[q] == key) ? v : TG[q];
-  };
-  // group g of lane owner, read out to every lane (the non-deferred path)
-  [[maybe_unused]] auto tg_at = [&](const tg_t& TG, int owner, int g) -> float {
-    const int key = owner * NG + g;
-    float v = 0.0f;
-#pragma unroll
-    for (int q = 0; q < NG; ++q) v = (tkey[q] == key) ? TG[q] : v;
-    return readlane_f(v, owner);
-  };
-#else
-  auto set_tg = [&](tg_t& TG, int owner, int g, float v) {
-    const float cur = TG[g];
-    TG[g] = (lane == owner) ? v : cur;
-  };
-  [[maybe_unused]] auto tg_at = [&](const tg_t& TG, int owner, int g) -> float { return readlane_f(TG[g], owner); };
-#endif
-  auto lane_total = [&](const tg_t& TG) -> float {
-    float t = TG[0];
-#pragma unroll
-    for (int q = 1; q < NG; ++q) t = t + TG[q];
-    return t;
+  // the pieces of a term (re-walks of a batch by readlane)
+  auto term_parts = [&](uint32_t e, int w, bool sat, float& cf, float& coef) {
+    const int t = (int)(e & ENT_TOPIC_MASK);
+    uint32_t c = e >> ENT_TOPIC_BITS;
+    if (sat && c == ENT_COUNT_SAT) c = (uint32_t)KARG(nw)[(int64_t)w * KP + t];
+    const float2 tb = tab[t];
+    coef = __builtin_fmaf((float)nd16_get(nd2, t), tb.x, tb.y);
+    cf = (float)c;
   };
 
   bool first_range = true;
@@ -2089,9 +2102,6 @@ __global__ __launch_bounds__(64 * sb_waves<C>()) void k_sample_sparse_big(Sample
     if (r >= p.num_ranges) break;
     const int64_t d0 = p.range_doc[r], d1 = p.range_end[r];
     const int64_t t0 = p.doc_off[d0];
-    // token positions below are 32-bit offsets from the range start (64-bit
-    // compares and adds cost two scalar instructions each, and the scalar
-    // unit binds this kernel)
     const int t1 = (int)(p.doc_off[d1] - t0);
     if (t1 <= 0) continue;
     const int32_t* __restrict__ wrd = p.words + t0;
@@ -2113,49 +2123,31 @@ __global__ __launch_bounds__(64 * sb_waves<C>()) void k_sample_sparse_big(Sample
       z2 = zr[128 + lane];
     }
     int cmn = row_nnz[cw], m1n = row_nnz[w1];
-    roff_t cmo = row_off[cw], m1o = row_off[w1];
+    uint32_t cmo = row_off[cw], m1o = row_off[w1];
     int cn = cz;
-    float cu = u01(draw_u32(gbase + (uint64_t)lane, p.c2, p.c3, p.k0, p.k1));
+    uint32_t cx0, cx1;
+    philox_x01(gbase + (uint64_t)lane, p.c2, p.c3, p.k0, p.k1, cx0, cx1);
+    __builtin_amdgcn_s_waitcnt(kVmcnt0);
 
-    // the chunk's count changes, lane i = token i: two delta atomics when its
-    // topic changed (lanes past the range hold cz == cn).  No nwsum atomics:
-    // the sparse apply derives the nwsum delta from the nw delta's column sums
-    // (k_apply_cols); two more device atomics per changed token into one
-    // Kp-cell array that every wave of the chip hits had cost ~64 of the
-    // kernel's 127 written B/token
     auto flush_chunk = [&]() {
       if (!FROZEN && cn != cz) {
         const uint64_t rb = (uint64_t)(uint32_t)cw * (uint64_t)KP;
-        atomicAdd(p.delta + (rb + (uint32_t)cz), -1);
-        atomicAdd(p.delta + (rb + (uint32_t)cn), 1);
-#if SB_DSUM_ATOMICS
-        // A/B only: round 3's nwsum atomics (the apply recomputes dsum anyway)
-        atomicAdd(p.dsum + cz, -1);
-        atomicAdd(p.dsum + cn, 1);
-#endif
+        atomicAdd(KARG(delta) + (rb + (uint32_t)cz), -1);
+        atomicAdd(KARG(delta) + (rb + (uint32_t)cn), 1);
       }
     };
 
-    tg_t TG;
-    // document start: every lane evaluates its own NG group trees serially
-    // (the same additions as the row scan, element by element)
+    // document start: counts into LDS, R = sum of F over the document's topics
+    uint64_t R = 0;
     auto build_doc = [&](int ts, int te) {
+      uint64_t rl = 0;
       for (int i = ts + lane; i < te; i += 64) {
         const int k = zr[i];
         atomicAdd(&nd2[k >> 1], (k & 1) ? 0x10000u : 1u);
+        rl += fixp(tab[k].x);
       }
+      R = uniform_u64(wave_sum_u64(rl));
       wave_lds_fence();
-#pragma nounroll
-      for (int g = 0; g < NG; ++g) {
-        float x[16];
-#pragma unroll
-        for (int j = 0; j < 16; ++j) x[j] = coef_at(lane * C + g * 16 + j, -1, 0.0f) * beta;
-#pragma unroll
-        for (int d = 1; d < 16; d <<= 1)
-#pragma unroll
-          for (int j = 15; j >= d; --j) x[j] = x[j - d] + x[j];
-        TG[g] = x[15];
-      }
     };
     auto clear_doc = [&]() {
 #pragma unroll
@@ -2170,46 +2162,47 @@ __global__ __launch_bounds__(64 * sb_waves<C>()) void k_sample_sparse_big(Sample
     build_doc(0, doc_end);
 
     // ring slot of token t: t % NS; slot (t + NS - 1) % NS is refilled during t
-    uint32_t ring[NS][RB];
-    float cinv[NS];
-    // the first RB rounds of token tp (< t1, at most 70 tokens past cbase)
-    auto prefetch = [&](uint32_t (&rg)[RB], float& ci, int tp) {
+    // the ring and the running sums as register vectors: the draw indexes
+    // them by a wave-uniform round (an indexed register move; as arrays they
+    // were placed in scratch)
+    typedef uint32_t ring_t __attribute__((ext_vector_type(RB)));
+    typedef float accq_t __attribute__((ext_vector_type(RB)));
+    ring_t ring[NS];
+    // per slot, the token's old topic: {inv_m1, ainv_m1, bits of Fm1, bits
+    // of Gm1 - G} (k_big_tables), loaded FIRST so the doc part can be formed
+    // at the token's start, off the draw's chain
+    float4 rm1[NS];
+    auto prefetch = [&](ring_t& rg, float4& m1, int tp) {
       const int pidx = tp - cbase;
       int np, zp;
-      roff_t op;
+      uint32_t op;
       if (pidx < 64) {
         np = readlane_i(cmn, pidx);
-        op = readlane_o(cmo, pidx);
+        op = (uint32_t)readlane_i((int)cmo, pidx);
         zp = readlane_i(cz, pidx);
       } else {
         np = readlane_i(m1n, pidx - 64);
-        op = readlane_o(m1o, pidx - 64);
+        op = (uint32_t)readlane_i((int)m1o, pidx - 64);
         zp = readlane_i(z1, pidx - 64);
       }
-#if SB_BUF
-      // past the range end: an empty row (every load returns 0)
-      const int nrp = tp < t1 ? ((np & 0x7FFFFFFF) + 63) >> 6 : 0;
-      const __amdgpu_buffer_rsrc_t rs =
-          __builtin_amdgcn_make_buffer_rsrc((void*)row_ptr(op), (short)0, nrp * 256, kBufWord3);
+      if (!FROZEN) m1 = tab_m1[zp];
+      // the range ends at the row's last entry: loads past it (the zero
+      // padding of the last round, rounds past the row, tokens past the
+      // range) return 0 without a memory access
+      const int nb = tp < t1 ? (np & 0x7FFFFFFF) * 4 : 0;
+      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)row_ptr(op), (short)0, nb, kBufWord3);
+      // lane * 4 opaque here: the constant q * 256 then folds into the loads'
+      // immediate offset (hoisted out of the loop, lane * 4 + q * 256 had
+      // taken one VGPR per round)
+      int lo4 = lane * 4;
+      asm volatile("" : "+v"(lo4));
 #pragma unroll
-      for (int q = 0; q < RB; ++q) rg[q] = __builtin_amdgcn_raw_buffer_load_b32(rs, lane * 4 + q * 256, 0, 0);
-#else
-      const int nrp = ((np & 0x7FFFFFFF) + 63) >> 6;
-      const uint32_t* rp = row_ptr(op) + lane;
-#pragma unroll
-      for (int q = 0; q < RB; ++q)
-        if (q < nrp) rg[q] = rp[q * 64];
-#endif
-      if (!FROZEN) ci = inv_m1[zp];
+      for (int q = 0; q < RB; ++q) rg[q] = __builtin_amdgcn_raw_buffer_load_b32(rs, lo4 + q * 256, 0, 0);
     };
 #pragma unroll
-    for (int s = 0; s < NS - 1; ++s)
-      if (SB_BUF || s < t1) prefetch(ring[s], cinv[s], s);
+    for (int s = 0; s < NS - 1; ++s) prefetch(ring[s], rm1[s], s);
 
-    // the previous token of this document: its new topic still to add back
-    // (pk < 0: none) and its old / new groups, whose sums are refreshed with
-    // this token's removal (SB_DEFER)
-    int pk = -1, plo = 0, pgo = 0, pln = 0, pgn = 0;
+    int pk = -1;   // the previous token of this document: its new topic, still to add back
     for (int tb = 0; tb < t1; tb += NS) {
 #pragma unroll
       for (int s = 0; s < NS; ++s) {
@@ -2217,8 +2210,9 @@ __global__ __launch_bounds__(64 * sb_waves<C>()) void k_sample_sparse_big(Sample
         if (t < t1) {
           int idx = t - cbase;
           if (idx == 64) {
-            flush_chunk();
-            zr[cbase + lane] = cn;
+            // the finished chunk's topics and count changes
+            const int ow = cw, oz = cz, on = cn;
+            const int ob = cbase;
             cbase += 64;
             idx = 0;
             cw = w1;
@@ -2230,357 +2224,372 @@ __global__ __launch_bounds__(64 * sb_waves<C>()) void k_sample_sparse_big(Sample
             m1n = row_nnz[w1];
             m1o = row_off[w1];
             cn = cz;
-            cu = u01(draw_u32(gbase + (uint64_t)(cbase + lane), p.c2, p.c3, p.k0, p.k1));
             if (cbase + 128 + lane < t1) {
               w2 = wrd[cbase + 128 + lane];
               z2 = zr[cbase + 128 + lane];
             }
+            zr[ob + lane] = on;
+            // the chunk registers land here, once per 64 tokens (every load
+            // but the z store just issued): a chunk register the compiler
+            // believes in flight makes it wait vmcnt(0) where a token reads
+            // it, i.e. drain the row ring
+            __builtin_amdgcn_s_waitcnt(kVmcnt1);
+            if (!FROZEN && on != oz) {
+              const uint64_t rb = (uint64_t)(uint32_t)ow * (uint64_t)KP;
+              atomicAdd(KARG(delta) + (rb + (uint32_t)oz), -1);
+              atomicAdd(KARG(delta) + (rb + (uint32_t)on), 1);
+            }
+            philox_x01(gbase + (uint64_t)(cbase + lane), p.c2, p.c3, p.k0, p.k1, cx0, cx1);
           }
           if (t == doc_end) {
             clear_doc();
             ++doc;
-            while (p.doc_off[doc + 1] - t0 <= t) ++doc;
-            doc_end = uniform_i((int)(p.doc_off[doc + 1] - t0));
+            const int64_t* dof = KARG(doc_off);
+            while (dof[doc + 1] - t0 <= t) ++doc;
+            doc_end = uniform_i((int)(dof[doc + 1] - t0));
             build_doc(t, doc_end);
-            pk = -1;                       // the last document's add-back is moot
+            pk = -1;
           }
 
           const int w = readlane_i(cw, idx);
           const int zo = readlane_i(cz, idx);
-          const float u = readlane_f(cu, idx);
+          const float u = u01((uint32_t)readlane_i((int)cx0, idx));
           const int n_raw = readlane_i(cmn, idx);
-          const bool row_sat = n_raw < 0;           // the row holds a saturated count
+          const bool row_sat = n_raw < 0;
           const int n = n_raw & 0x7FFFFFFF;
-          const roff_t off = readlane_o(cmo, idx);
+          const uint32_t off = (uint32_t)readlane_i((int)cmo, idx);
           const uint32_t* __restrict__ erow = row_ptr(off);
-#if SB_UDIV
-          const int lo = (int)((uint32_t)zo / (uint32_t)C);
-          const int go = (int)(((uint32_t)zo % (uint32_t)C) / 16u);
-#else
-          const int lo = zo / C;
-          const int go = (zo % C) / 16;
-#endif
-          // while the token is out: topic zc's coefficient uses invc (inv_m1[zo])
-          const int zc = FROZEN ? -1 : zo;
-          const float invc = FROZEN ? 0.0f : cinv[s];
-#if SB_DEFER
-          // add the previous token back under its new topic and remove this
-          // one, then one pass: row 0 / 1 the previous token's old / new
-          // group, rows 2-3 this token's (set last: it may be one of them)
+
+          // the previous token back under its new topic, this one out: two
+          // LDS adds in flight at once; the old count comes back for the
+          // fixed-point own-topic terms
           if (lane == 0) {
-#if SB_NDATOM
-            // no-return LDS atomics: both updates in flight at once (a plain
-            // += / -= is a read, a wait and a write each, one after the other)
-            if (pk >= 0)
-              __hip_atomic_fetch_add(&nd2[pk >> 1], (pk & 1) ? 0x10000u : 1u, __ATOMIC_RELAXED,
-                                     __HIP_MEMORY_SCOPE_WAVEFRONT);
+            const int pa = pk >= 0 ? pk : 0;
+            __hip_atomic_fetch_add(&nd2[pa >> 1], pk < 0 ? 0u : ((pa & 1) ? 0x10000u : 1u), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_WAVEFRONT);
             __hip_atomic_fetch_add(&nd2[zo >> 1], (zo & 1) ? 0xFFFF0000u : 0xFFFFFFFFu, __ATOMIC_RELAXED,
                                    __HIP_MEMORY_SCOPE_WAVEFRONT);
-#else
-            if (pk >= 0) nd2[pk >> 1] += (pk & 1) ? 0x10000u : 1u;
-            nd2[zo >> 1] -= (zo & 1) ? 0x10000u : 1u;
-#endif
           }
           wave_lds_fence();
-          {
-            const bool own_row = row >= 2;
-            const int ow = row == 0 ? plo : (row == 1 ? pln : lo);
-            const int og = row == 0 ? pgo : (row == 1 ? pgn : go);
-            const float x = row_scan16(coef_at(ow * C + og * 16 + col, own_row ? zc : -1, own_row ? invc : 0.0f) * beta);
-            if (pk >= 0) {
-              set_tg(TG, plo, pgo, readlane_f(x, 15));
-              set_tg(TG, pln, pgn, readlane_f(x, 31));
-            }
-            set_tg(TG, lo, go, readlane_f(x, 47));
-          }
-#else
-          const float g_saved = tg_at(TG, lo, go);
-
-          // remove the token from its document; re-evaluate its group
-          if (lane == 0) nd2[zo >> 1] -= (zo & 1) ? 0x10000u : 1u;
-          wave_lds_fence();
-          set_tg(TG, lo, go, readlane_f(row_pass(lo, go, zc, invc), 15));
-#endif
+          // the own topic's count after both updates: a plain read behind the
+          // no-return adds (a wave's LDS operations complete in order; a
+          // returning atomic held the rounds' reads behind it)
+          const int ndz = uniform_i(nd16_get(nd2, zo));
+          const float2 tz = tab[zo];
+          const float2 tp = tab[pk >= 0 ? pk : 0];
+          const uint32_t Fz = (uint32_t)uniform_i((int)fixp(tz.x));
+          // (a mask, not a branch: the read stays beside the others)
+          const uint32_t Fp = (uint32_t)uniform_i((int)fixp(tp.x)) & (uint32_t)(-(int)(pk >= 0));
+          R = R + (uint64_t)Fp - (uint64_t)Fz;
 
           // word part, register rounds: lane l holds entry l + 64 q; accq[q]
           // = the lane's running sum after round q
           const int nr_all = (n + 63) >> 6;
-          float accq[RB];
+          accq_t accq;
           float acc = 0.0f;
-          // rounds in groups of SB_GRP under one uniform branch, so the
-          // group's LDS reads are in flight together (a round past the row's
-          // last one is evaluated and not added)
-#if SB_PIPE
-          // every register round of a row that fills them (no branch per
-          // round): round q+1's two LDS reads are issued before round q is
-          // summed, and the wait for round q leaves them in flight.  A
-          // read's destination stays live (an operand of the wait that
-          // retires it) until the data has landed.  The terms and their
-          // order are term_of's.
-          auto rounds_full = [&]() {
-            uint32_t ndv[2];
-            double tbv[2];
-            auto issue = [&](int b, uint32_t e) {
-              const uint32_t k = e & ENT_TOPIC_MASK;
-              const uint32_t a_nd = nd_lds + 2u * k, a_tb = tab_lds + 8u * k;
-              asm volatile("ds_read_u16 %0, %1" : "=v"(ndv[b]) : "v"(a_nd) : "memory");
-              asm volatile("ds_read_b64 %0, %1" : "=v"(tbv[b]) : "v"(a_tb) : "memory");
-            };
-            issue(0, ring[s][0]);
+          // the doc part, A_fx = sum_k nd_k F'_k + sum_k G'_k (exact), from
+          // the slot's topic data; written out in the same basic block as the
+          // first SB_RU rounds (evaluated without a branch: a round past the
+          // row is zero entries, + 0), so the scheduler interleaves the two
+          // chains.  A row holding a saturated count takes the general path.
+          int64_t dG = 0;
+          uint32_t Fm1z = Fz;
+          uint64_t As = S0;
+          float A_f = 0.0f;
+          auto doc_part = [&]() __attribute__((always_inline)) {
+            uint64_t Afx;
+            if (!FROZEN) {
+              const float4 m1 = rm1[s];
+              Fm1z = (uint32_t)uniform_i(__builtin_bit_cast(int, m1.z));
+              dG = (int64_t)uniform_i(__builtin_bit_cast(int, m1.w));
+              const int64_t dF = (int64_t)ndz * ((int64_t)Fm1z - (int64_t)Fz);
+              As = (uint64_t)((int64_t)S0 + dG);
+              Afx = (uint64_t)((int64_t)(As + R) + dF);
+            } else {
+              Afx = S0 + R;
+            }
+            // A in fp32: beta 2^-S (hi 2^32 + lo), hi < 2^16 exact
+#ifdef SB_X_NOA
+            A_f = uniform_f((float)(uint32_t)S0 * bsig);   // attribution experiment only
+            (void)Afx;
+#else
+            A_f = uniform_f(__builtin_fmaf((float)(uint32_t)uniform_i((int)(uint32_t)(Afx >> 32)), bsig_hi,
+                                           (float)(uint32_t)uniform_i((int)(uint32_t)Afx) * bsig));
+#endif
+          };
+          auto rounds = [&](bool sat, int q0) __attribute__((always_inline)) {
 #pragma unroll
             for (int q = 0; q < RB; ++q) {
-              const int b = q & 1;
-              if (q + 1 < RB) {
-                issue(b ^ 1, ring[s][q + 1]);
-                asm volatile("s_waitcnt lgkmcnt(2)" : "+v"(ndv[b]), "+v"(tbv[b]));
-              } else {
-                asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(ndv[b]), "+v"(tbv[b]));
-              }
-              const uint32_t e = ring[s][q];
-              const int tq = (int)(e & ENT_TOPIC_MASK);
-              uint32_t cq = e >> ENT_TOPIC_BITS;
-              if (!FROZEN) cq = __builtin_elementwise_sub_sat(cq, (uint32_t)(tq == zc));
-              const float2 t = __builtin_bit_cast(float2, tbv[b]);
-              const float coef = ((float)(int)ndv[b] + t.x) * ((tq == zc) ? invc : t.y);
-              acc = acc + coef * (float)(int)cq;
+              if (q < q0) continue;
+              if (q < nr_all) acc = term_acc(ring[s][q], w, sat, acc);
               accq[q] = acc;
             }
           };
-#endif
-          auto rounds = [&](bool sat) {
-#if SB_PIPE
-            if (!sat && nr_all >= RB) {
-              rounds_full();
-              return;
+          if (!row_sat) {
+#pragma unroll
+            for (int q = 0; q < SB_RU; ++q) {
+              acc = term_acc(ring[s][q], w, false, acc);
+              accq[q] = acc;
             }
-#endif
-#pragma unroll
-            for (int q = 0; q < RB; q += SB_GRP) {
-              if (q < nr_all) {
-                float tt[SB_GRP];
-#pragma unroll
-                for (int g = 0; g < SB_GRP; ++g) tt[g] = term_of(ring[s][q + g], w, zc, invc, sat);
-#pragma unroll
-                for (int g = 0; g < SB_GRP; ++g) {
-                  const float na = acc + tt[g];
-                  acc = (g == 0 || q + g < nr_all) ? na : acc;
-                  accq[q + g] = acc;
-                }
-              } else {
-#pragma unroll
-                for (int g = 0; g < SB_GRP; ++g) accq[q + g] = acc;
-              }
-            }
-          };
-          if (!row_sat) rounds(false);
-          else rounds(true);
-          // every use of this token's ring slot is above: refill the slot of
-          // token t-1 now (the loads cannot move above this point)
-          asm volatile("" : "+v"(acc)::"memory");
-          {
-            const int sp = (s + NS - 1) % NS;
-            const int tp = t + NS - 1;
-            if (SB_BUF || tp < t1) prefetch(ring[sp], cinv[sp], tp);
+            doc_part();
+            rounds(false, SB_RU);
+          } else {
+            doc_part();
+            rounds(true, 0);
           }
-          // the rounds past RB (long rows), streamed in batches; the
-          // lane's running sum after each of the first SB_NB batches is kept
-          // so the draw re-reads one batch of the selected lane, not all
+          // every register of this token's ring slot has landed on every path
+          // (a row shorter than RB rounds skips the rest): otherwise the
+          // compiler keeps them "in flight" across the loop and, when it
+          // reuses them, waits for the NEXT token's prefetch (vmcnt counts
+          // in order)
+#pragma unroll
+          for (int q = 0; q < RB; ++q) asm volatile("" ::"v"(ring[s][q]));
+
           float accb[SB_NB];
 #pragma unroll
           for (int i = 0; i < SB_NB; ++i) accb[i] = 0.0f;
-          // the batch loop specialised on the row's saturation flag (uniform),
-          // as the register rounds are: a runtime flag inside term_of made every
-          // batch term a divergent branch (exec-mask save/restore on the scalar
-          // unit, which binds this kernel)
-#if SB_DBUF
-          // double-buffered: batch b+1's loads are in flight while batch b is
-          // summed; loads past the row return 0, and a 0 entry adds +0
+          // the rounds past RB (long rows), streamed in double-buffered batches
           auto batches = [&](bool sat) {
             const __amdgpu_buffer_rsrc_t rb =
-                __builtin_amdgcn_make_buffer_rsrc((void*)erow, (short)0, nr_all * 256, kBufWord3);
+                __builtin_amdgcn_make_buffer_rsrc((void*)erow, (short)0, n * 4, kBufWord3);
             uint32_t ea[SB_BATCH];
+            int lo4 = lane * 4;
+            asm volatile("" : "+v"(lo4));
 #pragma unroll
             for (int b = 0; b < SB_BATCH; ++b)
-              ea[b] = __builtin_amdgcn_raw_buffer_load_b32(rb, lane * 4 + (RB + b) * 256, 0, 0);
+              ea[b] = __builtin_amdgcn_raw_buffer_load_b32(rb, lo4 + (RB + b) * 256, 0, 0);
             int mb = 0;
-#if SB_REM
-            // whole batches only; the row's last 1..SB_BATCH-1 rounds below,
-            // without the zero rounds that pad them to a batch (a +0 term
-            // leaves the sum unchanged, so skipping it keeps the order)
-            int q0 = RB;
-            for (; q0 + SB_BATCH <= nr_all; q0 += SB_BATCH, ++mb) {
-#else
             for (int q0 = RB; q0 < nr_all; q0 += SB_BATCH, ++mb) {
-#endif
+              // the next batch's loads only when it exists: a load left
+              // unconsumed keeps its registers "in flight" into the next token
               uint32_t en[SB_BATCH];
-              const int vo = lane * 4 + (q0 + SB_BATCH) * 256;
+              if (q0 + SB_BATCH < nr_all) {
+                const int vo = lo4 + (q0 + SB_BATCH) * 256;
 #pragma unroll
-              for (int b = 0; b < SB_BATCH; ++b) en[b] = __builtin_amdgcn_raw_buffer_load_b32(rb, vo + b * 256, 0, 0);
+                for (int b = 0; b < SB_BATCH; ++b) en[b] = __builtin_amdgcn_raw_buffer_load_b32(rb, vo + b * 256, 0, 0);
+              } else {
 #pragma unroll
-              for (int b = 0; b < SB_BATCH; ++b) acc = acc + term_of(ea[b], w, zc, invc, sat);
+                for (int b = 0; b < SB_BATCH; ++b) en[b] = 0u;
+              }
+#pragma unroll
+              for (int b = 0; b < SB_BATCH; ++b) acc = term_acc(ea[b], w, sat, acc);
 #pragma unroll
               for (int i = 0; i < SB_NB; ++i) accb[i] = (mb == i) ? acc : accb[i];
 #pragma unroll
               for (int b = 0; b < SB_BATCH; ++b) ea[b] = en[b];
             }
-#if SB_REM
-            const int rem = nr_all - q0;   // uniform, 0 .. SB_BATCH-1
-            if (rem > 0) {
-#pragma unroll
-              for (int b = 0; b < SB_BATCH - 1; ++b)
-                if (b < rem) acc = acc + term_of(ea[b], w, zc, invc, sat);
-#pragma unroll
-              for (int i = 0; i < SB_NB; ++i) accb[i] = (mb == i) ? acc : accb[i];
-            }
-#endif
           };
-#else
-          auto batches = [&](bool sat) {
-            int mb = 0;
-            for (int q0 = RB; q0 < nr_all; q0 += SB_BATCH, ++mb) {
-              uint32_t eb[SB_BATCH];
-              const uint32_t* rp = erow + lane + q0 * 64;
-#pragma unroll
-              for (int b = 0; b < SB_BATCH; ++b) eb[b] = (q0 + b < nr_all) ? rp[b * 64] : 0u;
-#pragma unroll
-              for (int b = 0; b < SB_BATCH; b += SB_GRP) {
-                if (q0 + b < nr_all) {
-                  float tt[SB_GRP];
-#pragma unroll
-                  for (int g = 0; g < SB_GRP; ++g) tt[g] = term_of(eb[b + g], w, zc, invc, sat);
-#pragma unroll
-                  for (int g = 0; g < SB_GRP; ++g) {
-                    const float na = acc + tt[g];
-                    acc = (g == 0 || q0 + b + g < nr_all) ? na : acc;
-                  }
-                }
-              }
-#pragma unroll
-              for (int i = 0; i < SB_NB; ++i) accb[i] = (mb == i) ? acc : accb[i];
-            }
+          auto refill = [&]() {
+            // every use of this token's ring slot is above: refill the slot
+            // of token t-1 (the loads cannot move above this point)
+            asm volatile("" : "+v"(acc)::"memory");
+            const int sp = (s + NS - 1) % NS;
+            prefetch(ring[sp], rm1[sp], t + NS - 1);
           };
-#endif
-#if SB_SAT_SPLIT
+#if SB_REFILL_LAST
           if (nr_all > RB) {
             if (!row_sat) batches(false);
             else batches(true);
           }
 #else
-          batches(row_sat);
+          refill();
+          if (nr_all > RB) {
+            if (!row_sat) batches(false);
+            else batches(true);
+          }
 #endif
           const float TB = wave_incl_scan(acc);
-          const float TAs = wave_incl_scan(lane_total(TG));
           const float sumB = readlane_f(TB, 63);
-          const float sumA = readlane_f(TAs, 63);
-          const float thr = u * (sumB + sumA);
-          int kn;
+
+          // the serial re-walk of lane lstar's rounds [r0, r1) from a0: the
+          // first whose running sum exceeds thrE, else the last; its entry
+          // and the running sums before / after it (the sums are those of the
+          // rounds, fma for fma)
+          struct Walk {
+            uint32_t e;
+            float lo, hi;
+          };
+          auto rewalk = [&](int lstar, int r0, int r1, float a, float thrE) -> Walk {
+            const int nx = r1 - r0;
+            const uint32_t ex = lane < nx ? erow[lstar + 64 * (r0 + lane)] : 0u;
+            float cf, cof;
+            term_parts(ex, w, row_sat, cf, cof);
+            int sel = nx - 1;
+            float lo = a, hi = a;
+            for (int q = 0; q < nx; ++q) {
+              lo = a;
+              a = __builtin_fmaf(readlane_f(cf, q), readlane_f(cof, q), a);
+              hi = a;
+              if (a > thrE) {
+                sel = q;
+                break;
+              }
+            }
+            return Walk{(uint32_t)readlane_i((int)ex, sel), lo, hi};
+          };
+          // A: tfx in fixed point; the alpha part (prefix of G'), then the
+          // document part (prefix of nd F'), topics ascending
+          auto pick_a = [&](float thr) -> int {
+            const float t2 = thr - sumB;
+            const uint64_t tfx = d2u64((double)t2 * isig);
+            if (tfx < As) {
+              const int kc = C * lane + C - 1;
+              const int64_t vc = (int64_t)KARG(big.pfx)[kc] + ((!FROZEN && kc >= zo) ? dG : 0);
+              const uint64_t mc = __ballot((uint64_t)vc > tfx);
+              const int L = mc ? (int)__builtin_ctzll(mc) : 63;
+              const int kf = C * L + (lane < C ? lane : C - 1);
+              const int64_t vf = (int64_t)KARG(big.pfx)[kf] + ((!FROZEN && kf >= zo) ? dG : 0);
+              const uint64_t mf = __ballot(lane < C && (uint64_t)vf > tfx);
+              const int k = mf ? C * L + (int)__builtin_ctzll(mf) : last_topic;
+              return k < last_topic ? k : last_topic;
+            }
+            const uint64_t tr = tfx - As;
+            // lane l's topics [C l, C l + C): the counts as 16-byte LDS reads
+            // (single u16 reads at a 2C-byte lane stride all hit one bank),
+            // F as 16-byte global reads; the own topic's F' = Fm1 added as a
+            // correction on its lane
+            uint64_t ps = 0;
+            {
+              const uint4* ndv = reinterpret_cast<const uint4*>(nd2 + lane * (C / 2));
+              const uint4* fv = reinterpret_cast<const uint4*>(KARG(big.F) + C * lane);
+#pragma unroll 1
+              for (int j8 = 0; j8 < C / 8; ++j8) {
+                const uint4 nv = ndv[j8];
+                const uint4 f0 = fv[2 * j8], f1 = fv[2 * j8 + 1];
+                ps += (uint64_t)(nv.x & 0xFFFFu) * f0.x + (uint64_t)(nv.x >> 16) * f0.y;
+                ps += (uint64_t)(nv.y & 0xFFFFu) * f0.z + (uint64_t)(nv.y >> 16) * f0.w;
+                ps += (uint64_t)(nv.z & 0xFFFFu) * f1.x + (uint64_t)(nv.z >> 16) * f1.y;
+                ps += (uint64_t)(nv.w & 0xFFFFu) * f1.z + (uint64_t)(nv.w >> 16) * f1.w;
+              }
+              if (!FROZEN && lane == (int)((uint32_t)zo / (uint32_t)C))
+                ps += (uint64_t)((int64_t)ndz * ((int64_t)Fm1z - (int64_t)Fz));
+            }
+            const uint64_t incl = wave_incl_scan_u64(ps);
+            const uint64_t ml = __ballot(incl > tr);
+            if (!ml) return last_topic;
+            const int L = (int)__builtin_ctzll(ml);
+            const uint64_t El = L > 0 ? (((uint64_t)(uint32_t)readlane_i((int)(uint32_t)(incl >> 32), L - 1) << 32) |
+                                          (uint32_t)readlane_i((int)(uint32_t)incl, L - 1))
+                                       : 0ull;
+            const int kf = C * L + (lane < C ? lane : C - 1);
+            const uint32_t ff = (!FROZEN && kf == zo) ? Fm1z : KARG(big.F)[kf];
+            const uint64_t wf = lane < C ? (uint64_t)nd16_get(nd2, kf) * ff : 0ull;
+            const uint64_t i2 = wave_incl_scan_u64(wf);
+            const uint64_t mf = __ballot(lane < C && El + i2 > tr);
+            const int k = mf ? C * L + (int)__builtin_ctzll(mf) : last_topic;
+            return k < last_topic ? k : last_topic;
+          };
+
+          // the draw: B (lane, then round: register rounds, kept batch sums,
+          // one re-walk), else A.  qsel >= 0: the entry is register round
+          // qsel of lane lstar (its sums are read only for the own check)
+          const float T = sumB + A_f;
+          const float thr = uniform_f(u * T);
+          int kn, lstar = -1, qsel = -1;
+          Walk wk{0u, 0.0f, 0.0f};
           if (thr < sumB) {
             const int nl = n < 64 ? n : 64;
             const uint64_t m = __ballot((TB > thr) && (lane < nl));
-            const int lstar = m ? (int)__builtin_ctzll(m) : nl - 1;
+            lstar = m ? (int)__builtin_ctzll(m) : nl - 1;
             const float E = lstar > 0 ? readlane_f(TB, lstar - 1) : 0.0f;
-            const int nr = (n - lstar + 63) >> 6;  // rounds of lane lstar
-            // #{q : E + accq[q] <= thr} over lane lstar's register rounds; the
-            // sums are monotone and constant past its last round, so a count
-            // >= nr means "none exceeds" (oracle: the last round)
-#if SB_VCOUNT
+            const float thrE = thr - E;
+            const int nr = (n - lstar + 63) >> 6;   // rounds of lane lstar
             int cv = 0;
 #pragma unroll
-            for (int q = 0; q < RB; ++q) cv += (E + accq[q] <= thr) ? 1 : 0;
+            for (int q = 0; q < RB; ++q) cv += (accq[q] <= thrE) ? 1 : 0;
             const int cnt = readlane_i(cv, lstar);
-#else
-            int cnt = 0;
-#pragma unroll
-            for (int q = 0; q < RB; ++q) cnt = add_lane_bit(cnt, __ballot(E + accq[q] <= thr), lstar);
-#endif
-            int sel;
             if (cnt < nr && cnt < RB) {
-              sel = cnt;
-              kn = (int)((uint32_t)readlane_i((int)ring[s][sel], lstar) & ENT_TOPIC_MASK);
+              qsel = cnt;
             } else if (nr <= RB) {
-              sel = nr - 1;
-              kn = (int)((uint32_t)readlane_i((int)ring[s][sel], lstar) & ENT_TOPIC_MASK);
+              qsel = nr - 1;
             } else {
-              // lane lstar's batches: the first whose end sum exceeds (its
-              // sums are monotone), among the SB_NB kept ones
+              // lane lstar's rounds past RB: the first kept batch whose end
+              // sum exceeds, else the rest; one re-walk of it
               const int nbl = (nr - RB + SB_BATCH - 1) / SB_BATCH;
               int cb = 0;
 #pragma unroll
               for (int i = 0; i < SB_NB; ++i)
-                if (i < nbl && cb == i && E + readlane_f(accb[i], lstar) <= thr) cb = i + 1;
-              if (cb == nbl) {
-                sel = -1;                 // none exceeds: the lane's last round
-                const uint32_t e = erow[lstar + 64 * (nr - 1)];
-                kn = (int)(e & ENT_TOPIC_MASK);
-              } else {
-                // rounds r0.. of lane lstar (one batch, or all the rest past the
-                // kept batches), one per lane, continuing its serial sum
-                const int r0 = RB + SB_BATCH * cb;
-                const int nx = (cb < SB_NB ? min(nr, r0 + SB_BATCH) : nr) - r0;
-                const uint32_t e = lane < nx ? erow[lstar + 64 * (r0 + lane)] : 0u;
-                const float term = term_of(e, w, zc, invc, row_sat);
-                float a = readlane_f(accq[RB - 1], lstar);
+                if (i < nbl && cb == i && readlane_f(accb[i], lstar) <= thrE) cb = i + 1;
+              int r0, r1;
+              float a;
+              if (cb < nbl && cb < SB_NB) {
+                r0 = RB + SB_BATCH * cb;
+                r1 = min(nr, r0 + SB_BATCH);
+                a = readlane_f(accq[RB - 1], lstar);
 #pragma unroll
                 for (int i = 0; i < SB_NB; ++i)
                   if (cb == i + 1) a = readlane_f(accb[i], lstar);
-                sel = nx - 1;
-                for (int q = 0; q < nx; ++q) {
-                  a = a + readlane_f(term, q);
-                  if (!(E + a <= thr)) {
-                    sel = q;
-                    break;
-                  }
+              } else if (cb < nbl) {
+                r0 = RB + SB_BATCH * SB_NB;
+                r1 = nr;
+                a = readlane_f(accb[SB_NB - 1], lstar);
+              } else {
+                // none exceeds: the lane's last batch (its last round is taken)
+                r0 = RB + SB_BATCH * (nbl - 1);
+                r1 = nr;
+                a = readlane_f(accq[RB - 1], lstar);
+#pragma unroll
+                for (int i = 0; i < SB_NB; ++i)
+                  if (nbl - 1 == i + 1) a = readlane_f(accb[i], lstar);
+              }
+              wk = rewalk(lstar, r0, r1, a, thrE);
+            }
+            if (qsel >= 0) wk.e = (uint32_t)readlane_i((int)ring[s][qsel], lstar);
+            kn = (int)(wk.e & ENT_TOPIC_MASK);
+          } else {
+            kn = pick_a(thr);
+          }
+#ifdef SB_X_NOOWN
+          if (false) {   // attribution experiment only (wrong draws)
+#else
+          if (!FROZEN && lstar >= 0 && kn == zo) {
+#endif
+            // the own entry: keep zo with probability O / w, else one re-draw
+            // with the entry's width replaced by O
+            if (qsel >= 0) {
+              wk.hi = readlane_f(accq[qsel], lstar);
+              wk.lo = qsel > 0 ? readlane_f(accq[qsel > 0 ? qsel - 1 : 0], lstar) : 0.0f;
+            }
+            uint32_t c = wk.e >> ENT_TOPIC_BITS;
+            if (row_sat && c == ENT_COUNT_SAT) c = (uint32_t)KARG(nw)[(int64_t)w * KP + zo];
+            const float wo = wk.hi - wk.lo;
+            const float4 m1 = rm1[s];
+            const float O = (float)(c > 0 ? c - 1 : 0u) * __builtin_fmaf((float)ndz, m1.x, m1.y);
+            const float u1 = u01((uint32_t)readlane_i((int)cx1, idx));
+            if (!(u1 * wo < O)) {
+              // the re-draw (rare): x2 of the token's Philox block, computed
+              // here (the token index passes an opaque register, so the block
+              // is not hoisted into every token)
+              uint32_t gt = (uint32_t)t;
+              asm volatile("" : "+s"(gt));
+              uint32_t y0, y1, y2;
+              philox_x012(gbase + (uint64_t)gt, p.c2, p.c3, p.k0, p.k1, y0, y1, y2);
+              const float s_lo = (lstar > 0 ? readlane_f(TB, lstar - 1) : 0.0f) + wk.lo;
+              const float Tp = ((sumB - wo) + O) + A_f;
+              const float thr2 = uniform_f(u01(y2) * Tp);
+              if (!(thr2 >= s_lo && thr2 < s_lo + O)) {
+                const float th = thr2 < s_lo ? thr2 : uniform_f((thr2 - O) + wo);
+                // the same selection over the same sums, the lane's rounds
+                // re-walked from memory (rows just read: in L2)
+                if (th < sumB) {
+                  const int nl = n < 64 ? n : 64;
+                  const uint64_t m = __ballot((TB > th) && (lane < nl));
+                  const int l2 = m ? (int)__builtin_ctzll(m) : nl - 1;
+                  const float E = l2 > 0 ? readlane_f(TB, l2 - 1) : 0.0f;
+                  const int nr = (n - l2 + 63) >> 6;
+                  kn = (int)(rewalk(l2, 0, nr, 0.0f, th - E).e & ENT_TOPIC_MASK);
+                } else {
+                  kn = pick_a(th);
                 }
-                kn = (int)((uint32_t)readlane_i((int)e, sel) & ENT_TOPIC_MASK);
               }
             }
-          } else {
-            const float thr2 = thr - sumB;
-            const uint64_t m = __ballot((TAs > thr2) && (lane <= last_lane));
-            const int lstar = m ? (int)__builtin_ctzll(m) : last_lane;
-            const float E = lstar > 0 ? readlane_f(TAs, lstar - 1) : 0.0f;
-            // row r takes group r of lane lstar; group prefix P_{r-1} added on top
-            const float x = row_pass(lstar, row % NG, zc, invc);
-            float G[NG];
-#pragma unroll
-            for (int q = 0; q < NG; ++q) G[q] = readlane_f(x, 16 * q + 15);
-            float base = 0.0f, Pq = G[0];
-#pragma unroll
-            for (int q = 1; q < NG; ++q) {
-              if (row == q) base = Pq;
-              Pq = Pq + G[q];
-            }
-            const float val = row == 0 ? x : base + x;
-            const int cnt = __builtin_popcountll(__ballot((E + val <= thr2) && lane < C));
-            const int last_j = (lstar < last_lane) ? C - 1 : (p.K - 1) % C;
-            kn = lstar * C + (cnt < C ? cnt : last_j);
           }
-
-#if SB_DEFER
-          // the add-back waits for the document's next token
+#if SB_REFILL_LAST
+          // the refill after every load of this token (rare paths' waits
+          // would otherwise drain it; the next token's waits still count it)
+          refill();
+#endif
           pk = kn;
-          plo = lo;
-          pgo = go;
-          pln = (int)((uint32_t)kn / (uint32_t)C);
-          pgn = (int)(((uint32_t)kn % (uint32_t)C) / 16u);
-#else
-          // add the token back under its new topic
-          if (lane == 0) nd2[kn >> 1] += (kn & 1) ? 0x10000u : 1u;
-          wave_lds_fence();
-          if (kn == zo) {
-            set_tg(TG, lo, go, g_saved);        // the document is as before the removal
-          } else {
-#if SB_UDIV
-            const int ln = (int)((uint32_t)kn / (uint32_t)C), gn = (int)(((uint32_t)kn % (uint32_t)C) / 16u);
-#else
-            const int ln = kn / C, gn = (kn % C) / 16;
-#endif
-            const float x = row_pass(row == 0 ? lo : ln, row == 0 ? go : gn, -1, 0.0f);
-            const float gl = readlane_f(x, 15), gk = readlane_f(x, 31);
-            set_tg(TG, lo, go, gl);
-            set_tg(TG, ln, gn, gk);
-          }
-#endif
           cn = (lane == idx) ? kn : cn;
         }
       }
@@ -3498,7 +3507,7 @@ static size_t sparse_big_lds() {
   // {alpha, inv} table + per-wave 16-bit nd pairs; > 64 KiB at C = 64
   constexpr size_t lds = (2 * 64 * C + sb_waves<C>() * 32 * C) * sizeof(int32_t);
   static bool attr = [] {
-    return hipFuncSetAttribute(reinterpret_cast<const void*>(&k_sample_sparse_big<C, NS, RB, FROZEN>),
+    return hipFuncSetAttribute(reinterpret_cast<const void*>(&k_sample_big<C, NS, RB, FROZEN>),
                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) == hipSuccess;
   }();
   (void)attr;
@@ -3507,7 +3516,7 @@ static size_t sparse_big_lds() {
 template <int C, int NS, int RB, bool FROZEN>
 static hipError_t launch_sparse_big_rb(const SampleParams& p, int blocks, hipStream_t st) {
   const size_t lds = sparse_big_lds<C, NS, RB, FROZEN>();
-  hipLaunchKernelGGL((k_sample_sparse_big<C, NS, RB, FROZEN>), dim3(blocks), dim3(64 * sb_waves<C>()),
+  hipLaunchKernelGGL((k_sample_big<C, NS, RB, FROZEN>), dim3(blocks), dim3(64 * sb_waves<C>()),
                      lds, st, p);
   return hipGetLastError();
 }
@@ -3523,7 +3532,7 @@ template <int C, bool FROZEN>
 static int occupancy_sparse_big_t() {
   int nb = 0;
   const size_t lds = sparse_big_lds<C, SB_NS, SB_RB, FROZEN>();
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_sample_sparse_big<C, SB_NS, SB_RB, FROZEN>,
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_sample_big<C, SB_NS, SB_RB, FROZEN>,
                                                    64 * sb_waves<C>(), lds) != hipSuccess)
     return 1;
   return nb > 0 ? nb : 1;
@@ -3737,6 +3746,12 @@ hipError_t launch_prepare_topics(int32_t* nwsum, int32_t* dsum, const double* al
                                  float* inv_m1, hipStream_t st) {
   hipLaunchKernelGGL(k_prepare_topics, dim3((Kp + 255) / 256), dim3(256), 0, st, nwsum, dsum, alpha,
                      beta, vbeta, K, Kp, alpha_f, inv, inv_m1);
+  return hipGetLastError();
+}
+
+hipError_t launch_big_tables(const int32_t* nwsum, const float* alpha_f, const float* inv, const float* inv_m1,
+                             int32_t K, int32_t Kp, float beta, const BigTables& t, hipStream_t st) {
+  hipLaunchKernelGGL(k_big_tables, dim3(1), dim3(1024), 0, st, nwsum, alpha_f, inv, inv_m1, K, Kp, beta, t);
   return hipGetLastError();
 }
 

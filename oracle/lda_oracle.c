@@ -1,3 +1,4 @@
+#define _GNU_SOURCE
 /*
  * lda_oracle.c — CPU restatements of the collapsed-Gibbs LDA hot path.
  *
@@ -14,6 +15,8 @@
 
 #include <math.h>
 #include <pthread.h>
+#include <sched.h>
+#include <time.h>
 #include <stdlib.h>
 #include <string.h>
 #include <unistd.h>
@@ -55,6 +58,13 @@ uint32_t orc_draw(uint64_t seed, uint64_t gtok, uint32_t c2, uint32_t c3) {
   uint32_t out[4];
   orc_philox4x32_10(ctr, key, out);
   return out[0];
+}
+
+/* all four words of the token's Philox block (the large-K draw uses x1, x2) */
+void orc_draw4(uint64_t seed, uint64_t gtok, uint32_t c2, uint32_t c3, uint32_t out[4]) {
+  uint32_t ctr[4] = {(uint32_t)gtok, (uint32_t)(gtok >> 32), c2, c3};
+  uint32_t key[2] = {(uint32_t)seed, (uint32_t)(seed >> 32)};
+  orc_philox4x32_10(ctr, key, out);
 }
 
 float orc_u01(uint32_t x) { return (float)(x >> 8) * 0x1p-24f; }
@@ -234,12 +244,56 @@ struct orc_exact {
   float beta_f, vbeta_f;
   float* inv;    /* Kp: 1/(nwsum + V*beta), 0 in the padding */
   float* inv_m1; /* Kp: 1/(nwsum - 1 + V*beta) */
+  /* the large-K draw's tables (exact_draw_big; lda_kernels.hip k_big_tables) */
+  float* ainv;    /* Kp: alpha_f * inv */
+  float* ainv_m1; /* Kp: alpha_f * inv_m1 (0 for a topic with no tokens) */
+  uint32_t *bF, *bFm1, *bG, *bGm1; /* Kp: big_fix of inv, inv_m1, ainv, ainv_m1 */
+  uint64_t* bpfx; /* Kp: inclusive prefix of bG */
+  int32_t bS;     /* fixed-point exponent */
+  uint64_t bS0;   /* sum of bG */
+  float bsig, bsig_hi; /* beta * 2^-S, beta * 2^(32-S) */
+  double isig;         /* 2^S / beta */
   uint64_t seed;
   int64_t token_base;
   uint32_t sweep;
   int kind; /* 0 = dense draw, 1 = sparse (SparseLDA-split) draw */
   int half; /* dense, K <= 128: 1 = the half-wave variant's draw, 2 = the quarter-wave one */
 };
+
+/* The large-K draw's fixed-point doc part (ldagibbssampling_amd/csrc/
+ * lda_kernels.hip: k_big_tables).  m = the largest of inv_k, ainv_k and, for
+ * topics holding tokens, inv_m1_k and ainv_m1_k; S = 31 - e with m = f 2^e,
+ * f in [0.5, 1), so big_fix(x) = (uint32) ldexpf(x, S) < 2^31 for every table
+ * value (a power-of-two scaling is exact; the conversion truncates). */
+static uint32_t big_fix(float x, int S) { return (uint32_t)ldexpf(x, S); }
+
+static void exact_big_tables(orc_exact* s) {
+  float m = 0.0f;
+  for (int k = 0; k < s->Kp; ++k) {
+    const int live = k < s->K && s->nwsum[k] >= 1;
+    s->ainv[k] = s->alpha_f[k] * s->inv[k];
+    s->ainv_m1[k] = live ? s->alpha_f[k] * s->inv_m1[k] : 0.0f;
+    const float im1 = live ? s->inv_m1[k] : 0.0f;
+    m = fmaxf(m, fmaxf(fmaxf(s->inv[k], s->ainv[k]), fmaxf(im1, s->ainv_m1[k])));
+  }
+  int e = 0;
+  (void)frexpf(m, &e);
+  s->bS = m > 0.0f ? 31 - e : 0;
+  uint64_t acc = 0;
+  for (int k = 0; k < s->Kp; ++k) {
+    const int live = k < s->K && s->nwsum[k] >= 1;
+    s->bF[k] = big_fix(s->inv[k], s->bS);
+    s->bFm1[k] = live ? big_fix(s->inv_m1[k], s->bS) : 0u;
+    s->bG[k] = big_fix(s->ainv[k], s->bS);
+    s->bGm1[k] = big_fix(s->ainv_m1[k], s->bS);
+    acc += s->bG[k];
+    s->bpfx[k] = acc;
+  }
+  s->bS0 = acc;
+  s->bsig = ldexpf(s->beta_f, -s->bS);
+  s->bsig_hi = ldexpf(s->beta_f, 32 - s->bS);
+  s->isig = ldexp(1.0, s->bS) / (double)s->beta_f;
+}
 
 static void exact_prepare_topics(orc_exact* s) {
   for (int k = 0; k < s->Kp; ++k) {
@@ -253,6 +307,7 @@ static void exact_prepare_topics(orc_exact* s) {
       s->inv_m1[k] = 0.0f;
     }
   }
+  exact_big_tables(s);
 }
 
 orc_exact* orc_exact_create(int32_t K, int32_t V, int64_t D, const int64_t* doc_off,
@@ -285,6 +340,13 @@ orc_exact* orc_exact_create(int32_t K, int32_t V, int64_t D, const int64_t* doc_
   s->alpha_f = (float*)calloc(s->Kp, sizeof(float));
   s->inv = (float*)calloc(s->Kp, sizeof(float));
   s->inv_m1 = (float*)calloc(s->Kp, sizeof(float));
+  s->ainv = (float*)calloc(s->Kp, sizeof(float));
+  s->ainv_m1 = (float*)calloc(s->Kp, sizeof(float));
+  s->bF = (uint32_t*)calloc(s->Kp, sizeof(uint32_t));
+  s->bFm1 = (uint32_t*)calloc(s->Kp, sizeof(uint32_t));
+  s->bG = (uint32_t*)calloc(s->Kp, sizeof(uint32_t));
+  s->bGm1 = (uint32_t*)calloc(s->Kp, sizeof(uint32_t));
+  s->bpfx = (uint64_t*)calloc(s->Kp, sizeof(uint64_t));
   s->beta_f = (float)beta;
   s->vbeta_f = (float)((double)V * beta);
   s->seed = seed;
@@ -313,6 +375,8 @@ void orc_exact_destroy(orc_exact* s) {
   if (!s) return;
   free(s->doc_off); free(s->words); free(s->z); free(s->nw); free(s->nwsum); free(s->delta);
   free(s->alpha); free(s->alpha_f); free(s->inv); free(s->inv_m1);
+  free(s->ainv); free(s->ainv_m1); free(s->bF); free(s->bFm1); free(s->bG); free(s->bGm1);
+  free(s->bpfx);
   free(s);
 }
 
@@ -633,6 +697,147 @@ static int exact_draw_sparse(const orc_exact* s, const int32_t* nwrow, const int
   return lstar * C + jsel;
 }
 
+/* The large-K sparse draw (kind 1, C >= 32; lda_kernels.hip: k_sample_big,
+ * round 5).  The same p_k = (nd_k + a_k)(nw_k + b) inv_k, split as
+ *   B (word part) over the word's nonzero entries e (topic ascending, lane l
+ *     holding e = l, l+64, ...), WITHOUT the own-token correction:
+ *       coef_t = fmaf(float(nd_t), inv_t, ainv_t), ainv = alpha * inv
+ *       acc_l  = fmaf(float(c_e), coef_{t_e}, acc_l)   (per-lane running sum)
+ *     TB = the kernel's DPP wave scan of acc_l (wave_scan_emulate).
+ *   A (doc part, beta * sum_k (nd_k + a_k) inv'_k) exactly, in fixed point:
+ *       A_fx = sum_k nd_k F'_k + sum_k G'_k  (uint64; F = big_fix(inv),
+ *       G = big_fix(ainv); ' = the _m1 values at the token's own topic zo)
+ *       A_f  = fmaf(float(A_fx >> 32), beta 2^(32-S), float((uint32) A_fx) * beta 2^-S)
+ *   thr = u0 * (sumB + A_f).
+ * Selection (big_select): B first: the first lane with TB > thr, then the
+ * count of its running sums <= thr - E; else A: tfx = floor(double(thr -
+ * sumB) * isig), first the alpha part (prefix of G', topic ascending), then
+ * the document part (prefix of nd F', topic ascending); K-1 when none.
+ * The own token: B holds its entry as x = c * coef_zo where the exact weight
+ * is O = (c - 1) * fmaf(nd_zo, inv_m1_zo, ainv_m1_zo) <= x.  A draw that lands
+ * on it keeps zo when u1 * w < O (w = the entry's width in its lane's running
+ * sums); otherwise the draw is repeated once over the same sums with the
+ * entry's width replaced by O (thr2 = u2 * T', mapped around the entry), which
+ * makes the result exactly the corrected distribution. */
+typedef struct {
+  int n;               /* word entries */
+  const int32_t *et, *ec;
+  const float* acc_e;  /* acc_e[e]: lane (e & 63)'s running sum after entry e */
+  float TB[64];
+  float sumB, A_f;
+  uint64_t As;         /* the alpha part of A_fx */
+  int64_t dG;          /* G'_zo - G_zo (0 when frozen) */
+  int zo;              /* -1 when frozen */
+} big_draw;
+
+static int big_select(const orc_exact* s, const big_draw* d, const int32_t* nd, float thr, int* entry) {
+  *entry = -1;
+  if (thr < d->sumB) {
+    const int nl = d->n < 64 ? d->n : 64;
+    int lstar = nl - 1;
+    for (int l = 0; l < nl; ++l)
+      if (d->TB[l] > thr) {
+        lstar = l;
+        break;
+      }
+    const float E = lstar > 0 ? d->TB[lstar - 1] : 0.0f;
+    const float thrE = thr - E;
+    const int nr = (d->n - lstar + 63) / 64;
+    int cnt = 0;
+    for (int q = 0; q < nr; ++q) cnt += (d->acc_e[lstar + 64 * q] <= thrE) ? 1 : 0;
+    *entry = lstar + 64 * (cnt < nr ? cnt : nr - 1);
+    return d->et[*entry];
+  }
+  const float t2 = thr - d->sumB;
+  const uint64_t tfx = (uint64_t)((double)t2 * s->isig);
+  if (tfx < d->As) {
+    for (int k = 0; k < s->K; ++k) {
+      const int64_t v = (int64_t)s->bpfx[k] + (d->zo >= 0 && k >= d->zo ? d->dG : 0);
+      if ((uint64_t)v > tfx) return k;
+    }
+    return s->K - 1;
+  }
+  const uint64_t tr = tfx - d->As;
+  uint64_t acc = 0;
+  for (int k = 0; k < s->K; ++k) {
+    acc += (uint64_t)nd[k] * (k == d->zo ? s->bFm1[k] : s->bF[k]);
+    if (acc > tr) return k;
+  }
+  return s->K - 1;
+}
+
+static int exact_draw_big(const orc_exact* s, const int32_t* nwrow, const int32_t* nd, int zo,
+                          const uint32_t x[4], int32_t* et, int32_t* ec, float* acc_e) {
+  const int K = s->K;
+  big_draw d;
+  d.n = 0;
+  for (int k = 0; k < K; ++k)
+    if (nwrow[k] > 0) {
+      et[d.n] = k;
+      ec[d.n] = nwrow[k];
+      d.n++;
+    }
+  for (int l = 0; l < 64; ++l) {
+    float acc = 0.0f;
+    for (int e = l; e < d.n; e += 64) {
+      const int t = et[e];
+      acc = fmaf((float)ec[e], fmaf((float)nd[t], s->inv[t], s->ainv[t]), acc);
+      acc_e[e] = acc;
+    }
+    d.TB[l] = acc;
+  }
+  wave_scan_emulate(d.TB);
+  d.sumB = d.TB[63];
+  uint64_t R = 0;
+  for (int k = 0; k < s->Kp; ++k) R += (uint64_t)nd[k] * s->bF[k];
+  int64_t dF = 0;
+  d.dG = 0;
+  if (zo >= 0) {
+    dF = (int64_t)nd[zo] * ((int64_t)s->bFm1[zo] - (int64_t)s->bF[zo]);
+    d.dG = (int64_t)s->bGm1[zo] - (int64_t)s->bG[zo];
+  }
+  d.zo = zo;
+  d.As = (uint64_t)((int64_t)s->bS0 + d.dG);
+  const uint64_t Afx = (uint64_t)((int64_t)(d.As + R) + dF);
+  /* fp32: beta 2^-S (hi 2^32 + lo); hi < 2^16 is exact */
+  d.A_f = fmaf((float)(uint32_t)(Afx >> 32), s->bsig_hi, (float)(uint32_t)Afx * s->bsig);
+  d.et = et;
+  d.ec = ec;
+  d.acc_e = acc_e;
+  const float T = d.sumB + d.A_f;
+  int entry;
+  const int kn = big_select(s, &d, nd, orc_u01(x[0]) * T, &entry);
+  if (zo < 0 || entry < 0 || kn != zo) return kn;
+  /* the own entry */
+  const float hi = acc_e[entry], lo = entry >= 64 ? acc_e[entry - 64] : 0.0f;
+  const float w = hi - lo;
+  const int32_t cm1 = ec[entry] > 0 ? ec[entry] - 1 : 0;
+  const float O = (float)cm1 * fmaf((float)nd[zo], s->inv_m1[zo], s->ainv_m1[zo]);
+  if (orc_u01(x[1]) * w < O) return zo;
+  const int l = entry & 63;
+  const float s_lo = (l > 0 ? d.TB[l - 1] : 0.0f) + lo;
+  const float Tp = ((d.sumB - w) + O) + d.A_f;
+  const float thr2 = orc_u01(x[2]) * Tp;
+  if (thr2 < s_lo) return big_select(s, &d, nd, thr2, &entry);
+  if (thr2 < s_lo + O) return zo;
+  return big_select(s, &d, nd, (thr2 - O) + w, &entry);
+}
+
+/* Test hook: one large-K draw for word w with document counts nd (the token
+ * already removed), old topic zo (-1: frozen) and Philox words x[0..2]
+ * (tests/test_oracle.py checks its distribution against the exact
+ * conditional). */
+int orc_exact_big_draw(const orc_exact* s, int32_t w, const int32_t* nd, int32_t zo, const uint32_t* x) {
+  int32_t* et = (int32_t*)malloc(sizeof(int32_t) * s->Kp);
+  int32_t* ec = (int32_t*)malloc(sizeof(int32_t) * s->Kp);
+  float* acc_e = (float*)malloc(sizeof(float) * s->Kp);
+  const int kn = exact_draw_big(s, s->nw + (size_t)w * s->Kp, nd, zo, x, et, ec, acc_e);
+  free(et);
+  free(ec);
+  free(acc_e);
+  return kn;
+}
+
 /* Sample the docs [d0, d1) of a token stream against the snapshot.  frozen:
  * no self-correction (inference).  The snapshot is read-only and nd is per
  * document, so disjoint document blocks are independent; the count changes
@@ -645,7 +850,9 @@ static void exact_sample_docs(const orc_exact* s, const int64_t* doc_off, const 
   int32_t* et = (int32_t*)malloc(sizeof(int32_t) * s->Kp);
   int32_t* ec = (int32_t*)malloc(sizeof(int32_t) * s->Kp);
   float* af = (float*)malloc(sizeof(float) * s->Kp);
+  float* acc_e = (float*)malloc(sizeof(float) * s->Kp);
   const int quarter = s->kind == 0 && s->half == 2 && s->Kp <= 128;
+  const int big = s->kind == 1 && s->C >= 32;
   for (int64_t d = d0; d < d1; ++d) {
     memset(nd, 0, sizeof(int32_t) * s->Kp);
     for (int64_t i = doc_off[d]; i < doc_off[d + 1]; ++i) nd[z[i]]++;
@@ -654,10 +861,13 @@ static void exact_sample_docs(const orc_exact* s, const int64_t* doc_off, const 
     for (int64_t i = doc_off[d]; i < doc_off[d + 1]; ++i) {
       int w = words[i];
       int zo = z[i];
-      float u = orc_u01(orc_draw(s->seed, (uint64_t)(token_base + i), c2, c3));
+      uint32_t x[4];
+      orc_draw4(s->seed, (uint64_t)(token_base + i), c2, c3, x);
+      float u = orc_u01(x[0]);
       nd[zo]--;
       af[zo] -= 1.0f;
-      int kn = s->kind == 1
+      int kn = big ? exact_draw_big(s, s->nw + (size_t)w * s->Kp, nd, frozen ? -1 : zo, x, et, ec, acc_e)
+               : s->kind == 1
                    ? exact_draw_sparse(s, s->nw + (size_t)w * s->Kp, nd, frozen ? -1 : zo, u, S, et, ec)
                    : quarter
                          ? exact_draw_quarter(s, s->nw + (size_t)w * s->Kp, af, frozen ? -1 : zo, u, S)
@@ -670,6 +880,7 @@ static void exact_sample_docs(const orc_exact* s, const int64_t* doc_off, const 
     }
   }
   free(af);
+  free(acc_e);
   free(nd);
   free(S);
   free(et);
@@ -960,6 +1171,10 @@ struct orc_mallet {
   /* hyperparameter optimisation (setOptimizeInterval / setBurninPeriod) */
   int32_t optimize_interval, burnin, save_sample_interval, symmetric_alpha;
   int32_t max_len;
+  /* wall time of the sweeps' sampling (the workers' parallel section) and of
+   * the sumTypeTopicCounts merge (orc_mallet_timing; bench.py cpu_baseline) */
+  double t_sample, t_merge;
+  int pin_threads;   /* 1: worker t pinned to the t-th CPU of the affinity mask */
 };
 
 static int32_t** ttc_alloc(const orc_mallet* m) {
@@ -1403,24 +1618,57 @@ static void mallet_sum_type_topic_counts(orc_mallet* m) {
   }
 }
 
+static double wall_s(void) {
+  struct timespec ts;
+  clock_gettime(CLOCK_MONOTONIC, &ts);
+  return (double)ts.tv_sec + 1e-9 * (double)ts.tv_nsec;
+}
+
+void orc_mallet_set_pin_threads(orc_mallet* m, int32_t on) { m->pin_threads = on; }
+void orc_mallet_timing(orc_mallet* m, double* sample_s, double* merge_s, int32_t reset) {
+  if (sample_s) *sample_s = m->t_sample;
+  if (merge_s) *merge_s = m->t_merge;
+  if (reset) m->t_sample = m->t_merge = 0.0;
+}
+
 void orc_mallet_estimate(orc_mallet* m, int32_t n_iter) {
   mallet_job* jobs = (mallet_job*)malloc(sizeof(mallet_job) * m->T);
   pthread_t* th = (pthread_t*)malloc(sizeof(pthread_t) * m->T);
+  /* the CPUs this process may run on, for pinning worker t to the t-th */
+  cpu_set_t mask;
+  int ncpu = 0, cpus[1024];
+  if (m->pin_threads && sched_getaffinity(0, sizeof mask, &mask) == 0)
+    for (int c = 0; c < CPU_SETSIZE && ncpu < 1024; ++c)
+      if (CPU_ISSET(c, &mask)) cpus[ncpu++] = c;
   for (int it = 1; it <= n_iter; ++it) {
     const int opt_on = it > m->burnin && m->optimize_interval != 0;
     for (int t = 0; t < m->T; ++t) m->workers[t].collect = opt_on && it % m->save_sample_interval == 0;
+    const double t0 = wall_s();
     if (m->T > 1) {
       for (int t = 0; t < m->T; ++t) {
         jobs[t].m = m;
         jobs[t].t = t;
-        pthread_create(&th[t], NULL, mallet_worker_run, &jobs[t]);
+        pthread_attr_t at;
+        pthread_attr_init(&at);
+        if (ncpu > 0) {
+          cpu_set_t one;
+          CPU_ZERO(&one);
+          CPU_SET(cpus[t % ncpu], &one);
+          pthread_attr_setaffinity_np(&at, sizeof one, &one);
+        }
+        pthread_create(&th[t], &at, mallet_worker_run, &jobs[t]);
+        pthread_attr_destroy(&at);
       }
       for (int t = 0; t < m->T; ++t) pthread_join(th[t], NULL);
+      const double t1 = wall_s();
       mallet_sum_type_topic_counts(m);
+      m->t_sample += t1 - t0;
+      m->t_merge += wall_s() - t1;
     } else {
       jobs[0].m = m;
       jobs[0].t = 0;
       mallet_worker_run(&jobs[0]);
+      m->t_sample += wall_s() - t0;
     }
     for (int t = 0; t < m->T; ++t) m->workers[t].collect = 0;
     if (opt_on && it % m->optimize_interval == 0) {

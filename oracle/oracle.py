@@ -85,6 +85,9 @@ def lib():
     L.orc_exact_log_likelihood.argtypes = [C.c_void_p]
     L.orc_exact_log_likelihood_parts.argtypes = [C.c_void_p, C.POINTER(C.c_double),
                                                  C.POINTER(C.c_double)]
+    L.orc_exact_big_draw.restype = C.c_int
+    L.orc_exact_big_draw.argtypes = [C.c_void_p, C.c_int32, _i32p, C.c_int32,
+                                     np.ctypeslib.ndpointer(dtype=np.uint32, flags="C_CONTIGUOUS")]
     L.orc_exact_infer.argtypes = [C.c_void_p, C.c_int64, _i64p, _i32p, C.c_int32, C.c_int32,
                                   C.c_int32, C.c_uint64, _f64p]
 
@@ -93,6 +96,8 @@ def lib():
                                     _i64p, _i32p, C.c_int64, C.c_int32]
     L.orc_mallet_destroy.argtypes = [C.c_void_p]
     L.orc_mallet_estimate.argtypes = [C.c_void_p, C.c_int32]
+    L.orc_mallet_set_pin_threads.argtypes = [C.c_void_p, C.c_int32]
+    L.orc_mallet_timing.argtypes = [C.c_void_p, C.POINTER(C.c_double), C.POINTER(C.c_double), C.c_int32]
     L.orc_mallet_set_optimize.argtypes = [C.c_void_p, C.c_int32, C.c_int32, C.c_int32]
     L.orc_mallet_get_hyper.argtypes = [C.c_void_p, _f64p, C.POINTER(C.c_double)]
     L.orc_mallet_log_likelihood.restype = C.c_double
@@ -381,6 +386,14 @@ class ExactSampler:
         lib().orc_exact_log_likelihood_parts(self._h, C.byref(a), C.byref(b))
         return a.value, b.value
 
+    def big_draw(self, w: int, nd, zo: int, x) -> int:
+        """One large-K draw (exact_draw_big) for word w, document counts nd
+        [Kp] without the token, old topic zo (-1: frozen), Philox words x[0..2]."""
+        nd = np.ascontiguousarray(nd, dtype=np.int32)
+        assert nd.shape == (self.Kp,)
+        x = np.ascontiguousarray(x, dtype=np.uint32)
+        return int(lib().orc_exact_big_draw(self._h, int(w), nd, int(zo), x))
+
     def infer(self, doc_off, words, n_iter=100, burn_in=10, thin=10, seed=0):
         doc_off = np.ascontiguousarray(doc_off, dtype=np.int64)
         words = np.ascontiguousarray(words, dtype=np.int32)
@@ -409,6 +422,16 @@ class MalletModel:
         if h:
             lib().orc_mallet_destroy(h)
             self._h = None
+
+    def set_pin_threads(self, on: bool = True):
+        """Pin worker t to the t-th CPU of this process's affinity mask."""
+        lib().orc_mallet_set_pin_threads(self._h, 1 if on else 0)
+
+    def timing(self, reset: bool = False):
+        """(sampling s, sumTypeTopicCounts merge s) accumulated by estimate()."""
+        a, b = C.c_double(), C.c_double()
+        lib().orc_mallet_timing(self._h, C.byref(a), C.byref(b), 1 if reset else 0)
+        return a.value, b.value
 
     def estimate(self, n_iter):
         lib().orc_mallet_estimate(self._h, int(n_iter))

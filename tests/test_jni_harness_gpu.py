@@ -26,10 +26,11 @@ from ldagibbssampling_amd.corpus import Corpus, synthetic_lda
 pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 HARNESS = os.path.join(ROOT, "tests", "jni", "bin", "estimate_harness")
+FAKE = os.path.join(ROOT, "tests", "jni", "bin", "fake_env")
 
 
-def _run(K, V, corpus, z, alpha, hyper, sweep, options, seed):
-    assert os.path.exists(HARNESS), "build() compiles tests/jni/bin/estimate_harness"
+def _run(K, V, corpus, z, alpha, hyper, sweep, options, seed, prog=HARNESS):
+    assert os.path.exists(prog), "build() compiles tests/jni/bin/estimate_harness and fake_env"
     D = corpus.num_docs
     with tempfile.TemporaryDirectory() as d:
         fin, fout = os.path.join(d, "in.bin"), os.path.join(d, "out.bin")
@@ -43,7 +44,7 @@ def _run(K, V, corpus, z, alpha, hyper, sweep, options, seed):
             f.write(np.array([sweep], np.int64).tobytes())
             f.write(np.asarray(options, np.int32).tobytes())
             f.write(np.array([seed], np.int64).tobytes())
-        r = subprocess.run([HARNESS, fin, fout], capture_output=True, text=True, timeout=120)
+        r = subprocess.run([prog, fin, fout], capture_output=True, text=True, timeout=120)
         assert r.returncode == 0, r.stderr
         buf = open(fout, "rb").read()
     N = corpus.num_tokens
@@ -256,3 +257,22 @@ def test_estimate_ending_between_statistics_and_optimisation(oracle):
         iters, iters2, interval, burnin, save, threads=2)
     _check(out2, o2, alpha2, alpha_sum2, beta2, ll2, K, V, iters2)
     assert out2["sweep"] == iters + iters2
+
+
+def test_jni_glue_through_a_fake_jnienv_equals_the_harness():
+    """integration/jni/lda_jni.c itself (tests/jni/fake_env.c: HotSpot-like
+    copying arrays, every pin released exactly once, outputs copied back with
+    mode 0 and inputs released with JNI_ABORT) gives the harness's z, alpha,
+    hyper, sweep counter, packed rows, tokensPerTopic and LL trace bit for bit,
+    at numThreads 4 with optimisation and at K > 1024."""
+    for K, opts in ((20, [40, 10, 10, 10, 0, 4, 0]), (1500, [12, 200, 0, 10, 0, 1, 0])):
+        c = synthetic_lda(num_docs=60, num_types=200, num_topics=20, doc_len=None, mean_len=30,
+                          min_len=1, max_len=80, seed=K)
+        rng = np.random.default_rng(K)
+        z0 = rng.integers(0, K, size=c.num_tokens).astype(np.int32)
+        alpha0 = np.full(K, 0.1)
+        hyper0 = [0.1 * K, 0.01, 0.01 * c.num_types]
+        a = _run(K, c.num_types, c, z0, alpha0, hyper0, 3, opts, 11)
+        b = _run(K, c.num_types, c, z0, alpha0, hyper0, 3, opts, 11, prog=FAKE)
+        for key in a:
+            np.testing.assert_array_equal(np.asarray(a[key]), np.asarray(b[key]), err_msg=key)
