@@ -250,7 +250,16 @@ def cpu_baseline(corpus, K, alpha_sum, beta, budget_s=15.0, threads=4, runs=3):
     }
 
 
-def estimate_side_figure(device: int, iters: int = 100, burnin: int = 50):
+SIDE_WORKLOADS = {
+    # the C4 shard (block 0 of C4) and C2 (BASELINE configs[1]: K = 128, the
+    # reference's K <= 128 regime, src/cmu/TrainAndPredict.java:259 K = 100)
+    "c4": dict(docs=1_250_000, V=100_000, K=512,
+               desc="C4 shard (block 0 of C4: 1.25M docs x 200 tok, V=100k, K=512), one GPU"),
+    "c2": dict(docs=100_000, V=50_000, K=128, desc="C2 (100k docs x 200 tok, V=50k, K=128), one GPU"),
+}
+
+
+def estimate_side_figure(device: int, iters: int = 100, burnin: int = 50, workload: str = "c4"):
     """What the drop-in delivers: the native
     ParallelTopicModel (liblda_topic_model.so, the host mirror the JNI shim
     drives) running estimate() on the C4 shard (block 0 of the C4 corpus:
@@ -267,8 +276,9 @@ def estimate_side_figure(device: int, iters: int = 100, burnin: int = 50):
     from ldagibbssampling_amd.corpus import synthetic_lda_torch
     from ldagibbssampling_amd.topic_model import _check, load_tm
     L = load_tm()
-    K, V = 512, 100_000
-    c = synthetic_lda_torch(1_250_000, V, K, doc_len=200, seed=20261015, doc_seed=20261015,
+    wl = SIDE_WORKLOADS[workload]
+    K, V = wl["K"], wl["V"]
+    c = synthetic_lda_torch(wl["docs"], V, K, doc_len=200, seed=20261015, doc_seed=20261015,
                             device=f"cuda:{device}")
     h = C.c_void_p()
     _check(L.ldatm_create(C.byref(h), K, 0.1 * K, 0.01), "ldatm_create")
@@ -306,7 +316,8 @@ def estimate_side_figure(device: int, iters: int = 100, burnin: int = 50):
         "iterations": iters,
         "tokens": n,
         "shard_build_s": t_build,
-        "workload": "C4 shard (block 0 of C4: 1.25M docs x 200 tok, V=100k, K=512), one GPU",
+        "workload": wl["desc"],
+        "count_update": os.environ.get("LDA_RECOUNT", "auto (default)"),
         "settings": (f"native ParallelTopicModel.estimate(): setNumThreads(4) (one GPU shard; "
                      f"sweeps with 4 threads' staleness), warm start 4 x 50 (default), LL/token "
                      f"every 10, setOptimizeInterval(20), setBurninPeriod({burnin}) -> "
@@ -492,6 +503,10 @@ def main():
     count_mode = sampler.count_update()
     copy_gbs = stream_copy_gbs(device) if rank == 0 else None
 
+    # every rank's replica of nw / nwsum must be identical after the timed
+    # region (lda_counts_checksum + the LL's word part, MIN == MAX over the
+    # ranks), and the ranks' own timed-region seconds travel with the line
+    replicas = trainer.replica_check(seconds=elapsed)
     t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{device}")
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -549,6 +564,7 @@ def main():
         if trainer.exchange:
             xb = trainer.exchange_bytes()
             nbytes = xb["allreduce_bytes"] + xb["allgather_bytes"]
+            rs = replicas.get("rank_seconds") or []
             int32_bytes = 4 * (V * sampler.Kp + sampler.Kp)
             # modelled time of one exchange at N = 8 on one ring over xGMI links of
             # ~153 GB/s (the per-link figure; RCCL's several rings only cut it):
@@ -557,7 +573,11 @@ def main():
             model8 = (2 * 7 / 8 * xb["allreduce_bytes"] + 7 / 8 * xb["allgather_bytes"] * 8 / world) / link
             coll = {"op": (("compact exchange (lda_exchange_pack: two cells per int32 word + escape "
                             "lists): all_reduce(SUM, int32) of the packed words + all_gather of the "
-                            "escape lists" if trainer.compact else
+                            "escape lists" + (" at their used length (after a MAX all_reduce of the "
+                                              "counts; none gathered when no rank has one)"
+                                              if trainer.escape_lists == "used" else
+                                              " at their full capacity")
+                            if trainer.compact else
                             "all_reduce(SUM, int32) of the nw/nwsum delta")
                            + (", once per sweep" if parts == 1 else
                               f", for each of {parts} sweep parts, part i's overlapping part "
@@ -568,6 +588,14 @@ def main():
                     "bytes_per_sweep": nbytes * parts,
                     "allreduce_bytes_per_part": xb["allreduce_bytes"],
                     "allgather_bytes_per_part": xb["allgather_bytes"],
+                    "allgather_capacity_bytes_per_part": xb.get("allgather_capacity_bytes"),
+                    "escape_lists": xb.get("escape_lists", "none (int32 exchange)"),
+                    "escape_count_max": xb.get("escape_count_max"),
+                    "replicas_agree": replicas["replicas_agree"],
+                    "counts_checksum": replicas["counts_checksum"],
+                    "world_size": replicas["world_size"],
+                    "ranks_counted": replicas["ranks_counted"],
+                    "rank_ms_per_sweep": [1e3 * x / args.steps for x in rs],
                     "int32_bytes_per_sweep": int32_bytes * parts,
                     "ring_bytes_per_rank_per_sweep": 2 * (world - 1) * xb["allreduce_bytes"] * parts // world,
                     "modelled_n8_ms_per_sweep": model8 * parts * 1e3,
@@ -664,8 +692,8 @@ def main():
         }
         if nnz0 is not None:
             result["roofline"]["mean_row_nnz"] = [nnz0, nnz1]
-        if world == 1 and not args.no_estimate and args.config in ("c4", "c4shard") and not args.docs:
-            result["estimate_side"] = estimate_side_figure(device)
+        if world == 1 and not args.no_estimate and args.config in ("c4", "c4shard", "c2") and not args.docs:
+            result["estimate_side"] = estimate_side_figure(device, workload="c2" if args.config == "c2" else "c4")
         if world == 1 and not args.no_cpu_baseline:
             result["cpu_baseline"] = cpu_baseline(corpus, K, alpha_sum, beta, args.cpu_budget)
         print(json.dumps(result), flush=True)

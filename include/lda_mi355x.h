@@ -204,6 +204,24 @@ lda_status lda_exchange_pack(lda_ctx* ctx, int32_t part, int32_t world, int64_t 
                              void** escapes);
 lda_status lda_exchange_unpack(lda_ctx* ctx, int32_t part, int32_t world, int64_t max_shard_tokens,
                                const void* escapes_all);
+/* The escape lists sent at their used length (ldagibbssampling_amd/
+ * distributed.py): escapes[0] after lda_exchange_pack is the rank's escape
+ * count n (n > escape capacity cannot happen when every rank's shard holds at
+ * most max_shard_tokens tokens; a driver that reads n > capacity must stop).
+ * A driver that MAX-all-reduces n into m (identical on every rank) may
+ * all-gather only the first 1 + 3 m int32 of each rank's list into
+ * [world x (1 + 3 m)] and unpack with list_cap = m; m = 0 needs no all-gather
+ * (escapes_all may be NULL).  list_cap in [0, capacity]; lda_exchange_unpack
+ * is list_cap = capacity. */
+lda_status lda_exchange_unpack_lists(lda_ctx* ctx, int32_t part, int32_t world, int64_t max_shard_tokens,
+                                     const void* escapes_all, int32_t list_cap);
+/* Replica check (bench.py's multi-GPU line): a hash of the applied counts,
+ * the sum mod 2^64 over the nonzero cells of nw (V x K) and nwsum (K) of
+ * splitmix64's finaliser applied to (index << 32 | (uint32)value), index =
+ * w K + k in nw and V K + k in nwsum (oracle.counts_checksum).  Every rank of
+ * an AD-LDA group holds the same replica, so MIN == MAX over the ranks.
+ * LDA_ERR_STATE with a pending delta.  Synchronises the context's stream. */
+lda_status lda_counts_checksum(lda_ctx* ctx, uint64_t* checksum);
 
 /* Warm start.  The GPU sweep samples every document against one snapshot
  * (AD-LDA), while Mallet's setNumThreads(4) workers each see their own
@@ -422,8 +440,11 @@ void lda_debug_fail_host_alloc(int32_t nth);
  * lda_recount_times, lda_set_exchange_parts' reserve_cus < 0 = default; 4 --
  * lda_hyper_statistics, lda_set_alpha_beta returns without waiting for the
  * stream (its upload is asynchronous); 5 -- warm-start parts are interleaved
- * segments of the corpus (LDA_WARM_BLOCKS), lda_warm_part_tokens. */
-#define LDA_ABI_VERSION 5
+ * segments of the corpus (LDA_WARM_BLOCKS), lda_warm_part_tokens; 6 -- the
+ * large-K sampler's draw (C >= 32: exact fixed-point doc part, own-entry
+ * accept / re-draw), sequential sweeps recount under LDA_COUNT_RECOUNT,
+ * lda_exchange_unpack_lists, lda_counts_checksum. */
+#define LDA_ABI_VERSION 6
 const char* lda_version(void);
 int32_t lda_abi_version(void);
 

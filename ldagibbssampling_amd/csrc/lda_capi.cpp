@@ -666,12 +666,15 @@ static int sweep_parts(const lda_ctx* c) {
   return seq ? seq_schedule(c).parts : c->parts;
 }
 
-// Will the next sweep recount?  (never a warm-start sweep: its parts are
-// applied one by one as changes)
+// Will the next sweep recount?  A sequential sweep (warm start, staleness)
+// recounts the WHOLE shard after each of its parts (the parts are applied one
+// by one, and absolute counts must include every token), so its recount
+// costs a full pass per part: AUTO keeps it to plain sweeps (its measured
+// crossover), LDA_COUNT_RECOUNT makes every sweep recount.
 static bool next_sweep_recounts(const lda_ctx* c) {
-  if (!c->recount_ok || next_sweep_sequential(c)) return false;
+  if (!c->recount_ok) return false;
   if (c->count_mode == LDA_COUNT_RECOUNT) return true;
-  if (c->count_mode == LDA_COUNT_DELTA) return false;
+  if (c->count_mode == LDA_COUNT_DELTA || next_sweep_sequential(c)) return false;
   return c->sweeps_since_seed < c->recount_sweeps;
 }
 
@@ -1074,17 +1077,26 @@ static lda_status sample_part_impl(lda_ctx* c, int part) {
     if (probe >= 0) HIP_TRY(hipEventRecord(c->big_ev[probe][1], c->stream));
     HIP_TRY(hipEventRecord(c->ev1[slot], c->stream));
     if (c->sweep_recount) {
-      // this part's rows recounted into its exchange buffer (the apply left
-      // it zero)
-      const int64_t i0 = c->part_item[(size_t)part], i1 = c->part_item[(size_t)part + 1];
+      // a split sweep: this part's rows recounted into its exchange buffer
+      // (the apply left it zero; the parts' buffers sum to the counts); a
+      // sequential sweep: every token (the parts sampled so far with their
+      // new topics, the rest with their old ones) into buffer 0, whose
+      // counts the apply between the parts sets
+      const int64_t i0 = seq ? 0 : c->part_item[(size_t)part];
+      const int64_t i1 = seq ? c->part_item[(size_t)c->parts] : c->part_item[(size_t)part + 1];
       HIP_TRY(lda::launch_recount(c->Kp, c->perm, c->sweep_zw ? c->zw : nullptr, c->items + 4 * i0,
-                                  (int32_t)(i1 - i0), c->z, c->delta_part[part],
-                                  c->delta_part[part] + (int64_t)c->V * c->Kp, c->recount_blocks,
-                                  c->stream));
+                                  (int32_t)(i1 - i0), c->z, buf, buf + (int64_t)c->V * c->Kp,
+                                  c->recount_blocks, c->stream));
     }
     HIP_TRY(hipEventRecord(c->ev2[slot], c->stream));
     c->recounted[slot] = c->sweep_recount;
     c->launches++;
+  } else if (c->sweep_recount && seq && c->N > 0) {
+    // a sequential part with no documents here: the shard's counts are still
+    // the ones the apply between the parts sets
+    HIP_TRY(lda::launch_recount(c->Kp, c->perm, c->sweep_zw ? c->zw : nullptr, c->items,
+                                (int32_t)c->part_item[(size_t)c->parts], c->z, buf, buf + (int64_t)c->V * c->Kp,
+                                c->recount_blocks, c->stream));
   }
   c->pending = true;  // the part buffers hold this sweep's changes
   c->pending_absolute = c->sweep_recount;
@@ -1251,11 +1263,26 @@ lda_status lda_exchange_unpack(lda_ctx* c, int32_t part, int32_t world, int64_t 
                                const void* escapes_all) {
   return lda_abi::guarded([&]() -> lda_status {
   if (!c || !escapes_all) return fail(LDA_ERR_INVALID_ARG, "null argument");
+  size_t np = 0, ne = 0;
+  int32_t cap = 0;
+  lda_status s = exchange_dims(c, world, max_shard_tokens, &np, &ne, &cap);
+  if (s) return s;
+  return lda_exchange_unpack_lists(c, part, world, max_shard_tokens, escapes_all, cap);
+  });
+}
+
+lda_status lda_exchange_unpack_lists(lda_ctx* c, int32_t part, int32_t world, int64_t max_shard_tokens,
+                                     const void* escapes_all, int32_t list_cap) {
+  return lda_abi::guarded([&]() -> lda_status {
+  if (!c) return fail(LDA_ERR_INVALID_ARG, "null ctx");
   if (part < 0 || part >= sweep_parts(c)) return fail(LDA_ERR_INVALID_ARG, "part out of range [0, parts)");
   size_t np = 0, ne = 0;
   int32_t cap = 0;
   lda_status s = exchange_dims(c, world, max_shard_tokens, &np, &ne, &cap);
   if (s) return s;
+  if (list_cap < 0 || list_cap > cap) return fail(LDA_ERR_INVALID_ARG, "list_cap out of range [0, escape capacity]");
+  if (!escapes_all && list_cap > 0) return fail(LDA_ERR_INVALID_ARG, "null escapes_all with list_cap > 0");
+  cap = list_cap;
   const int slot = exchange_slot(c, part);
   if (!c->exch_packed[slot]) return fail(LDA_ERR_STATE, "lda_exchange_unpack before lda_exchange_pack");
   HIP_TRY(hipSetDevice(c->device));
@@ -1263,7 +1290,31 @@ lda_status lda_exchange_unpack(lda_ctx* c, int32_t part, int32_t world, int64_t 
   int32_t* buf = c->delta_part[slot];
   const int32_t* pk = c->exch_packed[slot];
   HIP_TRY(hipMemcpyAsync(buf + cells, pk + cells / 2, sizeof(int32_t) * c->Kp, hipMemcpyDeviceToDevice, c->stream));
-  HIP_TRY(lda::launch_exch_unpack(pk, cells, buf, world, static_cast<const int32_t*>(escapes_all), cap, c->stream));
+  HIP_TRY(lda::launch_exch_unpack(pk, cells, buf, world,
+                                  list_cap > 0 ? static_cast<const int32_t*>(escapes_all) : nullptr, cap,
+                                  c->stream));
+  return LDA_OK;
+  });
+}
+
+lda_status lda_counts_checksum(lda_ctx* c, uint64_t* checksum) {
+  return lda_abi::guarded([&]() -> lda_status {
+  if (!c || !checksum) return fail(LDA_ERR_INVALID_ARG, "null argument");
+  if (c->pending) return fail(LDA_ERR_STATE, "checksum with a pending delta: call lda_apply first");
+  HIP_TRY(hipSetDevice(c->device));
+  const int64_t n4 = (int64_t)c->V * c->Kp / 4;
+  const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>((n4 + 255) / 256, 2048));
+  uint64_t* part = nullptr;
+  HIP_TRY(dalloc(&part, (size_t)blocks));
+  std::vector<uint64_t> h((size_t)blocks);
+  hipError_t e = lda::launch_counts_checksum(c->nw, c->nwsum, c->K, c->Kp, c->V, part, blocks, c->stream);
+  if (e == hipSuccess) e = hipMemcpyAsync(h.data(), part, sizeof(uint64_t) * blocks, hipMemcpyDeviceToHost, c->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+  (void)hipFree(part);
+  HIP_TRY(e);
+  uint64_t s = 0;
+  for (uint64_t x : h) s += x;
+  *checksum = s;
   return LDA_OK;
   });
 }

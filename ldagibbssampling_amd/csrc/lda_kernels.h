@@ -195,9 +195,13 @@ inline int32_t exch_bias1(int32_t world) { return 16384 / world; }
 // cells: a multiple of 4; packed: cells / 2 words; esc: [1 + 3 cap] with esc[0] zeroed
 hipError_t launch_exch_pack(const int32_t* buf, int64_t cells, int32_t* packed, int32_t world,
                             int32_t* esc, int32_t cap, hipStream_t st);
-// buf[cells] = the unpacked sum, then + every rank's escapes (esc_all: world x [1 + 3 cap])
+// buf[cells] = the unpacked sum, then + every rank's escapes (esc_all: world x
+// [1 + 3 cap]; nullptr: none)
 hipError_t launch_exch_unpack(const int32_t* packed, int64_t cells, int32_t* buf, int32_t world,
                               const int32_t* esc_all, int32_t cap, hipStream_t st);
+// one uint64 partial per block of the nw / nwsum hash (lda_counts_checksum)
+hipError_t launch_counts_checksum(const int32_t* nw, const int32_t* nwsum, int32_t K, int32_t Kp, int64_t V,
+                                  uint64_t* partial, int blocks, hipStream_t st);
 hipError_t launch_fold_delta(int32_t* dst, int32_t* src, int64_t n, hipStream_t st);
 hipError_t launch_prepare_topics(int32_t* nwsum, int32_t* dsum, const double* alpha, double beta,
                                  double vbeta, int32_t K, int32_t Kp, float* alpha_f, float* inv,

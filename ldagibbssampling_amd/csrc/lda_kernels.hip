@@ -2889,6 +2889,51 @@ __global__ __launch_bounds__(256) void k_exch_escapes(const int32_t* __restrict_
   }
 }
 
+// lda_counts_checksum: sum (mod 2^64) over the nonzero cells of nw and nwsum
+// of mix64(index << 32 | value), index = w K + k for nw[w][k], V K + k for
+// nwsum[k] (the Kp padding is skipped, so the hash is that of the V x K
+// arrays lda_get_counts returns; oracle.counts_checksum).  One partial per
+// block, summed on the host: a sum is order-free, so every replica of the
+// same counts gives the same value whatever the launch geometry.
+__device__ __forceinline__ uint64_t mix64(uint64_t x) {
+  x ^= x >> 30;
+  x *= 0xBF58476D1CE4E5B9ull;
+  x ^= x >> 27;
+  x *= 0x94D049BB133111EBull;
+  return x ^ (x >> 31);
+}
+
+__device__ __forceinline__ uint64_t cell_hash(int64_t index, int32_t v) {
+  return v ? mix64(((uint64_t)index << 32) | (uint32_t)v) : 0ull;
+}
+
+__global__ __launch_bounds__(256) void k_counts_checksum(const int4* __restrict__ nw, int64_t n4,
+                                                         const int32_t* __restrict__ nwsum, int32_t K, int32_t Kp,
+                                                         int64_t V, uint64_t* __restrict__ partial) {
+  __shared__ uint64_t red[256];
+  uint64_t s = 0;
+  const int64_t q = Kp / 4;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += (int64_t)gridDim.x * 256) {
+    const int4 d = nw[i];
+    const int64_t w = i / q;
+    const int32_t k = (int32_t)(i - w * q) * 4;
+    const int64_t base = w * K + k;
+    if (k + 0 < K) s += cell_hash(base + 0, d.x);
+    if (k + 1 < K) s += cell_hash(base + 1, d.y);
+    if (k + 2 < K) s += cell_hash(base + 2, d.z);
+    if (k + 3 < K) s += cell_hash(base + 3, d.w);
+  }
+  if (blockIdx.x == 0)
+    for (int k = threadIdx.x; k < K; k += 256) s += cell_hash(V * K + k, nwsum[k]);
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int h = 128; h > 0; h >>= 1) {
+    if (threadIdx.x < h) red[threadIdx.x] += red[threadIdx.x + h];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) partial[blockIdx.x] = red[0];
+}
+
 // Split sweep (lda_set_exchange_parts): dst += src; src = 0 over the whole
 // [V*Kp | Kp] delta region (a multiple of 4 int32: Kp is a multiple of 64).
 // int4 groups that are zero in src are neither written nor re-zeroed.
@@ -3728,7 +3773,15 @@ hipError_t launch_exch_unpack(const int32_t* packed, int64_t cells, int32_t* buf
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
   }
+  if (!esc_all) return hipSuccess;      // no rank had an escape (lda_exchange_unpack_lists, list_cap 0)
   hipLaunchKernelGGL(k_exch_escapes, dim3(4 * world), dim3(256), 0, st, esc_all, cap, buf);
+  return hipGetLastError();
+}
+
+hipError_t launch_counts_checksum(const int32_t* nw, const int32_t* nwsum, int32_t K, int32_t Kp, int64_t V,
+                                  uint64_t* partial, int blocks, hipStream_t st) {
+  hipLaunchKernelGGL(k_counts_checksum, dim3(blocks), dim3(256), 0, st, reinterpret_cast<const int4*>(nw),
+                     V * Kp / 4, nwsum, K, Kp, V, partial);
   return hipGetLastError();
 }
 

@@ -19,6 +19,19 @@ escape lists for the cells whose change is out of that range; the unpack
 gives the int32 sum bit for bit at half the bytes (C4: 102 MB instead of
 205 MB per sweep, C5: 2.15 GB instead of 4.3 GB).
 
+Escape lists at their used length (escape_lists="used", the default): each
+rank's escape count is MAX-all-reduced first (4 bytes), every rank then
+all-gathers only that many triples (none when no rank has one), and
+lda_exchange_unpack_lists unpacks them; a count above the list capacity
+(impossible while every shard holds at most max_tokens tokens) raises.
+escape_lists="capacity" all-gathers the whole fixed-capacity lists (C4 at
+N = 8: 2.9 MB per rank) without the count read.
+
+Replica check (replica_check, bench.py's multi-GPU line): after the timed
+region the ranks MIN- and MAX-all-reduce a hash of their nw / nwsum
+(lda_counts_checksum) and the bits of the LL's word part; the replicas agree
+when MIN == MAX.
+
 Split sweeps (engine.exchange_parts > 1, lda_set_exchange_parts): the shard's
 documents are sampled in P parts with one delta buffer each; part i's
 all-reduce is issued asynchronously as soon as part i has been sampled, so it
@@ -28,6 +41,7 @@ for bit, as the unsplit one (tests/test_distributed.py::*split*).
 """
 from __future__ import annotations
 
+import struct
 from dataclasses import dataclass
 
 import numpy as np
@@ -70,7 +84,8 @@ class ADLDATrainer:
     """
 
     def __init__(self, engine, group=None, sync_before_reduce: bool = True,
-                 time_reduce: bool = False, compact: bool = True, exchange=None):
+                 time_reduce: bool = False, compact: bool = True, exchange=None,
+                 escape_lists: str = "used"):
         """sync_before_reduce=False when the engine already launches on the
         stream the collective runs behind (GibbsSampler.set_stream(torch's
         current stream)): then no host synchronisation per sweep is needed.
@@ -80,8 +95,17 @@ class ADLDATrainer:
         True on one rank puts the real backend's calls -- RCCL's in-place
         all-reduce on the library's buffers, the all-gather, the pack and
         unpack -- on the path of a one-GPU run, whose sums are then the
-        identity (tests/test_distributed_gpu.py)."""
+        identity (tests/test_distributed_gpu.py).
+        escape_lists: "used" (all-gather the escape lists at their used
+        length, after a MAX all-reduce of the counts) or "capacity" (the
+        whole fixed-capacity lists)."""
         import torch.distributed as dist
+
+        if escape_lists not in ("used", "capacity"):
+            raise ValueError('escape_lists must be "used" or "capacity"')
+        self.escape_lists = escape_lists
+        self._sent = []            # list_cap all-gathered per exchanged buffer ("used")
+        self._counts = None        # per-part escape counts, MAX-all-reduced ("used")
 
         self.engine = engine
         self.time_reduce = time_reduce
@@ -135,21 +159,58 @@ class ADLDATrainer:
         if not self.compact:
             return {"allreduce_bytes": 4 * cells, "allgather_bytes": 0}
         n_pk, n_es = self.engine.exchange_sizes(self.world, self.max_tokens)
-        return {"allreduce_bytes": 4 * n_pk, "allgather_bytes": 4 * n_es * self.world}
+        cap_bytes = 4 * n_es * self.world
+        if self.escape_lists == "capacity":
+            return {"allreduce_bytes": 4 * n_pk, "allgather_bytes": cap_bytes,
+                    "allgather_capacity_bytes": cap_bytes, "escape_lists": "capacity"}
+        # what the last exchanges (up to 256) gathered: 1 + 3 m int32 per rank
+        # when m > 0 (m = the largest count of any rank), nothing when m = 0
+        sent = self._sent or [0]
+        gathered = [4 * self.world * (1 + 3 * m) if m > 0 else 0 for m in sent]
+        return {"allreduce_bytes": 4 * n_pk + 4, "allgather_bytes": float(np.mean(gathered)),
+                "allgather_capacity_bytes": cap_bytes, "escape_lists": "used",
+                "escape_count_max": int(max(sent)), "exchanges_recorded": len(self._sent)}
 
-    def _escapes_all(self, part: int, esc):
-        """The all-gather target of part `part`: world x len(esc) int32."""
+    def _escapes_all(self, part: int, esc, n: int | None = None):
+        """The all-gather target of part `part`: world x n int32 (n: the
+        per-rank length sent, default len(esc)), a prefix of one buffer of
+        the full capacity."""
         import torch
+        n = esc.numel() if n is None else n
         buf = self._esc_all.get(part)
-        if buf is None or buf.numel() != self.world * esc.numel() or buf.device != esc.device:
+        if buf is None or buf.numel() < self.world * esc.numel() or buf.device != esc.device:
             buf = torch.empty(self.world * esc.numel(), dtype=esc.dtype, device=esc.device)
             self._esc_all[part] = buf
-        return buf
+        return buf[:self.world * n]
+
+    def _gather(self, part: int, esc, n: int, async_op: bool):
+        """All-gather the first n int32 of every rank's escape list."""
+        dist = self.dist
+        send = esc[:n]
+        esc_all = self._escapes_all(part, esc, n)
+        if esc.device.type == "cuda" and dist.get_backend(self.group) == "nccl":
+            w = dist.all_gather_into_tensor(esc_all, send, group=self.group, async_op=async_op)
+        else:
+            # gloo: a list of views of the one target array
+            chunks = list(esc_all.view(self.world, -1).unbind(0))
+            w = dist.all_gather(chunks, send, group=self.group, async_op=async_op)
+        return esc_all, w
+
+    def _count_slots(self, esc):
+        import torch
+        n = max(self.parts, 1)
+        if self._counts is None or self._counts.numel() < n or self._counts.device != esc.device:
+            self._counts = torch.zeros(n, dtype=torch.int32, device=esc.device)
+        return self._counts
 
     def _exchange_start(self, part: int, async_op: bool):
-        """Issue part `part`'s sum across the ranks; returns (works, finish):
-        wait on the works (and, with sync_before_reduce, synchronize torch's
-        current stream), then finish() leaves the sum in the part's buffer.
+        """Issue part `part`'s sum across the ranks; returns (works, pending):
+        escape_lists "used": wait on pending.count_work (async), read the
+        MAX-all-reduced escape counts on the host (_read_counts), and
+        pending.gather(count) issues the lists' all-gather (more works).
+        Then wait on the works and (with
+        sync_before_reduce, after synchronizing torch's current stream)
+        pending.finish() leaves the sum in the part's buffer.
         Compact: the pack is enqueued on the engine's stream, the collectives
         on torch's current one (the same stream when sync_before_reduce is
         off), and finish() enqueues the unpack on the engine's stream."""
@@ -159,22 +220,41 @@ class ADLDATrainer:
                 self.engine.synchronize()
             w = dist.all_reduce(self._part_delta(part), op=dist.ReduceOp.SUM, group=self.group,
                                 async_op=async_op)
-            return ([w] if async_op else []), (lambda: None)
+            return ([w] if async_op else []), _Pending()
         packed, esc = self.engine.exchange_pack(part, self.world, self.max_tokens)
-        esc_all = self._escapes_all(part, esc)
         if self.sync_before_reduce:
             self.engine.synchronize()
+        count_work = None
+        if self.escape_lists == "used":
+            # the count first: its all-reduce is done before the packed words'
+            cnt = self._count_slots(esc)[part:part + 1]
+            cnt.copy_(esc[:1])
+            count_work = dist.all_reduce(cnt, op=dist.ReduceOp.MAX, group=self.group, async_op=async_op)
         works = [dist.all_reduce(packed, op=dist.ReduceOp.SUM, group=self.group, async_op=async_op)]
-        if esc.device.type == "cuda" and dist.get_backend(self.group) == "nccl":
-            works.append(dist.all_gather_into_tensor(esc_all, esc, group=self.group, async_op=async_op))
+        if self.escape_lists == "capacity":
+            esc_all, w = self._gather(part, esc, esc.numel(), async_op)
+            works.append(w)
+            pend = _Pending(finish=lambda: self.engine.exchange_unpack(part, self.world, self.max_tokens,
+                                                                       esc_all))
         else:
-            # gloo: a list of views of the one target array
-            chunks = list(esc_all.view(self.world, -1).unbind(0))
-            works.append(dist.all_gather(chunks, esc, group=self.group, async_op=async_op))
+            pend = _Pending(self, part, esc)
+            pend.count_work = count_work
+        return ([w for w in works if w is not None] if async_op else []), pend
 
-        def finish():
-            self.engine.exchange_unpack(part, self.world, self.max_tokens, esc_all)
-        return ([w for w in works if w is not None] if async_op else []), finish
+    def _read_counts(self, parts: int):
+        """The MAX-all-reduced escape counts of the first `parts` parts (one
+        host read; the caller has waited on the count all-reduces)."""
+        if self.escape_lists != "used" or not self.compact:
+            return [0] * parts
+        cnt = [int(x) for x in self._counts[:parts].cpu().tolist()]
+        _, n_es = self.engine.exchange_sizes(self.world, self.max_tokens)
+        cap = (n_es - 1) // 3
+        for m in cnt:
+            if m > cap:
+                raise RuntimeError(f"escape list overflow: {m} escapes, capacity {cap} "
+                                   f"(a shard holds more than max_tokens = {self.max_tokens} tokens?)")
+        self._sent = (self._sent + cnt)[-256:]
+        return cnt
 
     def _landed(self):
         """With sync_before_reduce the engine's stream is not ordered behind
@@ -192,9 +272,11 @@ class ADLDATrainer:
                 import torch
                 ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
                 ev[0].record()
-            _, finish = self._exchange_start(0, async_op=False)
+            _, pend = self._exchange_start(0, async_op=False)
+            for w in pend.gather(self._read_counts(1)[0], async_op=False):
+                w.wait()
             self._landed()
-            finish()
+            pend.finish()
             if ev is not None:
                 ev[1].record()
                 self._events = (self._events + [ev])[-256:]
@@ -254,14 +336,23 @@ class ADLDATrainer:
                 import torch
                 ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
                 ev[0].record()
-            w, fin = self._exchange_start(i, async_op=True)
+            w, pend = self._exchange_start(i, async_op=True)
             works += w
-            finishers.append(fin)
+            finishers.append(pend)
+        if self.compact and self.escape_lists == "used":
+            # every part's escape lists at their used length: one host read of
+            # the parts' MAX-reduced counts (the count all-reduces were issued
+            # ahead of each part's packed all-reduce)
+            for pend in finishers:
+                if pend.count_work is not None:
+                    pend.count_work.wait()
+            for pend, m in zip(finishers, self._read_counts(parts)):
+                works += pend.gather(m, async_op=True)
         for w in works:
             w.wait()           # the current stream waits for every part's sum
         self._landed()
-        for fin in finishers:
-            fin()
+        for pend in finishers:
+            pend.finish()
         if ev is not None:
             ev[1].record()      # exposed exchange: the last part's collective (+ unpacks)
             self._events = (self._events + [ev])[-256:]
@@ -306,6 +397,48 @@ class ADLDATrainer:
                 self._reduce()
             self.engine.apply()
 
+    def replica_check(self, seconds: float | None = None) -> dict:
+        """After the timed region: every rank's replica of nw / nwsum and the
+        LL's word part (computed from them) must be identical.  MIN and MAX
+        all-reduces of (counts hash, word-part bits, total-LL bits); a SUM of
+        ones counts the ranks the collective reached; `seconds` (this rank's
+        timed-region time) is all-gathered into rank_seconds."""
+        import torch
+
+        h = int(self.engine.counts_checksum()) if hasattr(self.engine, "counts_checksum") else 0
+        doc, word = self.engine.log_likelihood_parts()
+        total = self.log_likelihood()
+
+        def bits(x):
+            return struct.unpack("<q", struct.pack("<d", float(x)))[0]
+
+        signed = h - (1 << 64) if h >= 1 << 63 else h
+        vals = [signed, bits(word), bits(total)]
+        out = {"world_size": self.world, "counts_checksum": f"{h:016x}", "ll_word_part": word,
+               "ll": total}
+        if not self.exchange:
+            out.update(replicas_agree=True, ranks_counted=1,
+                       rank_seconds=[seconds] if seconds is not None else None)
+            return out
+        dist = self.dist
+        dev = self._collective_device()
+        lo = torch.tensor(vals, dtype=torch.int64, device=dev)
+        hi = lo.clone()
+        dist.all_reduce(lo, op=dist.ReduceOp.MIN, group=self.group)
+        dist.all_reduce(hi, op=dist.ReduceOp.MAX, group=self.group)
+        one = torch.ones(1, dtype=torch.int64, device=dev)
+        dist.all_reduce(one, op=dist.ReduceOp.SUM, group=self.group)
+        lo, hi = lo.cpu().tolist(), hi.cpu().tolist()
+        out.update(replicas_agree=bool(lo == hi), ranks_counted=int(one.item()),
+                   checksum_min=f"{lo[0] & ((1 << 64) - 1):016x}",
+                   checksum_max=f"{hi[0] & ((1 << 64) - 1):016x}")
+        if seconds is not None:
+            t = torch.tensor([float(seconds)], dtype=torch.float64, device=dev)
+            ts = [torch.zeros_like(t) for _ in range(self.world)]
+            dist.all_gather(ts, t, group=self.group)
+            out["rank_seconds"] = [float(x.item()) for x in ts]
+        return out
+
     def log_likelihood(self) -> float:
         """modelLogLikelihood of the whole corpus: doc parts summed over ranks,
         the word part (global counts) taken once."""
@@ -318,3 +451,32 @@ class ADLDATrainer:
             self.dist.all_reduce(t, op=self.dist.ReduceOp.SUM, group=self.group)
             doc = float(t.item())
         return doc + word
+
+
+class _Pending:
+    """One exchanged buffer between its collectives and its unpack (see
+    ADLDATrainer._exchange_start)."""
+
+    def __init__(self, trainer=None, part=0, esc=None, finish=None):
+        self.trainer, self.part, self.esc = trainer, part, esc
+        self._finish = finish
+        self._esc_all, self._m = None, 0
+        self.count_work = None
+
+    def gather(self, m: int, async_op: bool = False):
+        """escape_lists "used": all-gather 1 + 3 m int32 of every rank's list
+        (nothing when m = 0); returns the works to wait on."""
+        if self.trainer is None or self._finish is not None:
+            return []
+        self._m = int(m)
+        if self._m == 0:
+            return []
+        self._esc_all, w = self.trainer._gather(self.part, self.esc, 1 + 3 * self._m, async_op)
+        return [w] if (async_op and w is not None) else []
+
+    def finish(self):
+        if self._finish is not None:
+            self._finish()
+        elif self.trainer is not None:
+            t = self.trainer
+            t.engine.exchange_unpack(self.part, t.world, t.max_tokens, self._esc_all, list_cap=self._m)

@@ -140,13 +140,24 @@ class GibbsSampler:
         return (torch.as_tensor(_DeviceArray(int(pk.value), n_pk), device=dev),
                 torch.as_tensor(_DeviceArray(int(es.value), n_es), device=dev))
 
-    def exchange_unpack(self, part: int, world: int, max_tokens: int, escapes_all):
+    def exchange_unpack(self, part: int, world: int, max_tokens: int, escapes_all, list_cap=None):
         """lda_exchange_unpack: the part's buffer = the summed packed words +
-        every rank's escapes (escapes_all: device int32 [world x escape len])."""
-        assert escapes_all.dtype.itemsize == 4 and escapes_all.is_contiguous()
-        capi.check(self._L.lda_exchange_unpack(self._h, int(part), int(world), int(max_tokens),
-                                               C.c_void_p(escapes_all.data_ptr())),
-                   "lda_exchange_unpack")
+        every rank's escapes (escapes_all: device int32 [world x escape len]).
+        list_cap: the lists were all-gathered at 1 + 3 list_cap int32 each
+        (lda_exchange_unpack_lists; 0 with escapes_all None: no rank had one)."""
+        if list_cap is None:
+            assert escapes_all.dtype.itemsize == 4 and escapes_all.is_contiguous()
+            capi.check(self._L.lda_exchange_unpack(self._h, int(part), int(world), int(max_tokens),
+                                                   C.c_void_p(escapes_all.data_ptr())),
+                       "lda_exchange_unpack")
+            return
+        ptr = None
+        if escapes_all is not None:
+            assert escapes_all.dtype.itemsize == 4 and escapes_all.is_contiguous()
+            assert escapes_all.numel() == world * (1 + 3 * int(list_cap))
+            ptr = C.c_void_p(escapes_all.data_ptr())
+        capi.check(self._L.lda_exchange_unpack_lists(self._h, int(part), int(world), int(max_tokens), ptr,
+                                                     int(list_cap)), "lda_exchange_unpack_lists")
 
     # ------------------------------------------------- split sweep (§5)
     def set_exchange_parts(self, parts: int, reserve_cus: int = 0):
@@ -286,6 +297,13 @@ class GibbsSampler:
                                           nd.ctypes.data if with_nd else None,
                                           ndsum.ctypes.data), "lda_get_counts")
         return nw, nwsum, nd, ndsum
+
+    def counts_checksum(self) -> int:
+        """lda_counts_checksum: a hash of the applied nw / nwsum (equal on every
+        replica; oracle.counts_checksum of counts()'s nw, nwsum)."""
+        h = C.c_uint64()
+        capi.check(self._L.lda_counts_checksum(self._h, C.byref(h)), "lda_counts_checksum")
+        return int(h.value)
 
     def set_alpha_beta(self, alpha, beta: float):
         a = np.ascontiguousarray(np.broadcast_to(np.asarray(alpha, dtype=np.float64), (self.K,)))

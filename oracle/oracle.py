@@ -520,12 +520,20 @@ def exchange_pack(buf, world: int, Kp: int, max_tokens: int):
     return packed.astype(np.int32), esc.astype(np.int32)
 
 
-def exchange_unpack(packed_sum, escapes_all, world: int, Kp: int, max_tokens: int):
+def exchange_unpack(packed_sum, escapes_all, world: int, Kp: int, max_tokens: int, list_cap=None):
     """lda_exchange_unpack: the summed packed words (int32 [cells/2 | Kp]) and
     every rank's escape list (world x [1 + 3 cap], rank order) -> the int32
-    sum of the ranks' buffers [cells | Kp]."""
+    sum of the ranks' buffers [cells | Kp].  list_cap: the lists were sent at
+    1 + 3 list_cap int32 each (lda_exchange_unpack_lists; 0 and escapes_all
+    None: no rank had an escape)."""
     b0, b1 = exchange_biases(world)
     cap = exchange_cap(world, max_tokens)
+    if list_cap is not None:
+        assert 0 <= list_cap <= cap
+        cap = int(list_cap)
+        if escapes_all is None:
+            assert cap == 0
+            escapes_all = np.zeros(world, dtype=np.int32)
     p = np.asarray(packed_sum, dtype=np.int64) & 0xFFFFFFFF
     half = p.size - Kp
     out = np.empty(2 * half + Kp, dtype=np.int64)
@@ -539,3 +547,25 @@ def exchange_unpack(packed_sum, escapes_all, world: int, Kp: int, max_tokens: in
         cell = (e[:, 0] & 0xFFFFFFFF) | (e[:, 1] << 32)
         np.add.at(out, cell, e[:, 2])
     return out.astype(np.int32)
+
+
+def _mix64(x):
+    """splitmix64's finaliser on uint64 arrays (k_counts_checksum's mix64)."""
+    x = x ^ (x >> np.uint64(30))
+    x = x * np.uint64(0xBF58476D1CE4E5B9)
+    x = x ^ (x >> np.uint64(27))
+    x = x * np.uint64(0x94D049BB133111EB)
+    return x ^ (x >> np.uint64(31))
+
+
+def counts_checksum(nw, nwsum) -> int:
+    """lda_counts_checksum restated: sum mod 2^64 over the nonzero cells of nw
+    (V x K) and nwsum (K) of mix64(index << 32 | (uint32) value), index = w K +
+    k in nw and V K + k in nwsum."""
+    nw = np.asarray(nw, dtype=np.int64)
+    V, K = nw.shape
+    vals = np.concatenate([nw.reshape(-1), np.asarray(nwsum, dtype=np.int64).reshape(-1)[:K]])
+    idx = np.flatnonzero(vals)
+    x = (idx.astype(np.uint64) << np.uint64(32)) | (vals[idx] & 0xFFFFFFFF).astype(np.uint64)
+    with np.errstate(over="ignore"):
+        return int(_mix64(x).sum(dtype=np.uint64))

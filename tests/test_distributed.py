@@ -56,10 +56,17 @@ class OracleEngine:
         self._packed[part] = torch.from_numpy(pk)
         return self._packed[part], torch.from_numpy(es)
 
-    def exchange_unpack(self, part, world, max_tokens, escapes_all):
+    def exchange_unpack(self, part, world, max_tokens, escapes_all, list_cap=None):
         from oracle import oracle as O
-        self._buf(part)[:] = O.exchange_unpack(self._packed[part].numpy(), escapes_all.numpy(), world,
-                                               self.s.Kp, max_tokens)
+        self.unpacked_lists = getattr(self, "unpacked_lists", []) + [list_cap]
+        self._buf(part)[:] = O.exchange_unpack(self._packed[part].numpy(),
+                                               None if escapes_all is None else escapes_all.numpy(), world,
+                                               self.s.Kp, max_tokens, list_cap=list_cap)
+
+    def counts_checksum(self):
+        from oracle import oracle as O
+        nw, nwsum, _, _ = self.s.counts()
+        return O.counts_checksum(nw, nwsum)
 
 
 class SplitOracleEngine(OracleEngine):
@@ -133,30 +140,57 @@ def _corpus():
 WARM = (3, 2)          # sweeps 0 and 1 in 3 sequential parts
 
 
-def _worker(rank, world, port, outdir, parts=1, compact=True):
+def _hot_corpus():
+    """Half the tokens are one word whose tokens start in topics 0 and 1: the
+    first exchange (the initial counts) has cells beyond both biases, so
+    escape lists travel (test_gloo_escape_lists)."""
+    rng = np.random.default_rng(5)
+    D, L = 480, 150
+    words = rng.integers(1, 200, size=D * L).astype(np.int32)
+    hot = rng.random(D * L) < 0.5
+    words[hot] = 0
+    z0 = rng.integers(0, K, size=D * L).astype(np.int32)
+    z0[hot] = rng.integers(0, 2, size=int(hot.sum()))
+    return np.arange(D + 1, dtype=np.int64) * L, words, z0, 200
+
+
+def _worker(rank, world, port, outdir, parts=1, compact=True, escape_lists="used", corpus="plain"):
     sys.path.insert(0, ROOT)
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     from oracle import oracle as O
     from ldagibbssampling_amd.distributed import ADLDATrainer, shard_corpus
-    c = _corpus()
-    sh = shard_corpus(c.doc_off, c.words, world, rank)
-    o = O.ExactSampler(K, c.num_types, sh.doc_off, sh.words, 0.1, 0.01, SEED, token_base=sh.token_base)
-    if parts in ("warm", "steady"):
-        o.set_warm_start(*WARM, 0, c.num_tokens)        # parts cut in the whole corpus
-        if parts == "steady":                           # + Mallet-staleness sweeps after it
-            o.set_sequential_sweeps(*O.staleness_schedule(4), 0, c.num_tokens)
-        tr = ADLDATrainer(WarmOracleEngine(o), compact=compact)
+    if corpus == "hot":
+        doc_off, words, z0, V = _hot_corpus()
     else:
-        tr = ADLDATrainer(OracleEngine(o) if parts == 1 else SplitOracleEngine(o, parts),
-                          compact=compact)
+        c = _corpus()
+        doc_off, words, z0, V = c.doc_off, c.words, None, c.num_types
+    sh = shard_corpus(doc_off, words, world, rank)
+    o = O.ExactSampler(K, V, sh.doc_off, sh.words, 0.1, 0.01, SEED, token_base=sh.token_base,
+                       z_init=None if z0 is None else z0[sh.token_base:sh.token_base + len(sh.words)])
+    if parts in ("warm", "steady"):
+        o.set_warm_start(*WARM, 0, len(words))          # parts cut in the whole corpus
+        if parts == "steady":                           # + Mallet-staleness sweeps after it
+            o.set_sequential_sweeps(*O.staleness_schedule(4), 0, len(words))
+        eng = WarmOracleEngine(o)
+    else:
+        eng = OracleEngine(o) if parts == 1 else SplitOracleEngine(o, parts)
+    if corpus == "corrupt" and rank == world - 1:
+        eng.counts_checksum = lambda: 12345             # a replica that differs
+    tr = ADLDATrainer(eng, compact=compact, escape_lists=escape_lists)
+    if parts not in ("warm", "steady"):
         assert tr.parts == parts
     assert tr.compact == compact
     tr.sweep(SWEEPS)
     ll = tr.log_likelihood()
+    chk = tr.replica_check(seconds=0.5 + rank)
     nw, nwsum, _, _ = o.counts()
     np.savez(os.path.join(outdir, f"r{rank}.npz"), z=o.z(), nw=nw, nwsum=nwsum, ll=ll,
-             docs=np.array([sh.doc_begin, sh.doc_end]))
+             docs=np.array([sh.doc_begin, sh.doc_end]), agree=chk["replicas_agree"],
+             ranks=chk["ranks_counted"], world=chk["world_size"], secs=np.array(chk["rank_seconds"]),
+             checksum=chk["counts_checksum"], lists=np.array([-1 if x is None else x for x in
+                                                               getattr(eng, "unpacked_lists", [])]),
+             xb=str(tr.exchange_bytes()))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -181,10 +215,7 @@ def test_gloo_adlda_matches_single(oracle, world, parts, compact):
     part summed and applied before the next) against one context's.
     compact: the packed exchange (two cells per int32 word + escape lists);
     False: the int32 buffers."""
-    with tempfile.TemporaryDirectory() as d:
-        mp.start_processes(_worker, args=(world, _free_port(), d, parts, compact), nprocs=world,
-                           start_method="spawn")
-        res = [np.load(os.path.join(d, f"r{r}.npz")) for r in range(world)]
+    res = _run(world, parts, compact)
     c = _corpus()
     single = oracle.ExactSampler(K, c.num_types, c.doc_off, c.words, 0.1, 0.01, SEED)
     if parts in ("warm", "steady"):
@@ -201,6 +232,69 @@ def test_gloo_adlda_matches_single(oracle, world, parts, compact):
     spans = [tuple(r["docs"]) for r in res]
     assert spans[0][0] == 0 and spans[-1][1] == c.num_docs
     assert all(a[1] == b[0] for a, b in zip(spans, spans[1:]))
+    # the replica check bench.py prints: every rank agrees, on the hash of the
+    # counts the oracle restates, over all `world` ranks
+    for r in res:
+        assert bool(r["agree"]) and int(r["ranks"]) == world and int(r["world"]) == world
+        assert str(r["checksum"]) == f"{oracle.counts_checksum(nw, nwsum):016x}"
+        np.testing.assert_array_equal(r["secs"], 0.5 + np.arange(world))
+
+
+def _run(world, parts=1, compact=True, escape_lists="used", corpus="plain"):
+    with tempfile.TemporaryDirectory() as d:
+        mp.start_processes(_worker, args=(world, _free_port(), d, parts, compact, escape_lists, corpus),
+                           nprocs=world, start_method="spawn")
+        return [dict(np.load(os.path.join(d, f"r{r}.npz"))) for r in range(world)]
+
+
+@pytest.mark.parametrize("world,parts,escape_lists", [(2, 1, "used"), (3, 1, "used"), (3, 2, "used"),
+                                                      (2, 1, "capacity")])
+def test_gloo_escape_lists(oracle, world, parts, escape_lists):
+    """A corpus whose first exchange has escapes (cells beyond 2^14/world):
+    "used" all-gathers the lists at the MAX-reduced count (lda_exchange_
+    unpack_lists; list_cap 0 without escapes, when nothing is gathered),
+    "capacity" the whole lists; both give the single-process run."""
+    res = _run(world, parts, True, escape_lists, "hot")
+    doc_off, words, z0, V = _hot_corpus()
+    single = oracle.ExactSampler(K, V, doc_off, words, 0.1, 0.01, SEED, z_init=z0)
+    single.sweep(SWEEPS)
+    np.testing.assert_array_equal(np.concatenate([r["z"] for r in res]), single.z())
+    nw, nwsum, _, _ = single.counts()
+    for r in res:
+        np.testing.assert_array_equal(r["nw"], nw)
+        np.testing.assert_array_equal(r["nwsum"], nwsum)
+        assert bool(r["agree"])
+        lists = r["lists"]
+        if escape_lists == "used":
+            assert lists[0] >= 1                     # the initial counts' escapes, at their count
+            assert (lists[1:] == 0).all()            # later deltas: none, nothing gathered
+            assert "'escape_lists': 'used'" in str(r["xb"])
+        else:
+            assert (lists == -1).all()
+
+
+def test_replica_check_flags_a_differing_replica():
+    res = _run(2, corpus="corrupt")
+    assert not any(bool(r["agree"]) for r in res)
+
+
+def test_escape_count_above_capacity_raises():
+    """A count beyond the list capacity (the bound's premise broken) stops
+    the exchange instead of unpacking a truncated list."""
+    from ldagibbssampling_amd.distributed import ADLDATrainer
+
+    class Fake:
+        def exchange_sizes(self, world, max_tokens):
+            return 8, 1 + 3 * 4
+
+    tr = ADLDATrainer.__new__(ADLDATrainer)
+    tr.escape_lists, tr.compact, tr.world, tr.max_tokens, tr._sent = "used", True, 2, 100, []
+    tr.engine = Fake()
+    tr._counts = torch.tensor([5], dtype=torch.int32)
+    with pytest.raises(RuntimeError, match="escape list overflow"):
+        tr._read_counts(1)
+    tr._counts = torch.tensor([4], dtype=torch.int32)
+    assert tr._read_counts(1) == [4]
 
 
 def test_shard_balanced_by_tokens():

@@ -54,8 +54,11 @@ def _worker(rank, world, port, outdir, stream_ordered=False, parts=1):
         tr = ADLDATrainer(g)
     tr.sweep(SWEEPS)
     ll = tr.log_likelihood()
+    chk = tr.replica_check(seconds=1.0 + rank)
     nw, nwsum, _, _ = g.counts()
-    np.savez(os.path.join(outdir, f"r{rank}.npz"), z=g.z(), nw=nw, nwsum=nwsum, ll=ll)
+    np.savez(os.path.join(outdir, f"r{rank}.npz"), z=g.z(), nw=nw, nwsum=nwsum, ll=ll,
+             agree=chk["replicas_agree"], ranks=chk["ranks_counted"], checksum=chk["counts_checksum"],
+             secs=np.array(chk["rank_seconds"]))
     g.close()
     dist.barrier()
     dist.destroy_process_group()
@@ -82,6 +85,10 @@ def test_two_ranks_one_gpu(oracle, stream_ordered, parts):
         np.testing.assert_array_equal(r["nw"], nw)
         np.testing.assert_array_equal(r["nwsum"], nwsum)
         assert abs(float(r["ll"]) - o.log_likelihood()) < 1e-9 * abs(o.log_likelihood())
+        # the replica check of bench.py's multi-GPU line (lda_counts_checksum)
+        assert bool(r["agree"]) and int(r["ranks"]) == world
+        assert str(r["checksum"]) == f"{oracle.counts_checksum(nw, nwsum):016x}"
+        np.testing.assert_array_equal(r["secs"], [1.0, 2.0])
 
 
 class _SlowCollective:
@@ -191,6 +198,8 @@ def _rccl_worker(rank, port, outdir, stream_ordered, parts, compact):
     ll = tr.log_likelihood()
     torch.cuda.synchronize()
     assert tr.reduce_ms(SWEEPS) is not None          # the collectives ran
+    chk = tr.replica_check(seconds=0.25)
+    assert chk["replicas_agree"] and chk["ranks_counted"] == 1 and chk["rank_seconds"] == [0.25]
     nw, nwsum, _, _ = g.counts()
     np.savez(os.path.join(outdir, "r0.npz"), z=g.z(), nw=nw, nwsum=nwsum, ll=ll,
              bytes=tr.exchange_bytes()["allreduce_bytes"])
@@ -227,5 +236,6 @@ def test_rccl_exchange_one_rank(oracle, stream_ordered, parts, compact):
     np.testing.assert_array_equal(r["nwsum"], nwsum)
     assert abs(float(r["ll"]) - o.log_likelihood()) < 1e-9 * abs(o.log_likelihood())
     vk, kp = c.num_types * 128, 128
-    # compact: two nw cells per int32 word, the nwsum part as raw int32
-    assert int(r["bytes"]) == (4 * (vk // 2 + kp) if compact else 4 * (vk + kp))
+    # compact: two nw cells per int32 word, the nwsum part as raw int32, and
+    # the escape count's 4-byte MAX all-reduce
+    assert int(r["bytes"]) == (4 * (vk // 2 + kp) + 4 if compact else 4 * (vk + kp))

@@ -132,9 +132,16 @@ def test_compact_exchange_bit_exact(oracle, world, kind, K):
     total = torch.stack([pk.to(torch.int64) for pk, _ in packs]).sum(0)
     assert int(total.max()) < 2 ** 31
     esc_all = torch.cat([es for _, es in packs])
-    for g, (pk, _) in zip(gs, packs):
+    # odd shards unpack the lists sent at their used length (lda_exchange_
+    # unpack_lists, what ADLDATrainer's escape_lists="used" all-gathers)
+    m = max(n_esc)
+    esc_used = torch.cat([es[:1 + 3 * m] for _, es in packs])
+    for i, (g, (pk, _)) in enumerate(zip(gs, packs)):
         pk.copy_(total.to(torch.int32))
-        g.exchange_unpack(0, world, N, esc_all)
+        if i % 2:
+            g.exchange_unpack(0, world, N, esc_used, list_cap=m)
+        else:
+            g.exchange_unpack(0, world, N, esc_all)
     torch.cuda.synchronize()
     for g in gs:
         assert torch.equal(g.delta_tensor(), want)
@@ -148,5 +155,40 @@ def test_compact_exchange_bit_exact(oracle, world, kind, K):
         nw, ns, _, _ = g.counts()
         np.testing.assert_array_equal(nw, nw1)
         np.testing.assert_array_equal(ns, ns1)
+        # lda_counts_checksum: the same on every replica, = the oracle's hash
+        assert g.counts_checksum() == oracle.counts_checksum(nw1, ns1)
         g.close()
     one.close()
+
+
+def test_unpack_lists_without_escapes_and_argument_checks():
+    """list_cap 0 with no list (no rank had an escape): the packed sum alone;
+    list_cap beyond the capacity or a missing list with list_cap > 0 fail;
+    the checksum refuses a pending delta."""
+    import torch
+    from ldagibbssampling_amd import capi
+    from ldagibbssampling_amd.sampler import GibbsSampler
+    rng = np.random.default_rng(3)
+    D, L, K = 40, 30, 8
+    words = rng.integers(0, 50, size=D * L).astype(np.int32)
+    doc_off = np.arange(D + 1, dtype=np.int64) * L
+    g = GibbsSampler(K, 50, doc_off, words, np.full(K, 0.1), 0.01, seed=2)
+    before = g.delta_tensor().clone()
+    pk, es = g.exchange_pack(0, 1, g.N)
+    torch.cuda.synchronize()
+    assert int(es[0]) == 0
+    with pytest.raises(capi.LdaError):
+        g.counts_checksum()                          # pending delta
+    cap = (es.numel() - 1) // 3
+    with pytest.raises(capi.LdaError):
+        g.exchange_unpack(0, 1, g.N, es, list_cap=cap + 1)
+    with pytest.raises(capi.LdaError):
+        g.exchange_unpack(0, 1, g.N, None, list_cap=1)
+    g.exchange_unpack(0, 1, g.N, None, list_cap=0)
+    torch.cuda.synchronize()
+    assert torch.equal(g.delta_tensor(), before)
+    g.apply()
+    nw, ns, _, _ = g.counts()
+    from oracle import oracle as O
+    assert g.counts_checksum() == O.counts_checksum(nw, ns)
+    g.close()

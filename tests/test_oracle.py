@@ -141,3 +141,45 @@ def test_exact_and_mallet_ll_same_formula(oracle):
     o = oracle.ExactSampler(K, c.num_types, c.doc_off, c.words, 10.0 / K, 0.01, 1, z_init=m.z())
     o.apply()
     assert abs(o.log_likelihood() - m.log_likelihood()) < 1e-9 * abs(m.log_likelihood())
+
+
+def test_large_k_draw_samples_the_exact_conditional(oracle):
+    """exact_draw_big (the large-K kernel's draw, k_sample_big) is an exact
+    sampler of p_k ~ (nd_k + a_k)(nw_wk - [k=zo] + b) / (nwsum_k - [k=zo] + V b):
+    its own entry enters the word part uncorrected and is fixed by the accept
+    / re-draw step, and the doc part is summed in fixed point.  Chi-square of
+    its draws against the float64 conditional, including own entries that hold
+    most of the mass (c = 40, 200) and a word seen once (c = 1, O = 0, the
+    re-draw always taken)."""
+    K, V = 2048, 40
+    rng = np.random.default_rng(7)
+    o = oracle.ExactSampler(K, V, np.array([0, 4], np.int64), np.zeros(4, np.int32), 0.05, 0.01, 5,
+                            kind="sparse")
+    for c_own, nd_own, others in [(1, 0, 0), (40, 5, 3), (200, 20, 1), (2, 1, 0), (5, 0, 40)]:
+        nw = np.zeros((V, K), np.int32)
+        zo, w = 777, 3
+        nw[w, zo] = c_own
+        for t in rng.choice(K, others, replace=False):
+            nw[w, t] += rng.integers(1, 30)
+        nw[10:] = rng.integers(0, 2, size=(V - 10, K))
+        nwsum = nw.sum(0).astype(np.int32)
+        o.load_snapshot(nw, nwsum)
+        nd = np.zeros(o.Kp, np.int32)
+        nd[zo] = nd_own
+        for t in rng.choice(K, 5, replace=False):
+            nd[t] += rng.integers(1, 4)
+        nwr = nw[w].astype(np.float64)
+        ns = nwsum.astype(np.float64)
+        nwr[zo] -= 1
+        ns[zo] -= 1
+        p = (nd[:K] + 0.05) * (nwr + 0.01) / (ns + V * 0.01)
+        p /= p.sum()
+        n = 30000
+        x = rng.integers(0, 2**32, size=(n, 4), dtype=np.uint64).astype(np.uint32)
+        cnt = np.bincount([o.big_draw(w, nd, zo, x[j]) for j in range(n)], minlength=K)
+        m = p * n > 20
+        chi = ((cnt[m] - n * p[m]) ** 2 / (n * p[m])).sum()
+        dof = max(int(m.sum()) - 1, 1)
+        # the null's chi2/dof has sd sqrt(2/dof); 1 + 5 sd (or 6 for dof 1)
+        assert chi / dof < 1 + 5 * np.sqrt(2 / dof) + (6 if dof == 1 else 0), (c_own, chi, dof)
+        assert abs(cnt[zo] / n - p[zo]) < 5 * np.sqrt(p[zo] * (1 - p[zo]) / n) + 1e-4

@@ -283,14 +283,19 @@ def test_num_threads_at_reference_scale_uses_one_gpu():
     assert m.numShards() == 1
 
 
-@pytest.mark.parametrize("kind,K,threads", [("dense", 20, 4), ("dense", 100, 3), ("dense", 500, 4),
-                                            ("dense", 500, 1), ("sparse", 1500, 4)])
-def test_staleness_sweeps_bit_exact(oracle, kind, K, threads):
+@pytest.mark.parametrize("kind,K,threads,mode", [("dense", 20, 4, "auto"), ("dense", 100, 3, "auto"),
+                                                 ("dense", 500, 4, "auto"), ("dense", 500, 1, "auto"),
+                                                 ("sparse", 1500, 4, "auto"), ("dense", 20, 4, "recount"),
+                                                 ("dense", 100, 1, "recount"), ("dense", 128, 4, "recount")])
+def test_staleness_sweeps_bit_exact(oracle, kind, K, threads, mode):
     """lda_set_sequential_sweeps with lda_staleness_schedule(T):
     after a warm start, every sweep in the sequential parts that give Mallet's
     mean live fraction 1/(2T) -- unequal pieces of every block for T > 1 --
     bit-exact against cpu_exact's same schedule, through lda_sweep (which
-    runs them one part at a time) and lda_sample."""
+    runs them one part at a time) and lda_sample.  mode "recount": every
+    sweep, warm-start and staleness sweeps included, recounts the whole shard
+    after each of its parts (lda_set_count_update(LDA_COUNT_RECOUNT)) instead
+    of adding a delta."""
     from ldagibbssampling_amd.sampler import GibbsSampler
     c = synthetic_lda(num_docs=300, num_types=800, num_topics=min(K, 40), doc_len=None, mean_len=50,
                       min_len=0, max_len=180, seed=K + threads)
@@ -298,6 +303,8 @@ def test_staleness_sweeps_bit_exact(oracle, kind, K, threads):
     parts, fr = oracle.staleness_schedule(threads)
     g = GibbsSampler(K, c.num_types, c.doc_off, c.words, alpha, 0.02, seed=5, sampler=kind,
                      tokens_per_range=64)
+    if mode == "recount":
+        g.set_count_update("recount")
     g.set_warm_start(3, 4)
     g.set_sequential_sweeps(parts, fr)
     assert g.sequential_sweeps() == (parts, oracle.quantise_fractions(fr))
@@ -308,6 +315,8 @@ def test_staleness_sweeps_bit_exact(oracle, kind, K, threads):
     o.sweep(7)
     np.testing.assert_array_equal(g.z(), o.z())
     g.sample()
+    if mode == "recount":
+        assert g.recount()
     g.apply()
     o.sweep(1)
     np.testing.assert_array_equal(g.z(), o.z())
