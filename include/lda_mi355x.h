@@ -134,14 +134,22 @@ lda_status lda_count_update_mode(lda_ctx* ctx, int32_t* recount);
  *                     Infinity Cache (4 N <= 256 MiB), else 0 (measured
  *                     crossover: DESIGN.md §4).
  *                     recount_sweeps < 0 keeps the current value.
- *                     Warm-start sweeps (lda_set_warm_start) never recount
+ *                     Sequential sweeps -- warm-start sweeps
+ *                     (lda_set_warm_start) and the steady ones of
+ *                     lda_set_sequential_sweeps -- never recount under AUTO
  *                     but do count toward the window: with the native
  *                     ParallelTopicModel's default 4 x 50 warm start the
  *                     window has passed before the first plain sweep, which
  *                     is right, since after ~20 sweeps the delta is the
- *                     faster update.  AUTO recount therefore
- *                     acts when the warm start is off (lda_sweep, bench).
- *  LDA_COUNT_RECOUNT  every sweep;  LDA_COUNT_DELTA  none.
+ *                     faster update; and its default Mallet-
+ *                     staleness schedule makes every later sweep sequential
+ *                     as well.  AUTO recount therefore acts only on plain
+ *                     snapshot sweeps (lda_sweep without either schedule,
+ *                     bench.py).
+ *  LDA_COUNT_RECOUNT  every sweep, sequential ones included (after each part
+ *                     the whole shard is recounted into buffer 0, the parts
+ *                     sampled so far with their new topics);
+ *  LDA_COUNT_DELTA    none.
  * Shards exchanging buffers must agree on it sweep by sweep: a distributed
  * driver sets the same mode and count on every rank (ADLDATrainer: the
  * minimum over ranks).  Results are identical in every mode.  On recount
@@ -171,7 +179,11 @@ lda_status lda_apply(lda_ctx* ctx);
  * (integer sums; draws keyed by the global token index).  lda_sample runs
  * every part.  reserve_cus: CUs' worth of sampler blocks left free in a split
  * sweep for the collective's kernels (0 = none, < 0 = the default: 1/32 of
- * the device's CUs, 8 on MI355X). */
+ * the device's CUs, 8 on MI355X).  Sequential sweeps (warm start, steady
+ * schedule) ignore the split: their parts are the schedule's, each summed and
+ * applied before the next part samples (an exchange per part, nothing to
+ * overlap), so under the native ParallelTopicModel's default staleness
+ * schedule a multi-GPU sweep exchanges 2-4 times. */
 #define LDA_MAX_EXCHANGE_PARTS 4
 lda_status lda_set_exchange_parts(lda_ctx* ctx, int32_t parts, int32_t reserve_cus);
 lda_status lda_get_exchange_parts(lda_ctx* ctx, int32_t* parts);

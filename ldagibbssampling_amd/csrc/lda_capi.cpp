@@ -136,8 +136,9 @@ std::vector<int64_t> make_cut_ranges(const std::vector<int64_t>& off, int64_t ta
 // token-balanced sharding into up to LDA_WARM_BLOCKS shards therefore holds
 // documents of every part (round 3 had cut P contiguous parts, so at G = 8,
 // P = 4 only 2 of 8 GPUs sampled in each step).  runs[i] = part i's local
-// document runs [d0, d1), in order.  Integer arithmetic: the oracle cuts the
-// same documents (gn < 2^40 keeps gn B Q < 2^63).
+// document runs [d0, d1), in order.  Integer arithmetic, the product gn (b Q
+// + cum) in 128 bits (B Q = 2^25.5: int64 would overflow past gn ~ 2^37): the
+// oracle (Python integers) cuts the same documents at any corpus size.
 std::vector<std::vector<std::pair<int64_t, int64_t>>> seq_part_runs(const std::vector<int64_t>& off,
                                                                     const std::vector<int64_t>& cum,
                                                                     int64_t base, int64_t g0, int64_t gn) {
@@ -150,7 +151,7 @@ std::vector<std::vector<std::pair<int64_t, int64_t>>> seq_part_runs(const std::v
     for (int i = 0; i < parts; ++i) {
       int64_t next = D;
       if (b + 1 < B || i + 1 < parts) {
-        const int64_t tgt = g0 + gn * (b * Q + cum[(size_t)i + 1]) / (B * Q) - base;
+        const int64_t tgt = g0 + (int64_t)((__int128)gn * (b * Q + cum[(size_t)i + 1]) / (B * Q)) - base;
         next = std::lower_bound(off.begin(), off.end(), tgt) - off.begin();
         next = std::min(std::max(next, prev), D);
       }
@@ -266,6 +267,10 @@ struct lda_ctx {
   int big_probe_slot = -1;           // the sweep being sampled is probe launch i (else -1)
   int64_t big_hold = 0;              // sweeps left before the next probe
   hipEvent_t big_ev[3][2] = {};
+  // what probe i timed: the first non-empty launch of its sweep, tagged
+  // (sweep kind, part, ranges); -1 = nothing launched (an empty shard or
+  // part).  Probes are compared only when all three timed the same tag.
+  int64_t big_ev_tag[3] = {-1, -1, -1};
   bool rows_ready = false;
   bool fused_apply = true;   // k_apply_build (LDA_FUSED_APPLY=0: k_apply_cols + k_build_sparse, A/B)
   int half = 0;    // dense K <= 128: 1 = the half-wave variant, 2 = the quarter-wave one (LDA_DENSE_HALF)
@@ -996,13 +1001,22 @@ static lda_status big_rb_next(lda_ctx* c) {
       for (auto& e : c->big_ev)
         for (hipEvent_t& x : e) HIP_TRY(hipEventCreate(&x));
     c->big_rb = c->big_probe == 1 ? lda::SB_RB_SHORT_ROUNDS : 0;
+    c->big_ev_tag[c->big_probe] = -1;
     c->big_probe_slot = c->big_probe++;
     return LDA_OK;
   }
-  HIP_TRY(hipEventSynchronize(c->big_ev[2][1]));
-  float ms[3];
-  for (int i = 0; i < 3; ++i) HIP_TRY(hipEventElapsedTime(&ms[i], c->big_ev[i][0], c->big_ev[i][1]));
-  c->big_rb = ms[1] < 0.5f * (ms[0] + ms[2]) ? lda::SB_RB_SHORT_ROUNDS : 0;
+  // decide only when the three probes timed the same launch shape (a probe
+  // whose sweep launched nothing, or that straddled a schedule change, is no
+  // comparison): otherwise keep the default depth for a hold and retry
+  const int64_t* t = c->big_ev_tag;
+  if (t[0] >= 0 && t[0] == t[1] && t[1] == t[2]) {
+    HIP_TRY(hipEventSynchronize(c->big_ev[2][1]));
+    float ms[3];
+    for (int i = 0; i < 3; ++i) HIP_TRY(hipEventElapsedTime(&ms[i], c->big_ev[i][0], c->big_ev[i][1]));
+    c->big_rb = ms[1] < 0.5f * (ms[0] + ms[2]) ? lda::SB_RB_SHORT_ROUNDS : 0;
+  } else {
+    c->big_rb = 0;
+  }
   c->big_hold = lda_ctx::PROBE_HOLD;
   c->big_probe = 0;
   return LDA_OK;
@@ -1068,8 +1082,12 @@ static lda_status sample_part_impl(lda_ctx* c, int part) {
     const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>(cap, (r1 - r0 + wpb - 1) / wpb));
     const int slot = (int)(c->launches % lda_ctx::LDA_TIME_RING);
     HIP_TRY(hipEventRecord(c->ev0[slot], c->stream));
-    const int probe = part == 0 ? c->big_probe_slot : -1;
-    if (probe >= 0) HIP_TRY(hipEventRecord(c->big_ev[probe][0], c->stream));
+    // a probe sweep times its first launch (part 0 unless that part is empty)
+    const int probe = c->big_probe_slot >= 0 && c->big_ev_tag[c->big_probe_slot] < 0 ? c->big_probe_slot : -1;
+    if (probe >= 0) {
+      c->big_ev_tag[probe] = ((int64_t)(r1 - r0) << 16) | ((int64_t)c->sweep_kind << 8) | part;
+      HIP_TRY(hipEventRecord(c->big_ev[probe][0], c->stream));
+    }
     if (c->sampler == LDA_SAMPLER_SPARSE)
       HIP_TRY(lda::launch_sample_sparse(c->C, false, p, blocks, c->stream, c->big_rb));
     else

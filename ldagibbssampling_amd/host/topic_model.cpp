@@ -125,6 +125,11 @@ class ShardGroup {
   // of all shards [G x escape_count]
   int64_t max_tokens = 0;
   bool compact = true;
+  // shards on one device exchange the compact form through device-side
+  // stand-ins for the collectives (sum of the packed words, copies of the
+  // escape lists): the pack / unpack ordering of the multi-GPU path, run on a
+  // one-GPU box (LDA_LOCAL_COMPACT=1; tests/test_topic_model_gpu.py)
+  bool local_compact = false;
   size_t packed_count = 0, escape_count = 0;
   std::vector<std::vector<void*>> packed, escapes;        // [part][shard]
   std::vector<std::vector<int32_t*>> escapes_all;         // [part][shard], device buffers
@@ -203,7 +208,22 @@ class ShardGroup {
     return static_cast<hipStream_t>(s);
   }
 
-  bool use_compact() const { return compact && !local_sum && ctx.size() > 1; }
+  bool use_compact() const { return compact && (!local_sum || local_compact) && ctx.size() > 1; }
+
+  // local_sum + use_compact(): the packed words summed on streams[0] as
+  // local_reduce sums the int32 buffers, and every shard's escape list copied
+  // into every shard's escapes_all [G x escape_count] in shard order (what
+  // ncclAllReduce + ncclAllGather leave on distinct devices)
+  void local_reduce_compact(int part, const std::vector<hipStream_t>& streams) {
+    const size_t G = ctx.size();
+    const auto& pk = packed[(size_t)part];
+    local_reduce(pk, packed_count, streams);      // packed_count: V Kp / 2 + Kp, a multiple of 4
+    for (size_t g = 0; g < G; ++g)
+      for (size_t r = 0; r < G; ++r)
+        hip_check(hipMemcpyAsync(escapes_all[(size_t)part][g] + r * escape_count, escapes[(size_t)part][r],
+                                 sizeof(int32_t) * escape_count, hipMemcpyDeviceToDevice, streams[g]),
+                  "hipMemcpyAsync");
+  }
 
   // the compact exchange's first step, on every shard's own stream: part
   // `part`'s buffer packed (lda_exchange_pack)
@@ -247,11 +267,14 @@ class ShardGroup {
     size_t count = 0;
     for (size_t g = 0; g < ctx.size(); ++g)
       check(lda_delta_buffer_part(ctx[g], part, &ptr[g], &count), "lda_delta_buffer_part");
+    const bool cmp = use_compact();
     if (local_sum) {
-      local_reduce(ptr, count, streams);
+      if (cmp)
+        local_reduce_compact(part, streams);
+      else
+        local_reduce(ptr, count, streams);
       return;
     }
-    const bool cmp = use_compact();
     ncclResult_t r = ncclGroupStart();
     for (size_t g = 0; g < ctx.size() && r == ncclSuccess; ++g) {
       if (cmp) {
@@ -563,6 +586,8 @@ void ParallelTopicModel::ensureShards() {
   {
     const char* e = std::getenv("LDA_EXCHANGE_INT32");
     sg->compact = compact_exchange_ && !(e && e[0] == '1');
+    const char* lc = std::getenv("LDA_LOCAL_COMPACT");
+    sg->local_compact = lc && lc[0] == '1';
   }
   if (G > 1) {
     // shards recount (or keep a delta) in the same sweeps: the smallest

@@ -96,6 +96,30 @@ def test_large_k_sparse_bit_exact(oracle, K):
     assert abs(lg - lo) <= 1e-9 * abs(lo), (lg, lo)
 
 
+@pytest.mark.parametrize("D,L", [(0, 0), (2, 5)])
+def test_large_k_ring_probe_with_empty_first_part(oracle, D, L):
+    """The large-K sampler times its ring depths on sweeps 8-10 (big_rb_next).
+    An empty shard launches nothing, and under the staleness schedule a tiny
+    shard's part 0 is empty (D=2, L=5: parts [], [docs 0-1]); the probe then
+    times the first launch that runs, or none, and decides only on three
+    equal launches -- sweeps past the decision keep working, bit-exact."""
+    K = 1500
+    rng = np.random.default_rng(D + L)
+    off = np.arange(D + 1, dtype=np.int64) * L
+    corpus = Corpus(off, rng.integers(0, 40, size=D * L).astype(np.int32), 40)
+    g, o = _pair(oracle, corpus, K, np.full(K, 0.05), 0.01, seed=9, kind="sparse")
+    if D:
+        g.set_sequential_sweeps(*oracle.staleness_schedule(4))
+        o.set_sequential_sweeps(*oracle.staleness_schedule(4))
+        o.apply()
+        assert o._sweep_runs()[0] == []          # the first part is empty
+        g.sweep(0)
+    for _ in range(14):
+        g.sweep(1)
+    o.sweep(14)
+    _assert_same_state(g, o)
+
+
 def test_large_k_sparse_long_rows_and_inference(oracle):
     """Frequent words with > 128 nonzero topics (more rounds than the prefetch
     ring holds), then frozen-model inference at K=4096."""

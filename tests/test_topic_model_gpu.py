@@ -274,6 +274,43 @@ def test_shard_group_on_one_device(oracle, shards, parts, kind):
     np.testing.assert_allclose([v for _, v in m.llTrace()], [v for _, v in single.llTrace()], rtol=1e-12)
 
 
+@pytest.mark.parametrize("shards,parts,sequential", [(2, 1, False), (3, 2, False), (3, 1, True)])
+def test_shard_group_compact_exchange_on_one_device(monkeypatch, shards, parts, sequential):
+    """The multi-GPU ShardGroup's compact exchange (pack_part, the packed
+    words' sum and the escape lists' all-gather, unpack_part) with the two
+    collectives replaced by device-side stand-ins (LDA_LOCAL_COMPACT=1), so
+    its ordering runs on the one-GPU box: plain snapshot sweeps (split into
+    `parts`, the exchange on the collective streams) or the default
+    sequential schedules.  K = 2 with one word holding half the tokens puts
+    cells beyond both biases, so escape lists travel; bit-exact against one
+    context."""
+    monkeypatch.setenv("LDA_LOCAL_COMPACT", "1")
+    from ldagibbssampling_amd.corpus import Corpus
+    rng = np.random.default_rng(shards * 10 + parts)
+    D, L, V, K = 1000, 150, 300, 2
+    words = rng.integers(1, V, size=D * L).astype(np.int32)
+    words[rng.random(D * L) < 0.5] = 0
+    c = Corpus(np.arange(D + 1, dtype=np.int64) * L, words, V)
+
+    def run(devices):
+        m, _ = _model(c, K, 1.0, 0.05, 7, setNumIterations=6, setOptimizeInterval=0)
+        if not sequential:
+            m.setWarmStart(1, 0)
+            m.setStalenessThreads(-1)
+        if devices:
+            m.setDevices(devices)
+            m.setExchangeParts(parts)
+        m.estimate()
+        return m
+
+    m = run([0] * shards)
+    single = run(None)
+    assert m.numShards() == shards and single.numShards() == 1
+    np.testing.assert_array_equal(m.topicAssignments(), single.topicAssignments())
+    for a, b in zip(m.typeTopicCounts(), single.typeTopicCounts()):
+        np.testing.assert_array_equal(a, b)
+
+
 def test_num_threads_at_reference_scale_uses_one_gpu():
     """setNumThreads(4) (src/cmu_ron/TrainAndPredict.java:164) on the
     reference's own corpus scale (C1: 2000 changelist docs, ~16k tokens) at
