@@ -881,7 +881,10 @@ std::string ParallelTopicModel::displayTopWords(int32_t num_words, bool using_ne
 // Mallet 2.0.7's new WorkerRunnables drop theirs, so a resumed model starts
 // its statistics empty whatever the file holds.
 namespace {
-constexpr char kMagic[8] = {'L', 'D', 'A', 'T', 'M', 0, 'v', '3'};    // v3: + staleness threads
+// v4: without the alpha-statistics histograms (estimate() starts them
+// empty, as Mallet's new WorkerRunnables do, so a file never needs them)
+constexpr char kMagic[8] = {'L', 'D', 'A', 'T', 'M', 0, 'v', '4'};
+constexpr char kMagicV3[8] = {'L', 'D', 'A', 'T', 'M', 0, 'v', '3'};  // v3: + staleness threads
 constexpr char kMagicV2[8] = {'L', 'D', 'A', 'T', 'M', 0, 'v', '2'};  // v2: + warm start
 constexpr char kMagicV1[8] = {'L', 'D', 'A', 'T', 'M', 0, 'v', '1'};
 
@@ -958,8 +961,6 @@ void ParallelTopicModel::save(const std::string& path) {
   w.vec(has_source_);
   for (const auto& src : sources_) w.str(src);
   w.pod(max_doc_len_);
-  w.vec(doc_len_counts_);
-  w.vec(topic_doc_counts_);
   w.pod(warm_parts_);
   w.pod(warm_sweeps_);
   w.pod(staleness_threads_);
@@ -974,7 +975,8 @@ std::unique_ptr<ParallelTopicModel> ParallelTopicModel::load(const std::string& 
   r.f.read(magic, 8);
   const bool v1 = r.f && std::memcmp(magic, kMagicV1, 8) == 0;
   const bool v2 = r.f && std::memcmp(magic, kMagicV2, 8) == 0;
-  if (!r.f || (!v1 && !v2 && std::memcmp(magic, kMagic, 8) != 0))
+  const bool v3 = r.f && std::memcmp(magic, kMagicV3, 8) == 0;
+  if (!r.f || (!v1 && !v2 && !v3 && std::memcmp(magic, kMagic, 8) != 0))
     raise(LDA_ERR_INVALID_ARG, "not an lda_topic_model checkpoint");
   const int32_t K = r.pod<int32_t>(), V = r.pod<int32_t>();
   const double alpha_sum = r.pod<double>(), beta = r.pod<double>();
@@ -1013,12 +1015,17 @@ std::unique_ptr<ParallelTopicModel> ParallelTopicModel::load(const std::string& 
   m->has_source_ = r.vec<uint8_t>(D);
   for (int64_t d = 0; d < (int64_t)m->has_source_.size(); ++d) m->sources_.push_back(r.str());
   m->max_doc_len_ = r.pod<int32_t>();
-  m->doc_len_counts_ = r.vec<int32_t>(big);
-  m->topic_doc_counts_ = r.vec<int32_t>(big);
-  if ((int64_t)m->has_source_.size() != D ||
-      (m->max_doc_len_ >= 0 && (m->doc_len_counts_.size() != (size_t)m->max_doc_len_ + 1 ||
-                                m->topic_doc_counts_.size() != (size_t)K * (m->max_doc_len_ + 1))))
-    raise(LDA_ERR_INVALID_ARG, "checkpoint corrupt (statistics)");
+  if (v1 || v2 || v3) {            // the histograms older files carry: read past them
+    const std::vector<int32_t> dl = r.vec<int32_t>(big), td = r.vec<int32_t>(big);
+    if (m->max_doc_len_ >= 0 &&
+        (dl.size() != (size_t)m->max_doc_len_ + 1 || td.size() != (size_t)K * (m->max_doc_len_ + 1)))
+      raise(LDA_ERR_INVALID_ARG, "checkpoint corrupt (statistics)");
+  }
+  if ((int64_t)m->has_source_.size() != D) raise(LDA_ERR_INVALID_ARG, "checkpoint corrupt (sources)");
+  if (m->max_doc_len_ >= 0) {
+    m->doc_len_counts_.assign((size_t)m->max_doc_len_ + 1, 0);
+    m->topic_doc_counts_.assign((size_t)K * (m->max_doc_len_ + 1), 0);
+  }
   if (!v1) {
     m->warm_parts_ = r.pod<int32_t>();
     m->warm_sweeps_ = r.pod<int32_t>();

@@ -120,6 +120,29 @@ def test_checkpoint_round_trip_without_gpu(L, tmp_path):
     trunc.write_bytes(p.read_bytes()[:60])
     with pytest.raises(capi.LdaError):
         tm.ParallelTopicModel.load(str(trunc))
+    # a v3 file (round 4) still carries the alpha-statistics histograms after
+    # max_doc_len; v4 files drop them (estimate() starts them empty) and v3
+    # files load with them skipped
+    raw = p.read_bytes()
+    assert raw[:8] == b"LDATM\x00v4"
+    # the last 16 bytes: max_doc_len (-1 before the first estimate), warm
+    # parts, warm sweeps, staleness (int32); a v3 file with sized histograms
+    assert int(np.frombuffer(raw[-16:-12], np.int32)[0]) == -1
+    max_len = 3
+    dl = np.arange(max_len + 1, dtype=np.int32)
+    td = np.arange(7 * (max_len + 1), dtype=np.int32)
+    hist = (np.int64(dl.size).tobytes() + dl.tobytes() + np.int64(td.size).tobytes() + td.tobytes())
+    body = raw[8:-16] + np.int32(max_len).tobytes()
+    v3 = tmp_path / "v3.ldatm"
+    v3.write_bytes(b"LDATM\x00v3" + body + hist + raw[-12:])
+    r3 = tm.ParallelTopicModel.load(str(v3))
+    assert r3._shape() == m._shape()
+    np.testing.assert_array_equal(r3.alpha, m.alpha)
+    bad3 = tmp_path / "bad3.ldatm"             # histograms of the wrong shape
+    bad3.write_bytes(b"LDATM\x00v3" + body + hist[:8 + 4 * dl.size] + np.int64(1).tobytes()
+                     + td[:1].tobytes() + raw[-12:])
+    with pytest.raises(capi.LdaError):
+        tm.ParallelTopicModel.load(str(bad3))
 
 
 def test_shard_plan():
