@@ -181,7 +181,8 @@ def test_unpack_lists_without_escapes_and_argument_checks():
         g.counts_checksum()                          # pending delta
     cap = (es.numel() - 1) // 3
     with pytest.raises(capi.LdaError):
-        g.exchange_unpack(0, 1, g.N, es, list_cap=cap + 1)
+        g.exchange_unpack(0, 1, g.N, torch.zeros(1 + 3 * (cap + 1), dtype=torch.int32, device=es.device),
+                          list_cap=cap + 1)
     with pytest.raises(capi.LdaError):
         g.exchange_unpack(0, 1, g.N, None, list_cap=1)
     g.exchange_unpack(0, 1, g.N, None, list_cap=0)
