@@ -353,7 +353,7 @@ def test_staleness_sweeps_bit_exact(oracle, kind, K, threads, mode):
     np.testing.assert_array_equal(g.z(), o.z())
     g.sample()
     if mode == "recount":
-        assert g.recount()
+        assert g.recount
     g.apply()
     o.sweep(1)
     np.testing.assert_array_equal(g.z(), o.z())
