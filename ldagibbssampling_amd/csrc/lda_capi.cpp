@@ -1347,7 +1347,9 @@ lda_status lda_debug_sample_trace(lda_ctx* c, float* host_trace) {
   HIP_TRY(hipSetDevice(c->device));
   float* tr = nullptr;
   HIP_TRY(dalloc(&tr, (size_t)8 * std::max<int64_t>(c->N, 1)));
-  hipError_t e = hipMemsetAsync(c->queue, 0, sizeof(int32_t), c->stream);
+  // zeroed: measurement builds of the large-K sampler count into it
+  hipError_t e = hipMemsetAsync(tr, 0, sizeof(float) * 8 * std::max<int64_t>(c->N, 1), c->stream);
+  if (e == hipSuccess) e = hipMemsetAsync(c->queue, 0, sizeof(int32_t), c->stream);
   lda::SampleParams p = c->params(false);
   p.trace = tr;
   const int64_t wpb = c->waves_per_block;

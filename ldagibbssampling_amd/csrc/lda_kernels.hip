@@ -1881,6 +1881,13 @@ __global__ __launch_bounds__(256) void k_sample_sparse(SampleParams p) {
 #ifndef SB_RU
 #define SB_RU 2
 #endif
+// 1: the A part's searches read LDS (the alpha part's block from tab, the
+// document part's per-lane sums with rotated reads) instead of global memory
+// -- one global round trip instead of two and eight (round 5; 0 until it has
+// run on the GPU: the searches' results are the same integers either way)
+#ifndef SB_APICK_LDS
+#define SB_APICK_LDS 0
+#endif
 // gfx9 buffer resource word 3 (raw 32-bit loads, bounds checked)
 constexpr int kBufWord3 = 0x00020000;
 #ifndef SB_WAVES
@@ -2034,6 +2041,17 @@ __global__ __launch_bounds__(1024) void k_big_tables(const int32_t* __restrict__
   }
 }
 
+// Inclusive integer wavefront scan (any order is exact for integers).
+__device__ __forceinline__ int wave_incl_scan_i(int x) {
+  x += __builtin_amdgcn_update_dpp(0, x, 0x111, 0xf, 0xf, true);
+  x += __builtin_amdgcn_update_dpp(0, x, 0x112, 0xf, 0xf, true);
+  x += __builtin_amdgcn_update_dpp(0, x, 0x114, 0xf, 0xf, true);
+  x += __builtin_amdgcn_update_dpp(0, x, 0x118, 0xf, 0xf, true);
+  x += __builtin_amdgcn_update_dpp(0, x, 0x142, 0xa, 0xf, false);
+  x += __builtin_amdgcn_update_dpp(0, x, 0x143, 0xc, 0xf, false);
+  return x;
+}
+
 __device__ __forceinline__ int nd16_get(const uint32_t* nd2, int k) {
   return (int)reinterpret_cast<const uint16_t*>(nd2)[k];
 }
@@ -2043,6 +2061,21 @@ __device__ __forceinline__ int nd16_get(const uint32_t* nd2, int k) {
 // out of SGPRs (36 spilled into VGPR lanes with every pointer held live);
 // pointers of rare paths (chunk and document switches, the doc-part search,
 // saturated rows) are re-read from the segment instead of held.
+// SB_X_COUNT (measurement builds only): per-path draw counters in p.trace
+// ([0] tokens, [1] A alpha part, [2] A doc part, [3] own-entry hits, [4]
+// re-draws) when the launch has a trace buffer (lda_debug_sample_trace;
+// plain sweeps have none)
+#ifdef SB_X_COUNT
+#define SB_COUNT(i)                                                                   \
+  do {                                                                                \
+    unsigned* ct_ = reinterpret_cast<unsigned*>(KARG(trace));                      \
+    if ((threadIdx.x & 63) == 0 && ct_ != nullptr) atomicAdd(ct_ + (i), 1u);       \
+  } while (0)
+#else
+#define SB_COUNT(i) \
+  do {              \
+  } while (0)
+#endif
 #define KARG(field)                                                                                   \
   (*reinterpret_cast<const volatile decltype(SampleParams::field)*>(                                  \
       (const char*)(__builtin_amdgcn_kernarg_segment_ptr()) + offsetof(SampleParams, field)))
@@ -2271,16 +2304,14 @@ __global__ __launch_bounds__(64 * sb_waves<C>()) void k_sample_big(SampleParams 
                                    __HIP_MEMORY_SCOPE_WAVEFRONT);
           }
           wave_lds_fence();
-          // the own topic's count after both updates: a plain read behind the
-          // no-return adds (a wave's LDS operations complete in order; a
-          // returning atomic held the rounds' reads behind it)
-          const int ndz = uniform_i(nd16_get(nd2, zo));
-          const float2 tz = tab[zo];
-          const float2 tp = tab[pk >= 0 ? pk : 0];
-          const uint32_t Fz = (uint32_t)uniform_i((int)fixp(tz.x));
-          // (a mask, not a branch: the read stays beside the others)
-          const uint32_t Fp = (uint32_t)uniform_i((int)fixp(tp.x)) & (uint32_t)(-(int)(pk >= 0));
-          R = R + (uint64_t)Fp - (uint64_t)Fz;
+          // the own topic's count after both updates (a plain read behind the
+          // no-return adds: a wave's LDS operations complete in order; a
+          // returning atomic held the rounds' reads behind it) and R's update
+          // are formed in doc_part, in the basic block of the first rounds:
+          // formed here, ahead of the row_sat branch, their reads were waited
+          // for (lgkmcnt(0)) before the rounds' reads were even issued
+          int ndz = 0;
+          uint32_t Fz = 0;
 
           // word part, register rounds: lane l holds entry l + 64 q; accq[q]
           // = the lane's running sum after round q
@@ -2293,10 +2324,26 @@ __global__ __launch_bounds__(64 * sb_waves<C>()) void k_sample_big(SampleParams 
           // row is zero entries, + 0), so the scheduler interleaves the two
           // chains.  A row holding a saturated count takes the general path.
           int64_t dG = 0;
-          uint32_t Fm1z = Fz;
+          uint32_t Fm1z = 0;
           uint64_t As = S0;
           float A_f = 0.0f;
-          auto doc_part = [&]() __attribute__((always_inline)) {
+          // its LDS reads first in the block (issued with, and ahead of, the
+          // rounds' reads: one LDS round trip for both), the rest after the
+          // first rounds
+          struct DocReads {
+            int nz;
+            float iz, ip;
+          };
+          auto doc_reads = [&]() __attribute__((always_inline)) -> DocReads {
+            return DocReads{nd16_get(nd2, zo), tab[zo].x, tab[pk >= 0 ? pk : 0].x};
+          };
+          auto doc_part = [&](const DocReads dr) __attribute__((always_inline)) {
+            ndz = uniform_i(dr.nz);
+            Fz = (uint32_t)uniform_i((int)fixp(dr.iz));
+            const float2 tp = make_float2(dr.ip, 0.0f);
+            // (a mask, not a branch: the read stays beside the others)
+            const uint32_t Fp = (uint32_t)uniform_i((int)fixp(tp.x)) & (uint32_t)(-(int)(pk >= 0));
+            R = R + (uint64_t)Fp - (uint64_t)Fz;
             uint64_t Afx;
             if (!FROZEN) {
               const float4 m1 = rm1[s];
@@ -2325,16 +2372,24 @@ __global__ __launch_bounds__(64 * sb_waves<C>()) void k_sample_big(SampleParams 
               accq[q] = acc;
             }
           };
+          // (the memory barriers keep the doc reads in the branches: hoisted
+          // above the branch, their wait and conversions went with them)
           if (!row_sat) {
+            asm volatile("" ::: "memory");
+            const DocReads dr = doc_reads();
+            // the doc reads issue first; nothing moves across (the scheduler
+            // had issued them after the rounds' reads had been waited for)
+            __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
             for (int q = 0; q < SB_RU; ++q) {
               acc = term_acc(ring[s][q], w, false, acc);
               accq[q] = acc;
             }
-            doc_part();
+            doc_part(dr);
             rounds(false, SB_RU);
           } else {
-            doc_part();
+            asm volatile("" ::: "memory");
+            doc_part(doc_reads());
             rounds(true, 0);
           }
           // every register of this token's ring slot has landed on every path
@@ -2433,6 +2488,31 @@ __global__ __launch_bounds__(64 * sb_waves<C>()) void k_sample_big(SampleParams 
             const float t2 = thr - sumB;
             const uint64_t tfx = d2u64((double)t2 * isig);
             if (tfx < As) {
+              SB_COUNT(1);
+#if SB_APICK_LDS
+              // the block of C topics: the block-end prefixes of G' (one
+              // global read); within it the prefix from LDS: G' = fixp(ainv)
+              // (+ dG at zo) split in 16-bit halves, each scanned in 32-bit
+              // lanes (< 2^22), so no second global round trip
+              const int kc = C * lane + C - 1;
+              const uint64_t pc = KARG(big.pfx)[kc];
+              const int64_t vc = (int64_t)pc + ((!FROZEN && kc >= zo) ? dG : 0);
+              const uint64_t mc = __ballot((uint64_t)vc > tfx);
+              const int L = mc ? (int)__builtin_ctzll(mc) : 63;
+              const int kb = C * L - 1;    // the topic before the block
+              const uint64_t pb = L > 0 ? (((uint64_t)(uint32_t)readlane_i((int)(uint32_t)(pc >> 32), L - 1) << 32) |
+                                           (uint32_t)readlane_i((int)(uint32_t)pc, L - 1))
+                                        : 0ull;
+              const uint64_t El = pb + (uint64_t)((!FROZEN && L > 0 && kb >= zo) ? dG : 0);
+              const int kf = C * L + lane;
+              uint32_t g = 0;
+              if (lane < C) g = fixp(tab[kf].y) + (uint32_t)((!FROZEN && kf == zo) ? dG : 0);
+              const uint32_t slo = (uint32_t)wave_incl_scan_i((int)(g & 0xFFFFu));
+              const uint32_t shi = (uint32_t)wave_incl_scan_i((int)(g >> 16));
+              const uint64_t incl = El + ((uint64_t)shi << 16) + slo;
+              const uint64_t mf = __ballot(lane < C && incl > tfx);
+              const int k = mf ? C * L + (int)__builtin_ctzll(mf) : last_topic;
+#else
               const int kc = C * lane + C - 1;
               const int64_t vc = (int64_t)KARG(big.pfx)[kc] + ((!FROZEN && kc >= zo) ? dG : 0);
               const uint64_t mc = __ballot((uint64_t)vc > tfx);
@@ -2441,9 +2521,32 @@ __global__ __launch_bounds__(64 * sb_waves<C>()) void k_sample_big(SampleParams 
               const int64_t vf = (int64_t)KARG(big.pfx)[kf] + ((!FROZEN && kf >= zo) ? dG : 0);
               const uint64_t mf = __ballot(lane < C && (uint64_t)vf > tfx);
               const int k = mf ? C * L + (int)__builtin_ctzll(mf) : last_topic;
+#endif
               return k < last_topic ? k : last_topic;
             }
             const uint64_t tr = tfx - As;
+            SB_COUNT(2);
+#if SB_APICK_LDS
+            // lane l's topics [C l, C l + C), counts and F (= fixp(inv), as
+            // k_big_tables makes it) from LDS, each lane starting its walk
+            // at its own lane index: at the 2C-word lane stride of the
+            // tables, lanes in step would hit one bank (round 5 had read F
+            // from global memory, one round trip per 8 topics: the document
+            // part of A was ~4% of the draws near init and most of their
+            // time); the own topic's F' = Fm1 added as a correction on its lane
+            uint64_t ps = 0;
+            {
+              const uint16_t* ndh = reinterpret_cast<const uint16_t*>(nd2) + C * lane;
+              const float2* tl = tab + C * lane;
+#pragma unroll 8
+              for (int j = 0; j < C; ++j) {
+                const int o = (j + lane) & (C - 1);
+                ps += (uint64_t)ndh[o] * fixp(tl[o].x);
+              }
+              if (!FROZEN && lane == (int)((uint32_t)zo / (uint32_t)C))
+                ps += (uint64_t)((int64_t)ndz * ((int64_t)Fm1z - (int64_t)Fz));
+            }
+#else
             // lane l's topics [C l, C l + C): the counts as 16-byte LDS reads
             // (single u16 reads at a 2C-byte lane stride all hit one bank),
             // F as 16-byte global reads; the own topic's F' = Fm1 added as a
@@ -2464,6 +2567,7 @@ __global__ __launch_bounds__(64 * sb_waves<C>()) void k_sample_big(SampleParams 
               if (!FROZEN && lane == (int)((uint32_t)zo / (uint32_t)C))
                 ps += (uint64_t)((int64_t)ndz * ((int64_t)Fm1z - (int64_t)Fz));
             }
+#endif
             const uint64_t incl = wave_incl_scan_u64(ps);
             const uint64_t ml = __ballot(incl > tr);
             if (!ml) return last_topic;
@@ -2472,7 +2576,11 @@ __global__ __launch_bounds__(64 * sb_waves<C>()) void k_sample_big(SampleParams 
                                           (uint32_t)readlane_i((int)(uint32_t)incl, L - 1))
                                        : 0ull;
             const int kf = C * L + (lane < C ? lane : C - 1);
+#if SB_APICK_LDS
+            const uint32_t ff = (!FROZEN && kf == zo) ? Fm1z : fixp(tab[kf].x);
+#else
             const uint32_t ff = (!FROZEN && kf == zo) ? Fm1z : KARG(big.F)[kf];
+#endif
             const uint64_t wf = lane < C ? (uint64_t)nd16_get(nd2, kf) * ff : 0ull;
             const uint64_t i2 = wave_incl_scan_u64(wf);
             const uint64_t mf = __ballot(lane < C && El + i2 > tr);
@@ -2485,6 +2593,7 @@ __global__ __launch_bounds__(64 * sb_waves<C>()) void k_sample_big(SampleParams 
           // qsel of lane lstar (its sums are read only for the own check)
           const float T = sumB + A_f;
           const float thr = uniform_f(u * T);
+          SB_COUNT(0);
           int kn, lstar = -1, qsel = -1;
           Walk wk{0u, 0.0f, 0.0f};
           if (thr < sumB) {
@@ -2546,6 +2655,7 @@ __global__ __launch_bounds__(64 * sb_waves<C>()) void k_sample_big(SampleParams 
 #endif
             // the own entry: keep zo with probability O / w, else one re-draw
             // with the entry's width replaced by O
+            SB_COUNT(3);
             if (qsel >= 0) {
               wk.hi = readlane_f(accq[qsel], lstar);
               wk.lo = qsel > 0 ? readlane_f(accq[qsel > 0 ? qsel - 1 : 0], lstar) : 0.0f;
@@ -2560,6 +2670,7 @@ __global__ __launch_bounds__(64 * sb_waves<C>()) void k_sample_big(SampleParams 
               // the re-draw (rare): x2 of the token's Philox block, computed
               // here (the token index passes an opaque register, so the block
               // is not hoisted into every token)
+              SB_COUNT(4);
               uint32_t gt = (uint32_t)t;
               asm volatile("" : "+s"(gt));
               uint32_t y0, y1, y2;
@@ -2600,16 +2711,6 @@ __global__ __launch_bounds__(64 * sb_waves<C>()) void k_sample_big(SampleParams 
   }
 }
 
-// Inclusive integer wavefront scan (any order is exact for integers).
-__device__ __forceinline__ int wave_incl_scan_i(int x) {
-  x += __builtin_amdgcn_update_dpp(0, x, 0x111, 0xf, 0xf, true);
-  x += __builtin_amdgcn_update_dpp(0, x, 0x112, 0xf, 0xf, true);
-  x += __builtin_amdgcn_update_dpp(0, x, 0x114, 0xf, 0xf, true);
-  x += __builtin_amdgcn_update_dpp(0, x, 0x118, 0xf, 0xf, true);
-  x += __builtin_amdgcn_update_dpp(0, x, 0x142, 0xa, 0xf, false);
-  x += __builtin_amdgcn_update_dpp(0, x, 0x143, 0xc, 0xf, false);
-  return x;
-}
 
 // Row capacities min(Kp, word total) (one wave per row).
 __global__ __launch_bounds__(256) void k_row_caps(const int32_t* __restrict__ nw, int64_t V,
