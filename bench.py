@@ -521,7 +521,7 @@ def main():
 
     if rank == 0:
         bpt = bytes_per_token(K)
-        kname = (("k_sample_sparse_big" if K > 1024 else "k_sample_sparse")
+        kname = (("k_sample_big" if K > 1024 else "k_sample_sparse")
                  if args.sampler == "sparse" else "k_sample")
         if args.sampler != "sparse" and sampler.Kp <= 128:
             # K <= 128 picks its dense kernel as lda_create does (LDA_DENSE_HALF:

@@ -52,7 +52,7 @@ def access_pattern(kernel):
     """The calibrated load pattern (tools/fetch_calib.hip) of a sampler kernel:
     its word rows are 16 B per lane at C >= 8, 4 B per lane at C = 2, and 4 B
     per lane in 256 B rounds for the large-K sparse sampler."""
-    if kernel.startswith("k_sample_sparse_big"):
+    if kernel.startswith("k_sample_big") or kernel.startswith("k_sample_sparse_big"):
         return "k_round4"
     if (kernel.startswith("k_sample<8") or kernel.startswith("k_sample<16")
             or kernel.startswith("k_sample_quarter<8")):     # quarter, K <= 128: uint4 per lane
