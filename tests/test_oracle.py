@@ -183,3 +183,38 @@ def test_large_k_draw_samples_the_exact_conditional(oracle):
         # the null's chi2/dof has sd sqrt(2/dof); 1 + 5 sd (or 6 for dof 1)
         assert chi / dof < 1 + 5 * np.sqrt(2 / dof) + (6 if dof == 1 else 0), (c_own, chi, dof)
         assert abs(cnt[zo] / n - p[zo]) < 5 * np.sqrt(p[zo] * (1 - p[zo]) / n) + 1e-4
+
+
+def test_counts_checksum_definition(oracle):
+    """oracle.counts_checksum (the restatement lda_counts_checksum is checked
+    against on the GPU) equals its definition written as a loop: the sum mod
+    2^64 over nonzero cells of splitmix64's finaliser of (index << 32 |
+    uint32 value), nw cells at w K + k, nwsum cells at V K + k; zero cells add
+    nothing, so the hash does not depend on the row padding; one changed
+    count changes it."""
+    M = (1 << 64) - 1
+
+    def mix(x):
+        x ^= x >> 30
+        x = (x * 0xBF58476D1CE4E5B9) & M
+        x ^= x >> 27
+        x = (x * 0x94D049BB133111EB) & M
+        return x ^ (x >> 31)
+
+    rng = np.random.default_rng(4)
+    V, K = 37, 11
+    nw = rng.integers(0, 5, size=(V, K)) * (rng.random((V, K)) < 0.4)
+    nw[3, 4] = 70000                        # beyond 16 bits
+    nwsum = nw.sum(0)
+    want = 0
+    for w in range(V):
+        for k in range(K):
+            if nw[w, k]:
+                want = (want + mix(((w * K + k) << 32) | (int(nw[w, k]) & 0xFFFFFFFF))) & M
+    for k in range(K):
+        if nwsum[k]:
+            want = (want + mix(((V * K + k) << 32) | (int(nwsum[k]) & 0xFFFFFFFF))) & M
+    assert oracle.counts_checksum(nw, nwsum) == want
+    nw2 = nw.copy()
+    nw2[0, 0] += 1
+    assert oracle.counts_checksum(nw2, nwsum) != want
