@@ -72,31 +72,37 @@ def _newest(pattern):
     return sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", pattern)))[::-1]
 
 
-def pmc_record(tokens_per_launch: int, kernel_prefix: str, K: int, burnin: int = 0):
+def pmc_record(tokens_per_launch: int, kernel_prefix: str, K: int, burnin: int = 0, C: int = None):
     """The newest committed rocprofv3 summary (profiles/rNN/traffic_*.json,
     tools/make_traffic.py over separate FETCH_SIZE / WRITE_SIZE / SQ passes of
-    this same command) measured on the kernel code loaded now (the library's
-    sha256, or the sha256 of the kernel sources it is built from), for this
+    this same command) measured on the machine code loaded now, for this
     workload, kernel and burn-in (a file without "burnin" profiled the
     command without one: rows, change rates and bytes per token move with the
-    sweep window); (None, None) otherwise."""
+    sweep window); (None, None) otherwise.
+
+    "The machine code loaded now" is the kernel family's own code
+    (`kernel_code_sha256`: the text and descriptor of every instantiation of
+    e.g. k_sample<8, ...> in the loaded library's gfx950 code object,
+    ldagibbssampling_amd/codeobj.py), so editing one kernel leaves the other
+    kernels' records valid (the whole-file source hash
+    had orphaned the unchanged dense kernel's record).  Records written
+    before round 6 carry only the library's sha256, which still matches."""
     import hashlib
-    from ldagibbssampling_amd import capi
+    from ldagibbssampling_amd import capi, codeobj
     lib = os.environ.get("LDA_MI355X_LIB") or capi.LIB_PATH
     with open(lib, "rb") as f:
         lib_sha = hashlib.sha256(f.read()).hexdigest()
-    # the kernel sources the in-tree library is built from (a variant library
-    # loaded through LDA_MI355X_LIB matches by its own sha only)
-    src = hashlib.sha256()
-    for name in ("lda_kernels.hip", "lda_kernels.h"):
-        with open(os.path.join(ROOT, "ldagibbssampling_amd", "csrc", name), "rb") as f:
-            src.update(f.read())
-    src_sha = None if os.environ.get("LDA_MI355X_LIB") else src.hexdigest()
+    fam = kernel_prefix.rstrip("<")
+    try:
+        code_sha = codeobj.family_sha256(lib, fam, C)
+    except (OSError, ValueError):
+        code_sha = None
     for path in _newest("traffic_*.json"):
         with open(path) as f:
             t = json.load(f)
         same_code = t.get("lib_sha256") == lib_sha or (
-            src_sha is not None and t.get("kernel_src_sha256") == src_sha)
+            code_sha is not None and t.get("kernel_code_sha256") == code_sha
+            and t.get("kernel_family") == codeobj.mangled_prefix(fam, C))
         if (t.get("tokens_per_launch") == tokens_per_launch and same_code
                 and t.get("kernel", "").startswith(kernel_prefix)
                 and t.get("num_topics", K) == K and t.get("burnin", 0) == burnin):
@@ -195,12 +201,9 @@ def cpu_baseline(corpus, K, alpha_sum, beta, budget_s=15.0, threads=4, runs=3):
     speed-up over one thread)."""
     from oracle import oracle as O
     O.build()
-    ndocs = min(corpus.num_docs, 20_000)
-    sub = corpus.subset(np.arange(ndocs))
 
-    def timed(T, budget, max_sweeps):
-        m = O.MalletModel(K, alpha_sum, beta, corpus.num_types, sub.doc_off, sub.words, seed=1,
-                          num_threads=T)
+    def timed(sub, V, T, budget, max_sweeps):
+        m = O.MalletModel(K, alpha_sum, beta, V, sub.doc_off, sub.words, seed=1, num_threads=T)
         m.set_pin_threads(True)
         m.estimate(2)                                    # warm-up sweeps
         m.timing(reset=True)
@@ -213,40 +216,79 @@ def cpu_baseline(corpus, K, alpha_sum, beta, budget_s=15.0, threads=4, runs=3):
                 break
         dt = time.perf_counter() - t0
         ts, tm = m.timing()
-        return sub.num_tokens * sweeps / dt, sweeps, tm / dt
+        n = sub.num_tokens * sweeps
+        return n / dt, sweeps, tm / dt, n / ts
 
-    def leg(T, budget, max_sweeps):
-        r = [timed(T, budget / runs, max_sweeps) for _ in range(runs)]
+    def leg(sub, V, T, budget, max_sweeps, nruns=runs):
+        r = [timed(sub, V, T, budget / nruns, max_sweeps) for _ in range(nruns)]
         v = sorted(x[0] for x in r)
-        return {"median": float(np.median(v)), "min": v[0], "max": v[-1], "runs": runs,
-                "sweeps": [x[1] for x in r], "merge_share": float(np.median([x[2] for x in r]))}
+        return {"median": float(np.median(v)), "min": v[0], "max": v[-1], "runs": nruns,
+                "sweeps": [x[1] for x in r], "merge_share": float(np.median([x[2] for x in r])),
+                # the workers' phase alone (sampling + Mallet's per-worker
+                # buildLocalTypeTopicCounts), without the single-threaded merge
+                "sampling_rate": float(np.median([x[3] for x in r]))}
 
-    l4 = leg(threads, budget_s, 50)
-    l1 = leg(1, budget_s / 2, 20)
+    # (1) the shape-matched sample: Mallet's cost per
+    # token grows with the word's row (its nonzero topics) and its merge with
+    # V x row length, so a 20k-document slice over the full vocabulary (~40
+    # tokens per word type against the workload's N / V) runs short rows and
+    # an inflated merge.  Here the first `nd` documents keep their lengths and
+    # topic mixtures and the vocabulary is folded onto Vs = V * nd / D types
+    # (w -> w mod Vs), so a word type holds the workload's tokens per type
+    # (C4: 2e9 / 1e5 = 20000) and its rows fill as they do at full scale.
+    nd = min(corpus.num_docs, 2_000)
+    vs = max(1, int(round(corpus.num_types * nd / corpus.num_docs)))
+    shaped = corpus.subset(np.arange(nd))
+    from ldagibbssampling_amd.corpus import Corpus
+    shaped = Corpus(shaped.doc_off, np.ascontiguousarray(shaped.words % vs, dtype=np.int32), vs)
+    s4 = leg(shaped, vs, threads, budget_s, 40)
+    s1 = leg(shaped, vs, 1, budget_s / 2, 20)
     tn = cpu_share()
-    ln = leg(tn, budget_s / 2, 50)
+    sn = leg(shaped, vs, tn, budget_s / 2, 40)
+    # (2) rounds 2-5's sample, for continuity: the first 20k documents over
+    # the full vocabulary, one run per leg
+    ndocs = min(corpus.num_docs, 20_000)
+    sub = corpus.subset(np.arange(ndocs))
+    l4 = leg(sub, corpus.num_types, threads, budget_s / 3, 50, nruns=1)
+    l1 = leg(sub, corpus.num_types, 1, budget_s / 3, 20, nruns=1)
     return {
-        "value": l4["median"],
+        "value": s4["median"],
         "unit": "tokens/s",
         "cores": threads,
         "kind": "port",
-        "spread": [l4["min"], l4["max"]],
-        "merge_share": l4["merge_share"],
-        "t1_value": l1["median"],
-        "t1_spread": [l1["min"], l1["max"]],
-        "tnproc_value": ln["median"],
-        "tnproc_spread": [ln["min"], ln["max"]],
-        "tnproc_merge_share": ln["merge_share"],
+        "spread": [s4["min"], s4["max"]],
+        "merge_share": s4["merge_share"],
+        "sampling_rate": s4["sampling_rate"],
+        "t1_value": s1["median"],
+        "t1_spread": [s1["min"], s1["max"]],
+        "t1_sampling_rate": s1["sampling_rate"],
+        "tnproc_value": sn["median"],
+        "tnproc_spread": [sn["min"], sn["max"]],
+        "tnproc_merge_share": sn["merge_share"],
+        "tnproc_sampling_rate": sn["sampling_rate"],
         "tnproc_cores": tn,
+        "sampling_speedup_4_over_1": s4["sampling_rate"] / s1["sampling_rate"],
         "sample": (f"cpu_mallet (Mallet 2.0.7 SparseLDA restatement, oracle/lda_oracle.c), "
                    f"{threads} threads (= setNumThreads(4), src/cmu_ron/TrainAndPredict.java:164), "
-                   f"first {ndocs} docs ({sub.num_tokens} tokens) of this workload; each leg {runs} runs "
-                   f"(2 warm-up sweeps, then timed sweeps: {l4['sweeps']} / 1 thread {l1['sweeps']} / "
-                   f"{tn} threads {ln['sweeps']}), median reported with [min, max] spread, worker t pinned "
-                   f"to the t-th CPU of the job's affinity mask; merge_share = the fraction of the timed wall "
-                   f"time in Mallet's single-threaded sumTypeTopicCounts merge after each sweep; "
-                   f"tnproc: {tn} threads = this job's CPU share (OMP_NUM_THREADS, else the affinity mask); "
-                   f"host {_cpu_model()}, {os.cpu_count()} logical CPUs visible"),
+                   f"shape-matched sample: the first {nd} docs ({shaped.num_tokens} tokens) of this "
+                   f"workload with the vocabulary folded onto {vs} types (w mod {vs}), so that a type "
+                   f"holds the workload's tokens per type ({corpus.num_tokens / max(corpus.num_types, 1):.0f}"
+                   f" in the full corpus, {shaped.num_tokens / vs:.0f} here) and rows reach their "
+                   f"full-scale length; each leg {runs} runs (2 warm-up sweeps, then timed sweeps: "
+                   f"{s4['sweeps']} / 1 thread {s1['sweeps']} / {tn} threads {sn['sweeps']}), median "
+                   f"with [min, max] spread, worker t pinned to the t-th CPU of the job's affinity mask; "
+                   f"merge_share = the fraction of the timed wall time in Mallet's single-threaded "
+                   f"sumTypeTopicCounts merge; sampling_rate = tokens per second of the workers' phase "
+                   f"alone; tnproc: {tn} threads = this job's CPU share (OMP_NUM_THREADS, else the "
+                   f"affinity mask); host {_cpu_model()}, {os.cpu_count()} logical CPUs visible"),
+        "doc_sample": {
+            "docs": ndocs, "tokens": sub.num_tokens, "num_types": corpus.num_types,
+            "value": l4["median"], "merge_share": l4["merge_share"],
+            "sampling_rate": l4["sampling_rate"], "t1_value": l1["median"],
+            "t1_sampling_rate": l1["sampling_rate"],
+            "note": "rounds 2-5's sample (first 20k docs over the full vocabulary: short rows, "
+                    "V-sized merge), one run per leg, kept for continuity",
+        },
     }
 
 
@@ -328,6 +370,61 @@ def estimate_side_figure(device: int, iters: int = 100, burnin: int = 50, worklo
     }
 
 
+def dropin_schedule(args, sampler, trainer, world, device, tokens_all):
+    """What the Java drop-in runs per sweep: the native
+    ParallelTopicModel's default schedule past its warm start -- Mallet's
+    setNumThreads(4) staleness (src/cmu_ron/TrainAndPredict.java:164),
+    lda_staleness_schedule(4): two sequential parts per sweep, each sampled,
+    exchanged across the ranks (N > 1) and applied before the next -- timed
+    over --dropin-steps sweeps after the main timed region (1 untimed warm-up
+    sweep), barrier + synchronize on both sides, max over ranks.  The parts
+    are cut in the whole corpus's global token order (every rank passes the
+    same corpus range), as the shard group does.  Never `value`."""
+    import torch
+    import torch.distributed as dist
+    from ldagibbssampling_amd.sampler import staleness_schedule
+    if args.config.startswith("c1") and world > 1:
+        return None            # c1 shards are separate corpora (token_base = rank << 32)
+    parts, fr = staleness_schedule(4)
+    sampler.set_sequential_sweeps(parts, fr, 0, tokens_all)
+    try:
+        n_ex0 = len(trainer._sent)
+        trainer.sweep(1)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        trainer.sweep(args.dropin_steps)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        t = torch.tensor([dt], dtype=torch.float64, device=f"cuda:{device}")
+        if world > 1:
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+        ks = sampler.sample_times(args.dropin_steps * parts)
+        out = {
+            "tokens_per_s": tokens_all * args.dropin_steps / dt,
+            "ms_per_sweep": 1e3 * dt / args.dropin_steps,
+            "sweeps": args.dropin_steps,
+            "parts_per_sweep": parts,
+            "part_fractions": [float(x) for x in fr],
+            "exchanges_per_sweep": parts if trainer.exchange else 0,
+            "sampler_ms_per_sweep": float(np.sum(ks)) / args.dropin_steps,
+            "escape_counts_read": len(trainer._sent) - n_ex0 if trainer.exchange else 0,
+            "schedule": "lda_staleness_schedule(4): Mallet's setNumThreads(4) mean live fraction "
+                        "1/8, two sequential parts, each exchanged and applied before the next",
+        }
+        if trainer.exchange and trainer.time_reduce:
+            out["collective_ms_per_sweep"] = trainer.reduce_ms(args.dropin_steps * parts) * parts
+        return out
+    finally:
+        sampler.set_sequential_sweeps(1)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -360,6 +457,10 @@ def main():
                     help="N = 1: run the exchange anyway (an RCCL process group of one rank: the "
                          "pack, the in-place all-reduce, the all-gather and the unpack, whose sum "
                          "is the identity) to price the exchange's on-GPU cost; never the default")
+    ap.add_argument("--dropin-steps", type=int, default=5,
+                    help="after the timed region, time this many sweeps under the Java drop-in's "
+                         "default schedule (Mallet's 4-thread staleness: two sequential parts, "
+                         "each exchanged when N > 1; DESIGN.md §2, §5); 0 = skip")
     ap.add_argument("--reserve-cus", type=int, default=-1,
                     help="split sweeps: CUs' worth of sampler blocks left free for RCCL (-1: the library default, 1/32 of the CUs)")
     args = ap.parse_args()
@@ -518,6 +619,8 @@ def main():
     total_tokens = tokens_all * args.steps
     value = total_tokens / elapsed
     ll = trainer.log_likelihood()
+    dropin = dropin_schedule(args, sampler, trainer, world, device, tokens_all) \
+        if args.dropin_steps > 0 else None
 
     if rank == 0:
         bpt = bytes_per_token(K)
@@ -541,7 +644,11 @@ def main():
             enc_model = (f"16-bit row over Kp={sampler.Kp} topics (2 Kp) + word + z read + z write "
                          f"+ amortised delta (4 each)")
         achieved = n_local * enc / (kern_ms * 1e-3) / 1e9          # GB/s, shipped encoding
-        rec, rec_src = pmc_record(n_local, kname + "<", K, args.burnin)
+        # the family's first template argument is C = Kp / 64 for the full-wave
+        # kernels; the half / quarter-wave ones are matched over all their
+        # instantiations
+        farg = None if kname in ("k_sample_half", "k_sample_quarter") else sampler.Kp // 64
+        rec, rec_src = pmc_record(n_local, kname + "<", K, args.burnin, C=farg)
         traffic_gb = rec["hbm_bytes_per_launch"] / 1e9 if rec else None
         tok_s_kernel = n_local / (kern_ms * 1e-3)
         # what binds the sampler.  The dense rows of a table that
@@ -687,6 +794,7 @@ def main():
                             "streamed nonzero entries of long rows + scalar issue; see issue.frac"),
             },
             "collective": coll,
+            "dropin_schedule": dropin,
             "ll_per_token": ll / tokens_all,
             "corpus_gen_s": t_gen,
         }

@@ -106,6 +106,8 @@ class ADLDATrainer:
         self.escape_lists = escape_lists
         self._sent = []            # list_cap all-gathered per exchanged buffer ("used")
         self._counts = None        # per-part escape counts, MAX-all-reduced ("used")
+        self._host_counts = None   # their pinned host copies (GPU)
+        self._count_events = {}    # part -> event recorded after its host copy
 
         self.engine = engine
         self.time_reduce = time_reduce
@@ -229,7 +231,17 @@ class ADLDATrainer:
             # the count first: its all-reduce is done before the packed words'
             cnt = self._count_slots(esc)[part:part + 1]
             cnt.copy_(esc[:1])
-            count_work = dist.all_reduce(cnt, op=dist.ReduceOp.MAX, group=self.group, async_op=async_op)
+            count_work = dist.all_reduce(cnt, op=dist.ReduceOp.MAX, group=self.group, async_op=True)
+            if cnt.device.type == "cuda":
+                # the count travels to pinned host memory behind its own
+                # all-reduce only, before the packed words' all-reduce is
+                # issued: the host's read (_read_counts) waits for this copy,
+                # not for the packed sum, so it overlaps that collective and
+                # leaves the GPU no gap (round 6)
+                if count_work is not None:
+                    count_work.wait()
+                self._stage_count(part, cnt)
+                count_work = None
         works = [dist.all_reduce(packed, op=dist.ReduceOp.SUM, group=self.group, async_op=async_op)]
         if self.escape_lists == "capacity":
             esc_all, w = self._gather(part, esc, esc.numel(), async_op)
@@ -241,12 +253,34 @@ class ADLDATrainer:
             pend.count_work = count_work
         return ([w for w in works if w is not None] if async_op else []), pend
 
+    def _stage_count(self, part: int, cnt):
+        """Copy part `part`'s MAX-reduced count to pinned host memory on
+        torch's current stream (ordered behind the count's all-reduce) and
+        record the event _read_counts waits for."""
+        import torch
+        if self._host_counts is None or self._host_counts.numel() < max(self.parts, part + 1):
+            self._host_counts = torch.zeros(max(self.parts, part + 1), dtype=torch.int32,
+                                            pin_memory=True)
+        self._host_counts[part:part + 1].copy_(cnt, non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        self._count_events[part] = ev
+
     def _read_counts(self, parts: int):
-        """The MAX-all-reduced escape counts of the first `parts` parts (one
-        host read; the caller has waited on the count all-reduces)."""
+        """The MAX-all-reduced escape counts of the first `parts` parts.  On
+        the GPU each count was staged to pinned memory right behind its own
+        all-reduce (_stage_count): this waits for those copies only, while
+        the packed all-reduces issued after them keep running, so the read
+        costs the host a wait but the GPU no idle gap.  On the CPU (gloo) the
+        caller has waited on the count all-reduces."""
         if self.escape_lists != "used" or not self.compact:
             return [0] * parts
-        cnt = [int(x) for x in self._counts[:parts].cpu().tolist()]
+        if getattr(self, "_count_events", None):
+            for i in range(parts):
+                self._count_events.pop(i).synchronize()
+            cnt = [int(x) for x in self._host_counts[:parts].tolist()]
+        else:
+            cnt = [int(x) for x in self._counts[:parts].cpu().tolist()]
         _, n_es = self.engine.exchange_sizes(self.world, self.max_tokens)
         cap = (n_es - 1) // 3
         for m in cnt:
@@ -273,6 +307,8 @@ class ADLDATrainer:
                 ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
                 ev[0].record()
             _, pend = self._exchange_start(0, async_op=False)
+            if pend.count_work is not None:
+                pend.count_work.wait()
             for w in pend.gather(self._read_counts(1)[0], async_op=False):
                 w.wait()
             self._landed()

@@ -14,6 +14,19 @@ import numpy as np
 from . import capi
 
 
+def staleness_schedule(threads: int):
+    """lda_staleness_schedule: (parts, fractions) of the sequential sweeps that
+    give every token the mean live fraction of Mallet's `threads` worker
+    threads (the native ParallelTopicModel's default schedule
+    past the warm start, what the Java drop-in runs)."""
+    L = capi.load()
+    parts = C.c_int32()
+    fr = np.zeros(capi.MAX_EXCHANGE_PARTS, dtype=np.float64)
+    capi.check(L.lda_staleness_schedule(int(threads), C.byref(parts), fr.ctypes.data),
+               "lda_staleness_schedule")
+    return int(parts.value), fr[:parts.value].copy()
+
+
 class _DeviceArray:
     """Exposes a device pointer through __cuda_array_interface__ (zero-copy
     torch.as_tensor view of the delta buffer for torch.distributed)."""

@@ -113,16 +113,16 @@ def test_bench_traffic_record_matches_its_sweep_window():
     spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(root, "bench.py"))
     bench = importlib.util.module_from_spec(spec)
     spec.loader.exec_module(bench)
-    rec, src = bench.pmc_record(250_000_000, "k_sample_big<", 4096, 0)
+    rec, src = bench.pmc_record(250_000_000, "k_sample_big<", 4096, 0, C=64)
     if rec is None:
         pytest.skip("no C5 profile of the kernel sources in the tree")
     assert src.endswith("traffic_c5.json")
     assert rec.get("burnin", 0) == 0
-    rec30, src30 = bench.pmc_record(250_000_000, "k_sample_big<", 4096, 30)
+    rec30, src30 = bench.pmc_record(250_000_000, "k_sample_big<", 4096, 30, C=64)
     if rec30 is not None:
         assert src30.endswith("traffic_c5_b30.json") and rec30["burnin"] == 30
         assert rec30["bytes_per_token"] < rec["bytes_per_token"]
-    assert bench.pmc_record(250_000_000, "k_sample_big<", 4096, 7) == (None, None)
+    assert bench.pmc_record(250_000_000, "k_sample_big<", 4096, 7, C=64) == (None, None)
 
 
 def test_version_string_carries_the_abi_number(lib):

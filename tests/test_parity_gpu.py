@@ -333,8 +333,38 @@ def test_sparse_saturated_counts(oracle):
     _assert_same_state(g, o, with_nd=False)
 
 
-@pytest.mark.parametrize("kind", ["dense", "sparse"])
-def test_wide_rows_escape(oracle, kind):
+def test_large_k_saturated_counts(oracle):
+    """The large-K sampler's saturated entries: a count >= 2^20 - 1
+    does not fit the packed 20-bit field, and k_sample_big reads it from the
+    dense row in three places -- the B-part term, the own-entry accept step
+    (which reloads c of the selected entry) and the re-walk after a re-draw.
+    K = 1500 (C = 32), one word holding 97% of 2.4M tokens, its tokens
+    assigned in order so that topic 0 starts at exactly 2^20 - 1 (the first
+    saturated value; the first sweep moves it below), topic 1 at 2^20 + 20000
+    (saturated in every sweep: ~99% of the word's draws and own entries hit
+    it) and topic 2 the rest; every other token starts at a random topic.
+    Bit-exact against exact_draw_big for 4 sweeps."""
+    D, L, K = 40, 60000, 1500
+    rng = np.random.default_rng(11)
+    words = np.where(rng.random(D * L) < 0.97, 0, rng.integers(1, 50, D * L)).astype(np.int32)
+    c = Corpus(np.arange(D + 1, dtype=np.int64) * L, words, 50)
+    sat = (1 << 20) - 1
+    hot = np.flatnonzero(words == 0)
+    n1 = sat + 20001
+    assert len(hot) > sat + n1
+    z0 = rng.integers(0, K, D * L).astype(np.int32)
+    z0[hot[:sat]] = 0
+    z0[hot[sat:sat + n1]] = 1
+    z0[hot[sat + n1:]] = 2
+    g, o = _pair(oracle, c, K, np.full(K, 0.1), 0.01, seed=5, z_init=z0, kind="sparse")
+    g.sweep(0)
+    o.apply()
+    assert g.counts()[0][0, 0] == sat and g.counts()[0][0, 1] == n1
+    for _ in range(4):
+        g.sweep(1)
+        o.sweep(1)
+        _assert_same_state(g, o, with_nd=False)
+        assert g.counts()[0][0, 1] >= sat          # the saturated path runs every sweep
     """Large counts (> 65535) through both draws: fp32 conversion of big counts
     in the dense word factors, exact escape reads in the sparse entries."""
     from ldagibbssampling_amd.corpus import Corpus

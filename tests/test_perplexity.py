@@ -54,8 +54,11 @@ def score_state(oracle, K, V, train, z, held_obs, held_sc, alpha=None, beta=None
     model's learned ones."""
     alpha = np.full(K, ALPHA_SUM / K) if alpha is None else np.asarray(alpha, dtype=np.float64)
     beta = BETA if beta is None else float(beta)
+    # K > 1024 runs the large-K sparse sampler (k_sample_big), whose frozen
+    # draw cpu_exact restates as exact_draw_big
     e = oracle.ExactSampler(K, V, train.doc_off, train.words, alpha, beta, 1,
-                            z_init=z, half=2 if K <= 128 else 0)
+                            z_init=z, half=2 if K <= 128 else 0,
+                            kind="sparse" if K > LARGE_K else "dense")
     e.sweep(0)
     theta = e.infer(held_obs.doc_off, held_obs.words, n_iter=100, burn_in=10, thin=10, seed=7)
     nw, nwsum, _, _ = e.counts()
@@ -72,16 +75,21 @@ def _perplexity(sampler, held_obs, held_sc, oracle):
 
 
 SEEDS = range(1, 97)
+LARGE_K = 1024        # above: the large-K sparse sampler (the dense kernels stop at 1024)
 WARM = (4, 50)        # the training loop's default warm start (ParallelTopicModel.setWarmStart)
 TRAP = 1.02
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 
 
 def mallet_fixture(K):
-    with open(os.path.join(GOLDEN, f"mallet_ppl_k{K}.json")) as f:
+    """cpu_mallet's per-seed perplexities (and the seeds) for the plain test."""
+    path = os.path.join(GOLDEN, f"mallet_ppl_k{K}.json")
+    if not os.path.exists(path):
+        pytest.skip(f"no cpu_mallet fixture {path} (tools/ppl_mallet_seeds.py makes it)")
+    with open(path) as f:
         d = json.load(f)
     assert (d["K"], d["alpha_sum"], d["beta"], d["sweeps"]) == (K, ALPHA_SUM, BETA, 1000)
-    return np.asarray(d["perplexity"])
+    return np.asarray(d["perplexity"]), list(d.get("seeds", SEEDS))
 
 
 def parity_bars(pg, pm):
@@ -95,23 +103,32 @@ def parity_bars(pg, pm):
     return pg.mean() / pm.mean() - 1, np.median(pg) / np.median(pm) - 1, float(p), a, b
 
 
-@pytest.mark.parametrize("K", [20, 100])
+@pytest.mark.parametrize("K", [20, 100, 2048, 4096])
 def test_heldout_perplexity_within_1pct(oracle, K):
+    """K = 20 / 100: the quarter-wave / full-wave dense kernels over 96 seeds.
+    K = 2048 / 4096 (round 6, VERDICT r5 missing #2): the large-K sparse
+    sampler k_sample_big (C = 32 / 64), whose round-5 draw -- the exact
+    fixed-point doc part and the own-entry accept / re-draw --
+    had only a per-draw chi-square test behind it; 16 seeds each against the
+    committed cpu_mallet fixture (tools/ppl_mallet_seeds.py, scored with the
+    large-K inference draw), the same three bars."""
     from ldagibbssampling_amd.sampler import GibbsSampler
     c, train, held_obs, held_sc = _corpus_split(K)
     alpha = np.full(K, ALPHA_SUM / K)
+    pm, seeds = mallet_fixture(K)
     pg = []
-    for seed in SEEDS:
-        g = GibbsSampler(K, c.num_types, train.doc_off, train.words, alpha, BETA, seed=seed)
+    for seed in seeds:
+        g = GibbsSampler(K, c.num_types, train.doc_off, train.words, alpha, BETA, seed=seed,
+                         sampler="sparse" if K > LARGE_K else "dense")
         g.set_warm_start(*WARM)
         g.sweep(1000)
         pg.append(_perplexity(g, held_obs, held_sc, oracle))
         g.close()
-    pm = mallet_fixture(K)
     dmean, dmed, p, a, b = parity_bars(pg, pm)
     print(f"K={K}: gpu mean {np.mean(pg):.3f} median {np.median(pg):.3f} trapped {a}/{len(pg)} | "
           f"cpu_mallet mean {pm.mean():.3f} median {np.median(pm):.3f} trapped {b}/{len(pm)} | "
           f"mean {dmean:+.3%} median {dmed:+.3%} Fisher p {p:.3f}")
+    print("GPU_PER_SEED " + json.dumps({"K": K, "seeds": seeds, "perplexity": pg}))
     assert abs(dmean) <= 0.01
     assert -0.01 <= dmed <= 0.005
     assert p >= 0.01

@@ -128,6 +128,16 @@ def main(d, kernel, tokens, workload, out, K=None, burnin=None):
         "liblda_mi355x.so")
     t["lib_sha256"] = lib_sha256(lib)
     t["kernel_src_sha256"] = kernel_src_sha256()
+    # the machine code of this kernel family (every instantiation's text and
+    # descriptor, ldagibbssampling_amd/codeobj.py): what bench.py matches on,
+    # so an edit to another kernel does not orphan this record
+    sys.path.insert(0, ROOT)
+    from ldagibbssampling_amd import codeobj
+    fam, arg = codeobj.family_of(kernel)
+    if fam in ("k_sample_half", "k_sample_quarter"):
+        arg = None       # bench.py matches these over all their instantiations
+    t["kernel_family"] = codeobj.mangled_prefix(fam, arg)
+    t["kernel_code_sha256"] = codeobj.family_sha256(lib, fam, arg)
     with open(out, "w") as f:
         json.dump(t, f, indent=1)
     print(json.dumps(t, indent=1))

@@ -8,6 +8,9 @@ quarter-wave kernel, which cpu_exact restates bit for bit).
 
   python tools/ppl_mallet_seeds.py K first_seed last_seed > out.json
 
+K > 1024 (round 6): scored with the large-K sparse sampler's inference draw
+(exact_draw_big), the kernel the GPU leg runs there.
+
 The output is the committed fixture tests/golden/mallet_ppl_k{K}.json that
 tests/test_perplexity.py compares the GPU sampler against (the GPU test does
 not retrain cpu_mallet: 96 seeds take ~16 CPU-minutes).
@@ -24,14 +27,16 @@ sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "tests"))
 
 from oracle import oracle  # noqa: E402  (the checker)
-from test_perplexity import ALPHA_SUM, BETA, _corpus_split, score_state  # noqa: E402
+from test_perplexity import ALPHA_SUM, BETA, LARGE_K, _corpus_split, score_state  # noqa: E402
 
 
 def main():
     K, s0, s1 = int(sys.argv[1]), int(sys.argv[2]), int(sys.argv[3])
     c, train, held_obs, held_sc = _corpus_split(K)
     out = {"K": K, "alpha_sum": ALPHA_SUM, "beta": BETA, "sweeps": 1000, "threads": 4,
-           "estimator": "document completion, lda_infer(100, 10, 10, seed 7), quarter-wave draw",
+           "estimator": "document completion, lda_infer(100, 10, 10, seed 7), " + (
+               "large-K sparse draw (exact_draw_big)" if K > LARGE_K else
+               "quarter-wave draw" if K <= 128 else "full-wave dense draw"),
            "seeds": [], "perplexity": []}
     for seed in range(s0, s1 + 1):
         t = time.time()

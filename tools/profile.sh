@@ -11,7 +11,7 @@ export TMPDIR=/tmp
 P=gpurun_out/prof_${LABEL:-run}
 mkdir -p $P
 STEPS=${STEPS:-10}; WARMUP=${WARMUP:-3}; BURNIN=${BURNIN:-0}
-B="python3 bench.py --steps $STEPS --warmup $WARMUP --burnin $BURNIN --no-cpu-baseline --no-estimate ${BENCH_ARGS:-}"
+B="python3 bench.py --steps $STEPS --warmup $WARMUP --burnin $BURNIN --no-cpu-baseline --no-estimate --dropin-steps 0 ${BENCH_ARGS:-}"
 SKIP=$((WARMUP + BURNIN))
 PER_SWEEP=${PER_SWEEP:-1}   # sampler launches per sweep (--exchange-parts P: P)
 SEL='--kernel-include-regex k_sample|k_apply|k_prepare|k_count|k_build|k_recount'
