@@ -216,8 +216,9 @@ def cpu_baseline(corpus, K, alpha_sum, beta, budget_s=15.0, threads=4, runs=3):
                 break
         dt = time.perf_counter() - t0
         ts, tm = m.timing()
+        tb = m.build_time()
         n = sub.num_tokens * sweeps
-        return n / dt, sweeps, tm / dt, n / ts
+        return n / dt, sweeps, tm / dt, n / ts, n / max(ts - tb, 1e-12), tb / ts
 
     def leg(sub, V, T, budget, max_sweeps, nruns=runs):
         r = [timed(sub, V, T, budget / nruns, max_sweeps) for _ in range(nruns)]
@@ -226,7 +227,12 @@ def cpu_baseline(corpus, K, alpha_sum, beta, budget_s=15.0, threads=4, runs=3):
                 "sweeps": [x[1] for x in r], "merge_share": float(np.median([x[2] for x in r])),
                 # the workers' phase alone (sampling + Mallet's per-worker
                 # buildLocalTypeTopicCounts), without the single-threaded merge
-                "sampling_rate": float(np.median([x[3] for x in r]))}
+                "sampling_rate": float(np.median([x[3] for x in r])),
+                # the draws alone: the workers' phase less Mallet's per-worker
+                # buildLocalTypeTopicCounts (each T > 1 worker re-inserts its
+                # documents' tokens into count-sorted rows every sweep)
+                "draw_rate": float(np.median([x[4] for x in r])),
+                "build_share": float(np.median([x[5] for x in r]))}
 
     # (1) the shape-matched sample: Mallet's cost per
     # token grows with the word's row (its nonzero topics) and its merge with
@@ -268,6 +274,17 @@ def cpu_baseline(corpus, K, alpha_sum, beta, budget_s=15.0, threads=4, runs=3):
         "tnproc_sampling_rate": sn["sampling_rate"],
         "tnproc_cores": tn,
         "sampling_speedup_4_over_1": s4["sampling_rate"] / s1["sampling_rate"],
+        "draw_rate": s4["draw_rate"],
+        "t1_draw_rate": s1["draw_rate"],
+        "draw_speedup_4_over_1": s4["draw_rate"] / s1["draw_rate"],
+        "build_share": s4["build_share"],
+        "why_4_threads_scale_weakly": (
+            "Mallet's multi-thread sweep does work a single thread does not: after its draws every "
+            "worker rebuilds its local typeTopicCounts from its own documents "
+            "(buildLocalTypeTopicCounts: a linear search and re-sort in the count-sorted row per "
+            "token; build_share of the workers' phase), then one thread merges them "
+            "(sumTypeTopicCounts, merge_share of the wall time); the draws alone scale by "
+            "draw_speedup_4_over_1"),
         "sample": (f"cpu_mallet (Mallet 2.0.7 SparseLDA restatement, oracle/lda_oracle.c), "
                    f"{threads} threads (= setNumThreads(4), src/cmu_ron/TrainAndPredict.java:164), "
                    f"shape-matched sample: the first {nd} docs ({shaped.num_tokens} tokens) of this "

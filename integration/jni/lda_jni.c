@@ -14,9 +14,15 @@
  *   - a Get<Type>ArrayElements that returns NULL leaves the JVM's
  *     OutOfMemoryError pending: every array pinned so far is released with
  *     JNI_ABORT and the call returns 0 without a second exception;
- *   - an ldaj_estimate error releases every array with JNI_ABORT (the Java
- *     arrays keep their values: no half-written state is published) and
- *     throws java.lang.RuntimeException carrying ldaj_last_error();
+ *   - an ldaj_estimate error releases every array with JNI_ABORT and throws
+ *     java.lang.RuntimeException carrying ldaj_last_error().  On a JVM that
+ *     hands out copies (isCopy == JNI_TRUE, HotSpot's usual behaviour) the
+ *     Java arrays keep their values; on one that pins them in place
+ *     (isCopy == JNI_FALSE, which the JNI spec allows) ldaj_estimate may
+ *     already have written z, alpha, the packed rows and tokensPerTopic, and
+ *     JNI_ABORT cannot undo that: after the exception those arrays are
+ *     indeterminate and the model must be rebuilt (Mallet's own estimate()
+ *     gives no stronger guarantee on an exception);
  *   - on success the inputs (docOff, words, options, rowOff) are released with
  *     JNI_ABORT and the outputs with mode 0 (copied back).
  */

@@ -1167,6 +1167,8 @@ __device__ __forceinline__ float row_get_f(float v, int rowbase, int i) {
   return __builtin_bit_cast(float, row_get_i(__builtin_bit_cast(int, v), rowbase, i));
 }
 
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
 template <int CH, int P, bool FROZEN>
 // 5 waves per SIMD for the training kernel (96 VGPRs + 24 B/lane of spill
 // at CH = 8): +7% on C2 after burn-in, equal near
@@ -1174,6 +1176,11 @@ template <int CH, int P, bool FROZEN>
 // lose 25% (profiles/r02/quarter/ab).  The frozen kernel fits 5 unforced.
 #ifndef QUARTER_WPE
 #define QUARTER_WPE 5
+#endif
+// 1: the word factors and the prefix-count sums two topics per packed fp32
+// instruction (round 6 A/B)
+#ifndef QUARTER_PK
+#define QUARTER_PK 0
 #endif
 #define QUARTER_ATTR __attribute__((amdgpu_waves_per_eu(FROZEN ? 4 : QUARTER_WPE)))
 __global__ __launch_bounds__(256) QUARTER_ATTR void k_sample_quarter(SampleParams p) {
@@ -1413,6 +1420,29 @@ __global__ __launch_bounds__(256) QUARTER_ATTR void k_sample_quarter(SampleParam
       const float bc = FROZEN ? 0.0f : ((float)(c_old - 1) + beta) * cinv;
       float S[CH];
       float acc = 0.0f;
+#if QUARTER_PK
+      // the word factors two topics per instruction (v_pk_add_f32 /
+      // v_pk_mul_f32: the same IEEE operations, element for element)
+      float bw[CH];
+#pragma unroll
+      for (int j = 0; j < CH; j += 2) {
+        if (j + 1 < CH) {
+          const f32x2 cf = {(float)cfull[j], (float)cfull[j + 1]};
+          const f32x2 iv = {inv_r[j], inv_r[j + 1]};
+          const f32x2 bb = {beta, beta};
+          const f32x2 r = (cf + bb) * iv;
+          bw[j] = r.x;
+          bw[j + 1] = r.y;
+        } else {
+          bw[j] = ((float)cfull[j] + beta) * inv_r[j];
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < CH; ++j) {
+        acc = __builtin_fmaf(a[j], own[j] ? bc : bw[j], acc);
+        S[j] = acc;
+      }
+#else
 #pragma unroll
       for (int j = 0; j < CH; ++j) {
         const float bw = ((float)cfull[j] + beta) * inv_r[j];
@@ -1420,6 +1450,7 @@ __global__ __launch_bounds__(256) QUARTER_ATTR void k_sample_quarter(SampleParam
         acc = __builtin_fmaf(a[j], b, acc);
         S[j] = acc;
       }
+#endif
       const float T = row_scan16_q(acc);
       const float thr = u * row_bcast15_f(T);
       // l* = #{row-lanes with T <= thr} (T is monotone), clamped to the last:
@@ -1431,8 +1462,25 @@ __global__ __launch_bounds__(256) QUARTER_ATTR void k_sample_quarter(SampleParam
       // lane l*'s is the draw's (E = T_{l*-1}), fetched once
       const float E = dpp_mov<0x111, 0xf, true>(T);
       int cl = 0;
+#if QUARTER_PK
+      {
+        const f32x2 ee = {E, E};
+#pragma unroll
+        for (int j = 0; j < CH; j += 2) {
+          if (j + 1 < CH) {
+            const f32x2 sj = {S[j], S[j + 1]};
+            const f32x2 es = ee + sj;
+            cl += (es.x <= thr) ? 1 : 0;
+            cl += (es.y <= thr) ? 1 : 0;
+          } else {
+            cl += (E + S[j] <= thr) ? 1 : 0;
+          }
+        }
+      }
+#else
 #pragma unroll
       for (int j = 0; j < CH; ++j) cl += (E + S[j] <= thr) ? 1 : 0;
+#endif
       const int cnt = row_get_i(cl, rb, ls);
       const int lim = ls < last_lane ? CH - 1 : last_j_tail;
       const int kn = ls * CH + (cnt < lim ? cnt : lim);
@@ -1881,12 +1929,14 @@ __global__ __launch_bounds__(256) void k_sample_sparse(SampleParams p) {
 #ifndef SB_RU
 #define SB_RU 2
 #endif
-// 1: the A part's searches read LDS (the alpha part's block from tab, the
-// document part's per-lane sums with rotated reads) instead of global memory
-// -- one global round trip instead of two and eight (round 5; 0 until it has
-// run on the GPU: the searches' results are the same integers either way)
+// 1 (default since round 6): the A part's searches read LDS (the alpha
+// part's block from tab, the document part's per-lane sums with rotated
+// reads) instead of global memory -- one global round trip instead of two and
+// eight.  Same integers either way: 32 large-K parity tests green on both
+// builds; C5 2.18 -> 2.29e9 near init, 2.70 -> 2.77e9 after 30 sweeps
+// (profiles/r06/c5ab/).  0 keeps round 5's global-memory searches.
 #ifndef SB_APICK_LDS
-#define SB_APICK_LDS 0
+#define SB_APICK_LDS 1
 #endif
 // gfx9 buffer resource word 3 (raw 32-bit loads, bounds checked)
 constexpr int kBufWord3 = 0x00020000;
@@ -2162,8 +2212,16 @@ __global__ __launch_bounds__(64 * sb_waves<C>()) void k_sample_big(SampleParams 
     philox_x01(gbase + (uint64_t)lane, p.c2, p.c3, p.k0, p.k1, cx0, cx1);
     __builtin_amdgcn_s_waitcnt(kVmcnt0);
 
+    // SB_X_NODELTA: attribution builds only (wrong counts): no delta atomics.
+    // Not informative as run in round 6: without the changes the counts stay
+    // at their random start, the rows stay long and the sweep ran 2x slower
+#ifdef SB_X_NODELTA
+    constexpr bool kDelta = false;
+#else
+    constexpr bool kDelta = !FROZEN;
+#endif
     auto flush_chunk = [&]() {
-      if (!FROZEN && cn != cz) {
+      if (kDelta && cn != cz) {
         const uint64_t rb = (uint64_t)(uint32_t)cw * (uint64_t)KP;
         atomicAdd(KARG(delta) + (rb + (uint32_t)cz), -1);
         atomicAdd(KARG(delta) + (rb + (uint32_t)cn), 1);
@@ -2267,7 +2325,7 @@ __global__ __launch_bounds__(64 * sb_waves<C>()) void k_sample_big(SampleParams 
             // believes in flight makes it wait vmcnt(0) where a token reads
             // it, i.e. drain the row ring
             __builtin_amdgcn_s_waitcnt(kVmcnt1);
-            if (!FROZEN && on != oz) {
+            if (kDelta && on != oz) {
               const uint64_t rb = (uint64_t)(uint32_t)ow * (uint64_t)KP;
               atomicAdd(KARG(delta) + (rb + (uint32_t)oz), -1);
               atomicAdd(KARG(delta) + (rb + (uint32_t)on), 1);

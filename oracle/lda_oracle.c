@@ -1151,6 +1151,7 @@ typedef struct {
   int collect;                 /* shouldSaveState: record alpha statistics */
   int32_t* doc_len_counts;     /* [max_len+1] */
   int32_t* topic_doc_counts;   /* [K][max_len+1] */
+  double t_build;              /* this sweep's buildLocalTypeTopicCounts seconds */
 } mallet_worker;
 
 struct orc_mallet {
@@ -1174,6 +1175,7 @@ struct orc_mallet {
   /* wall time of the sweeps' sampling (the workers' parallel section) and of
    * the sumTypeTopicCounts merge (orc_mallet_timing; bench.py cpu_baseline) */
   double t_sample, t_merge;
+  double t_build;   /* per sweep, the slowest worker's buildLocalTypeTopicCounts */
   int pin_threads;   /* 1: worker t pinned to the t-th CPU of the affinity mask */
 };
 
@@ -1550,6 +1552,12 @@ typedef struct {
   int t;
 } mallet_job;
 
+static double wall_s(void) {
+  struct timespec ts;
+  clock_gettime(CLOCK_MONOTONIC, &ts);
+  return (double)ts.tv_sec + 1e-9 * (double)ts.tv_nsec;
+}
+
 /* WorkerRunnable.run() [M] */
 static void* mallet_worker_run(void* arg) {
   mallet_job* job = (mallet_job*)arg;
@@ -1562,7 +1570,11 @@ static void* mallet_worker_run(void* arg) {
   }
   for (int64_t d = wk->start_doc; d < m->D && d < wk->start_doc + wk->num_docs; ++d)
     mallet_sample_doc(m, wk, d);
-  if (m->T > 1) build_counts(m, wk->ttc, wk->tpt, wk->start_doc, wk->start_doc + wk->num_docs);
+  if (m->T > 1) {
+    const double tb = wall_s();
+    build_counts(m, wk->ttc, wk->tpt, wk->start_doc, wk->start_doc + wk->num_docs);
+    wk->t_build = wall_s() - tb;
+  }
   return NULL;
 }
 
@@ -1618,18 +1630,15 @@ static void mallet_sum_type_topic_counts(orc_mallet* m) {
   }
 }
 
-static double wall_s(void) {
-  struct timespec ts;
-  clock_gettime(CLOCK_MONOTONIC, &ts);
-  return (double)ts.tv_sec + 1e-9 * (double)ts.tv_nsec;
-}
-
 void orc_mallet_set_pin_threads(orc_mallet* m, int32_t on) { m->pin_threads = on; }
 void orc_mallet_timing(orc_mallet* m, double* sample_s, double* merge_s, int32_t reset) {
   if (sample_s) *sample_s = m->t_sample;
   if (merge_s) *merge_s = m->t_merge;
-  if (reset) m->t_sample = m->t_merge = 0.0;
+  if (reset) m->t_sample = m->t_merge = m->t_build = 0.0;
 }
+/* the part of the timed sampling phase spent in the workers'
+ * buildLocalTypeTopicCounts (the slowest worker's, summed over sweeps) */
+void orc_mallet_timing_build(const orc_mallet* m, double* build_s) { *build_s = m->t_build; }
 
 void orc_mallet_estimate(orc_mallet* m, int32_t n_iter) {
   mallet_job* jobs = (mallet_job*)malloc(sizeof(mallet_job) * m->T);
@@ -1661,6 +1670,9 @@ void orc_mallet_estimate(orc_mallet* m, int32_t n_iter) {
       }
       for (int t = 0; t < m->T; ++t) pthread_join(th[t], NULL);
       const double t1 = wall_s();
+      double tb = 0.0;
+      for (int t = 0; t < m->T; ++t) tb = m->workers[t].t_build > tb ? m->workers[t].t_build : tb;
+      m->t_build += tb;
       mallet_sum_type_topic_counts(m);
       m->t_sample += t1 - t0;
       m->t_merge += wall_s() - t1;

@@ -98,6 +98,7 @@ def lib():
     L.orc_mallet_estimate.argtypes = [C.c_void_p, C.c_int32]
     L.orc_mallet_set_pin_threads.argtypes = [C.c_void_p, C.c_int32]
     L.orc_mallet_timing.argtypes = [C.c_void_p, C.POINTER(C.c_double), C.POINTER(C.c_double), C.c_int32]
+    L.orc_mallet_timing_build.argtypes = [C.c_void_p, C.POINTER(C.c_double)]
     L.orc_mallet_set_optimize.argtypes = [C.c_void_p, C.c_int32, C.c_int32, C.c_int32]
     L.orc_mallet_get_hyper.argtypes = [C.c_void_p, _f64p, C.POINTER(C.c_double)]
     L.orc_mallet_log_likelihood.restype = C.c_double
@@ -432,6 +433,14 @@ class MalletModel:
         a, b = C.c_double(), C.c_double()
         lib().orc_mallet_timing(self._h, C.byref(a), C.byref(b), 1 if reset else 0)
         return a.value, b.value
+
+    def build_time(self) -> float:
+        """Seconds of the timed sampling phase spent in the workers'
+        buildLocalTypeTopicCounts (the slowest worker per sweep; 0 with one
+        thread, which Mallet does not rebuild); reset with timing(reset=True)."""
+        a = C.c_double()
+        lib().orc_mallet_timing_build(self._h, C.byref(a))
+        return a.value
 
     def estimate(self, n_iter):
         lib().orc_mallet_estimate(self._h, int(n_iter))

@@ -238,3 +238,25 @@ def test_profile_summary_windows_the_bench_sweeps(tmp_path):
     assert s["kernels"][k8]["calls"] == 1 and s["kernels"][k8]["avg_ns"] == 50     # sweep 5
     assert s["counters"][k10]["WRITE_SIZE"]["avg_per_dispatch"] == 50
     assert s["kernels"]["k_apply"]["calls"] == 3
+
+
+def test_kernel_code_hashes_cover_the_samplers(lib):
+    """bench.py matches PMC records to the machine code of one kernel family
+    (ldagibbssampling_amd/codeobj.py): every sampler family is found in the
+    library's gfx950 code object, none holds a PC-relative reference (whose
+    immediate would move with the layout), and the hashes of two families
+    differ while one family's hash is reproducible."""
+    from ldagibbssampling_amd import codeobj
+    ks = codeobj.kernels(codeobj.device_code_object(capi.LIB_PATH))
+    for fam, arg in (("k_sample", 8), ("k_sample", 16), ("k_sample_big", 64), ("k_sample_big", 32),
+                     ("k_sample_quarter", None), ("k_sample_sparse", 8)):
+        pre = codeobj.mangled_prefix(fam, arg)
+        names = [k for k in ks if k.startswith(pre)]
+        assert names, pre
+        assert all(codeobj.pc_relative_free(ks[k][0]) for k in names), pre
+        assert all(len(ks[k][1]) == 64 for k in names), pre        # the kernel descriptor
+    h8 = codeobj.family_sha256(capi.LIB_PATH, "k_sample", 8)
+    assert h8 == codeobj.family_sha256(capi.LIB_PATH, "k_sample", 8)
+    assert h8 != codeobj.family_sha256(capi.LIB_PATH, "k_sample", 16)
+    assert codeobj.family_of("k_sample_big<64, 2, 12, false>") == ("k_sample_big", 64)
+    assert codeobj.family_of("k_sample_quarter<8, 4, false>") == ("k_sample_quarter", 8)

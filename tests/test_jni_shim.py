@@ -80,7 +80,11 @@ def _write_input(path, K=8, V=30, D=12, seed=3):
 
 
 def _fake(*args):
-    assert os.path.exists(FAKE), "build() compiles tests/jni/bin/fake_env"
+    if not os.path.exists(FAKE):
+        # built by build() / `make -C integration/jni harness`, which links the
+        # HIP libraries: a checkout without the HIP build skips, as the gcc
+        # check above does without gcc
+        pytest.skip("tests/jni/bin/fake_env not built (build() / make -C integration/jni harness)")
     return subprocess.run([FAKE, *args], capture_output=True, text=True, timeout=60)
 
 

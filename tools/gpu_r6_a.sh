@@ -11,7 +11,7 @@ LDA_MI355X_LIB=variants/apick/liblda_mi355x.so timeout -k 10 400 python -u -m py
   --timeout-method thread -m gpu tests/test_parity_gpu.py -k "large_k or sparse" > $O/apick_parity.log 2>&1 \
   || { tail -20 $O/apick_parity.log; exit 1; }
 tail -1 $O/apick_parity.log
-bash tools/gpu_r5_c5ab.sh r6a 0 tree variants/apick/liblda_mi355x.so || exit 1
+bash tools/gpu_r5_c5ab.sh r6a 0 tree variants/apick/liblda_mi355x.so variants/nodelta/liblda_mi355x.so || exit 1
 # the C2 / C3 lines (tree), then the C4 profile passes on the shipped dense kernel
 for cfg in c2 c3; do
   timeout -k 10 300 python bench.py --config $cfg --no-cpu-baseline --no-estimate > $O/bench_$cfg.log 2>&1 || { tail -5 $O/bench_$cfg.log; exit 1; }
