@@ -27,6 +27,9 @@ timeout -k 10 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 
   || { tail -30 $O/bench_2ranks.log; exit 1; }
 grep '^{' $O/bench_2ranks.log | tail -1 > $O/bench_2ranks.jsonl
 python3 -c "import json;d=json.loads(open('$O/bench_2ranks.jsonl').read());print('2 ranks', round(d['value']/1e9,3), d['collective']['replicas_agree'], d['dropin_schedule'])"
+timeout -k 10 600 python bench.py > $O/bench_default.log 2>&1 || { tail -20 $O/bench_default.log; exit 1; }
+tail -n 1 $O/bench_default.log > $O/bench_default.jsonl
+python3 -c "import json;d=json.loads(open('$O/bench_default.jsonl').read());r=d['roofline'];print('default', round(d['value']/1e9,4), 'traffic', r['traffic'], 'issue', (r['issue'] or {}).get('frac'), 'dropin', d['dropin_schedule']['tokens_per_s']/1e9, 'cpu', d['cpu_baseline']['value'])"
 LDA_MI355X_LIB=variants/xcount/liblda_mi355x.so timeout -k 10 300 python tools/count_paths.py 300000 0 30 > $O/count_paths.jsonl 2> $O/count_paths.err \
   || { tail -20 $O/count_paths.err; exit 1; }
 cat $O/count_paths.jsonl
