@@ -1088,12 +1088,33 @@ static lda_status sample_part_impl(lda_ctx* c, int part) {
       c->big_ev_tag[probe] = ((int64_t)(r1 - r0) << 16) | ((int64_t)c->sweep_kind << 8) | part;
       HIP_TRY(hipEventRecord(c->big_ev[probe][0], c->stream));
     }
+#ifdef SB_X_DELTA_KERNEL
+    // measurement builds only (tools/build_variant.sh): the large-K sampler
+    // without its delta atomics, the changes made by k_delta_from_z from a
+    // copy of z taken before the pass (plain one-part sweeps of the whole shard)
+    static int32_t* zold = nullptr;
+    static int64_t zold_n = 0;
+    const bool dz = c->sampler == LDA_SAMPLER_SPARSE && c->C >= 32 && !seq && c->parts == 1 && !c->sweep_recount;
+    if (dz) {
+      if (zold_n < c->N) {
+        if (zold) HIP_TRY(hipFree(zold));
+        HIP_TRY(hipMalloc(&zold, sizeof(int32_t) * (size_t)c->N));
+        zold_n = c->N;
+      }
+      HIP_TRY(hipMemcpyAsync(zold, c->z, sizeof(int32_t) * (size_t)c->N, hipMemcpyDeviceToDevice, c->stream));
+    } else if (c->sampler == LDA_SAMPLER_SPARSE && c->C >= 32) {
+      return fail(LDA_ERR_UNSUPPORTED, "SB_X_DELTA_KERNEL build: plain one-part sweeps only");
+    }
+#endif
     if (c->sampler == LDA_SAMPLER_SPARSE)
       HIP_TRY(lda::launch_sample_sparse(c->C, false, p, blocks, c->stream, c->big_rb));
     else
       HIP_TRY(lda::launch_sample(c->C, false, p, blocks, c->stream, c->half));
     if (probe >= 0) HIP_TRY(hipEventRecord(c->big_ev[probe][1], c->stream));
     HIP_TRY(hipEventRecord(c->ev1[slot], c->stream));
+#ifdef SB_X_DELTA_KERNEL
+    if (dz) HIP_TRY(lda::launch_delta_from_z(c->words, zold, c->z, c->N, c->Kp, buf, c->stream));
+#endif
     if (c->sweep_recount) {
       // a split sweep: this part's rows recounted into its exchange buffer
       // (the apply left it zero; the parts' buffers sum to the counts); a

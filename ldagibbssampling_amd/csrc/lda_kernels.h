@@ -180,6 +180,10 @@ hipError_t launch_philox_draws(const int64_t* gtok, int64_t n, uint32_t c2, uint
                                uint32_t* out, hipStream_t st);
 hipError_t launch_init_z(int32_t* z, int64_t n, int32_t K, int64_t token_base, uint32_t k0,
                          uint32_t k1, hipStream_t st);
+#ifdef SB_X_DELTA_KERNEL
+hipError_t launch_delta_from_z(const int32_t* words, const int32_t* zold, const int32_t* z, int64_t n,
+                               int32_t Kp, int32_t* delta, hipStream_t st);
+#endif
 hipError_t launch_count(const int32_t* words, const int32_t* z, int64_t n, int32_t Kp,
                         int32_t* delta, int32_t* dsum, hipStream_t st);
 hipError_t launch_apply(int32_t* nw, int32_t* delta, int64_t n, hipStream_t st);

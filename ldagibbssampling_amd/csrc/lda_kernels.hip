@@ -2214,8 +2214,11 @@ __global__ __launch_bounds__(64 * sb_waves<C>()) void k_sample_big(SampleParams 
 
     // SB_X_NODELTA: attribution builds only (wrong counts): no delta atomics.
     // Not informative as run in round 6: without the changes the counts stay
-    // at their random start, the rows stay long and the sweep ran 2x slower
-#ifdef SB_X_NODELTA
+    // at their random start, the rows stay long and the sweep ran 2x slower.
+    // SB_X_DELTA_KERNEL: the same sampler with the count changes made right
+    // by k_delta_from_z after it (lda_capi.cpp), an A/B of where the atomics
+    // cost less (measurement builds only)
+#if defined(SB_X_NODELTA) || defined(SB_X_DELTA_KERNEL)
     constexpr bool kDelta = false;
 #else
     constexpr bool kDelta = !FROZEN;
@@ -3858,6 +3861,31 @@ hipError_t launch_count(const int32_t* words, const int32_t* z, int64_t n, int32
                      delta, dsum);
   return hipGetLastError();
 }
+
+#ifdef SB_X_DELTA_KERNEL
+// measurement builds only: a token's count change from its topic before
+// (zold) and after (z) the sampling pass, as the sampler's own atomics make it
+__global__ __launch_bounds__(256) void k_delta_from_z(const int32_t* __restrict__ words,
+                                                      const int32_t* __restrict__ zold,
+                                                      const int32_t* __restrict__ z, int64_t n, int32_t Kp,
+                                                      int32_t* __restrict__ delta) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    const int zo = zold[i], zn = z[i];
+    if (zo != zn) {
+      const int64_t rb = (int64_t)words[i] * Kp;
+      atomicAdd(delta + rb + zo, -1);
+      atomicAdd(delta + rb + zn, 1);
+    }
+  }
+}
+hipError_t launch_delta_from_z(const int32_t* words, const int32_t* zold, const int32_t* z, int64_t n,
+                               int32_t Kp, int32_t* delta, hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  const int blocks = (int)std::min<int64_t>((n + 255) / 256, 16384);
+  hipLaunchKernelGGL(k_delta_from_z, dim3(blocks), dim3(256), 0, st, words, zold, z, n, Kp, delta);
+  return hipGetLastError();
+}
+#endif
 
 hipError_t launch_apply(int32_t* nw, int32_t* delta, int64_t n, hipStream_t st) {
   const int64_t n4 = n / 4;

@@ -16,9 +16,9 @@ for lib in "$@"; do
   [ "$lib" = "tree" ] && n=tree
   for bi in 0 30; do
     if [ "$lib" = "tree" ]; then
-      timeout -k 10 600 python bench.py --config c5 --burnin $bi --no-cpu-baseline --no-estimate > $O/c5_${n}_b$bi.log 2>&1 || { echo "BENCH $n $bi FAILED"; tail -5 $O/c5_${n}_b$bi.log; exit 1; }
+      timeout -k 10 600 python bench.py --config c5 --burnin $bi --no-cpu-baseline --no-estimate --dropin-steps 0 > $O/c5_${n}_b$bi.log 2>&1 || { echo "BENCH $n $bi FAILED"; tail -5 $O/c5_${n}_b$bi.log; exit 1; }
     else
-      LDA_MI355X_LIB=$lib timeout -k 10 600 python bench.py --config c5 --burnin $bi --no-cpu-baseline --no-estimate > $O/c5_${n}_b$bi.log 2>&1 || { echo "BENCH $n $bi FAILED"; tail -5 $O/c5_${n}_b$bi.log; exit 1; }
+      LDA_MI355X_LIB=$lib timeout -k 10 600 python bench.py --config c5 --burnin $bi --no-cpu-baseline --no-estimate --dropin-steps 0 > $O/c5_${n}_b$bi.log 2>&1 || { echo "BENCH $n $bi FAILED"; tail -5 $O/c5_${n}_b$bi.log; exit 1; }
     fi
     python3 -c "import json;d=json.loads(open('$O/c5_${n}_b$bi.log').read().strip().splitlines()[-1]);r=d['roofline'];print('$n b$bi', round(d['value']/1e9,4),'Gtok/s kernel ms',round(r['kernel_ms_timed_region'],3),'frac',round(r['frac'],3))"
   done
