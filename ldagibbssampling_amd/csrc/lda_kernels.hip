@@ -2102,7 +2102,25 @@ __device__ __forceinline__ int wave_incl_scan_i(int x) {
   return x;
 }
 
+// SB_ND8 (measurement builds, round 6): the per-wave document counts as
+// bytes (documents of at most 255 tokens of one topic), 4 KiB per wave at
+// K = 4096 instead of 8 KiB, so that two 10-wave blocks (20 waves per CU,
+// with SB_WAVES 10 and SB_WPE 5) fit the 160 KiB of LDS
+#ifndef SB_ND8
+#define SB_ND8 0
+#endif
+#ifndef SB_WPE
+#define SB_WPE 0
+#endif
+#if SB_ND8 && !SB_APICK_LDS
+#error "SB_ND8 needs SB_APICK_LDS (the global-memory doc search reads 16-bit pairs)"
+#endif
+constexpr int kNdShift = SB_ND8 ? 2 : 1;     // counts per 32-bit LDS word: 4 or 2
+constexpr int kNdBits = SB_ND8 ? 8 : 16;
 __device__ __forceinline__ int nd16_get(const uint32_t* nd2, int k) {
+#if SB_ND8
+  return (int)reinterpret_cast<const uint8_t*>(nd2)[k];
+#endif
   return (int)reinterpret_cast<const uint16_t*>(nd2)[k];
 }
 
@@ -2130,7 +2148,12 @@ __device__ __forceinline__ int nd16_get(const uint32_t* nd2, int k) {
   (*reinterpret_cast<const volatile decltype(SampleParams::field)*>(                                  \
       (const char*)(__builtin_amdgcn_kernarg_segment_ptr()) + offsetof(SampleParams, field)))
 template <int C, int NS, int RB, bool FROZEN>
-__global__ __launch_bounds__(64 * sb_waves<C>()) void k_sample_big(SampleParams p) {
+#if SB_WPE
+#define SB_ATTR __attribute__((amdgpu_waves_per_eu(SB_WPE, SB_WPE)))
+#else
+#define SB_ATTR
+#endif
+__global__ __launch_bounds__(64 * sb_waves<C>()) SB_ATTR void k_sample_big(SampleParams p) {
   extern __shared__ __attribute__((aligned(16))) int32_t smem[];
   constexpr int KP = C * 64;
   constexpr int WB = sb_waves<C>();
@@ -2138,10 +2161,11 @@ __global__ __launch_bounds__(64 * sb_waves<C>()) void k_sample_big(SampleParams 
   const int lane = threadIdx.x & 63;
   const int wid = threadIdx.x >> 6;
   float2* tab = reinterpret_cast<float2*>(smem);                              // [KP] {inv, ainv}
-  uint32_t* nd2 = reinterpret_cast<uint32_t*>(smem + 2 * KP) + wid * (KP / 2); // [KP/2]
+  constexpr int NDW = KP >> kNdShift;                                          // LDS words of a wave's counts
+  uint32_t* nd2 = reinterpret_cast<uint32_t*>(smem + 2 * KP) + wid * NDW;      // [KP/2] (16-bit) or [KP/4]
 
   for (int i = threadIdx.x; i < KP; i += 64 * WB) tab[i] = p.big.tab[i];
-  for (int i = threadIdx.x; i < WB * (KP / 2); i += 64 * WB) smem[2 * KP + i] = 0;
+  for (int i = threadIdx.x; i < WB * NDW; i += 64 * WB) smem[2 * KP + i] = 0;
   __syncthreads();
 
   const int S = uniform_i(p.big.scal->S);
@@ -2237,7 +2261,11 @@ __global__ __launch_bounds__(64 * sb_waves<C>()) void k_sample_big(SampleParams 
       uint64_t rl = 0;
       for (int i = ts + lane; i < te; i += 64) {
         const int k = zr[i];
+#if SB_ND8
+        atomicAdd(&nd2[k >> 2], 1u << (8 * (k & 3)));
+#else
         atomicAdd(&nd2[k >> 1], (k & 1) ? 0x10000u : 1u);
+#endif
         rl += fixp(tab[k].x);
       }
       R = uniform_u64(wave_sum_u64(rl));
@@ -2245,8 +2273,8 @@ __global__ __launch_bounds__(64 * sb_waves<C>()) void k_sample_big(SampleParams 
     };
     auto clear_doc = [&]() {
 #pragma unroll
-      for (int j = 0; j < C / 2; j += 4)
-        *reinterpret_cast<uint4*>(nd2 + lane * (C / 2) + j) = make_uint4(0u, 0u, 0u, 0u);
+      for (int j = 0; j < NDW / 64; j += 4)
+        *reinterpret_cast<uint4*>(nd2 + lane * (NDW / 64) + j) = make_uint4(0u, 0u, 0u, 0u);
       wave_lds_fence();
     };
 
@@ -2359,10 +2387,17 @@ __global__ __launch_bounds__(64 * sb_waves<C>()) void k_sample_big(SampleParams 
           // fixed-point own-topic terms
           if (lane == 0) {
             const int pa = pk >= 0 ? pk : 0;
+#if SB_ND8
+            __hip_atomic_fetch_add(&nd2[pa >> 2], pk < 0 ? 0u : (1u << (8 * (pa & 3))), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_WAVEFRONT);
+            __hip_atomic_fetch_add(&nd2[zo >> 2], 0xFFFFFFFFu << (8 * (zo & 3)), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_WAVEFRONT);
+#else
             __hip_atomic_fetch_add(&nd2[pa >> 1], pk < 0 ? 0u : ((pa & 1) ? 0x10000u : 1u), __ATOMIC_RELAXED,
                                    __HIP_MEMORY_SCOPE_WAVEFRONT);
             __hip_atomic_fetch_add(&nd2[zo >> 1], (zo & 1) ? 0xFFFF0000u : 0xFFFFFFFFu, __ATOMIC_RELAXED,
                                    __HIP_MEMORY_SCOPE_WAVEFRONT);
+#endif
           }
           wave_lds_fence();
           // the own topic's count after both updates (a plain read behind the
@@ -2597,7 +2632,11 @@ __global__ __launch_bounds__(64 * sb_waves<C>()) void k_sample_big(SampleParams 
             // time); the own topic's F' = Fm1 added as a correction on its lane
             uint64_t ps = 0;
             {
+#if SB_ND8
+              const uint8_t* ndh = reinterpret_cast<const uint8_t*>(nd2) + C * lane;
+#else
               const uint16_t* ndh = reinterpret_cast<const uint16_t*>(nd2) + C * lane;
+#endif
               const float2* tl = tab + C * lane;
 #pragma unroll 8
               for (int j = 0; j < C; ++j) {
@@ -3712,7 +3751,7 @@ static int occupancy_sparse_t() {
 template <int C, int NS, int RB, bool FROZEN>
 static size_t sparse_big_lds() {
   // {alpha, inv} table + per-wave 16-bit nd pairs; > 64 KiB at C = 64
-  constexpr size_t lds = (2 * 64 * C + sb_waves<C>() * 32 * C) * sizeof(int32_t);
+  constexpr size_t lds = (2 * 64 * C + sb_waves<C>() * ((64 * C) >> kNdShift)) * sizeof(int32_t);
   static bool attr = [] {
     return hipFuncSetAttribute(reinterpret_cast<const void*>(&k_sample_big<C, NS, RB, FROZEN>),
                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) == hipSuccess;
