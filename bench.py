@@ -636,8 +636,16 @@ def main():
     total_tokens = tokens_all * args.steps
     value = total_tokens / elapsed
     ll = trainer.log_likelihood()
-    dropin = dropin_schedule(args, sampler, trainer, world, device, tokens_all) \
-        if args.dropin_steps > 0 else None
+    dropin = None
+    if args.dropin_steps > 0:
+        # a side figure: an error raised identically on every rank (the same
+        # call sequence everywhere) is reported in the line instead of
+        # dropping the main measurement above
+        try:
+            dropin = dropin_schedule(args, sampler, trainer, world, device, tokens_all)
+        except Exception as e:  # noqa: BLE001
+            print(f"dropin_schedule failed: {e!r}", file=sys.stderr)
+            dropin = {"error": repr(e)}
 
     if rank == 0:
         bpt = bytes_per_token(K)
