@@ -467,6 +467,9 @@ def main():
     ap.add_argument("--exchange-parts", type=int, default=None,
                     help="N > 1: split every sweep into P parts whose all-reduces overlap the "
                          "next part's sampling (default 1: DESIGN.md §5)")
+    ap.add_argument("--exchange-cells", type=int, default=2, choices=[2, 4],
+                    help="N > 1: cells per packed exchange word (lda_set_exchange_cells: 4 halves "
+                         "the bytes, more escapes; DESIGN.md §5)")
     ap.add_argument("--int32-exchange", action="store_true",
                     help="N > 1: all-reduce the int32 exchange buffer instead of the compact "
                          "packed form (A/B)")
@@ -580,6 +583,8 @@ def main():
         args.exchange_parts = 1
     if args.exchange_parts > 1:
         sampler.set_exchange_parts(args.exchange_parts, args.reserve_cus)
+    if args.exchange_cells != 2:
+        sampler.set_exchange_cells(args.exchange_cells)
     trainer = ADLDATrainer(sampler, sync_before_reduce=False, time_reduce=True,
                            compact=not args.int32_exchange,
                            exchange=True if args.force_exchange else None)
@@ -703,7 +708,7 @@ def main():
             # all-reduce 2 (W-1)/W M, all-gather (W-1)/W of the W lists
             link = 153e9
             model8 = (2 * 7 / 8 * xb["allreduce_bytes"] + 7 / 8 * xb["allgather_bytes"] * 8 / world) / link
-            coll = {"op": (("compact exchange (lda_exchange_pack: two cells per int32 word + escape "
+            coll = {"op": ((f"compact exchange (lda_exchange_pack: {sampler.exchange_cells} cells per int32 word + escape "
                             "lists): all_reduce(SUM, int32) of the packed words + all_gather of the "
                             "escape lists" + (" at their used length (after a MAX all_reduce of the "
                                               "counts; none gathered when no rank has one)"
@@ -715,6 +720,7 @@ def main():
                               f", for each of {parts} sweep parts, part i's overlapping part "
                               f"i+1's sampling")),
                     "compact": trainer.compact,
+                    "cells_per_word": sampler.exchange_cells if trainer.compact else None,
                     "exchange_parts": parts,
                     "reserve_cus": args.reserve_cus if parts > 1 else 0,
                     "bytes_per_sweep": nbytes * parts,

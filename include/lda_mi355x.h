@@ -227,6 +227,16 @@ lda_status lda_exchange_unpack(lda_ctx* ctx, int32_t part, int32_t world, int64_
  * is list_cap = capacity. */
 lda_status lda_exchange_unpack_lists(lda_ctx* ctx, int32_t part, int32_t world, int64_t max_shard_tokens,
                                      const void* escapes_all, int32_t list_cap);
+/* Cells per packed word (round 6): 2 (the default, above) or 4 -- cells
+ * 4i..4i+2 as d + 2^7/world in bits 0..7, 8..15, 16..23 and cell 4i+3 as
+ * d + 2^6/world in bits 24..30 (world <= 64), half the packed bytes of the
+ * default (C5 at 8 ranks: 1.07 GB instead of 2.15 GB per exchange) at the
+ * price of more escapes (a cell escapes beyond [-16, 16) at 8 ranks instead
+ * of [-2048, 2048)); the escape capacity of lda_exchange_sizes follows the
+ * smaller bias.  Every rank of a group must use the same value.  The result
+ * is the same int32 sum, bit for bit. */
+lda_status lda_set_exchange_cells(lda_ctx* ctx, int32_t cells_per_word);
+lda_status lda_get_exchange_cells(lda_ctx* ctx, int32_t* cells_per_word);
 /* Replica check (bench.py's multi-GPU line): a hash of the applied counts,
  * the sum mod 2^64 over the nonzero cells of nw (V x K) and nwsum (K) of
  * splitmix64's finaliser applied to (index << 32 | (uint32)value), index =
@@ -455,8 +465,9 @@ void lda_debug_fail_host_alloc(int32_t nth);
  * segments of the corpus (LDA_WARM_BLOCKS), lda_warm_part_tokens; 6 -- the
  * large-K sampler's draw (C >= 32: exact fixed-point doc part, own-entry
  * accept / re-draw), sequential sweeps recount under LDA_COUNT_RECOUNT,
- * lda_exchange_unpack_lists, lda_counts_checksum. */
-#define LDA_ABI_VERSION 6
+ * lda_exchange_unpack_lists, lda_counts_checksum; 7 -- lda_set_exchange_cells
+ * (four 8-bit cells per packed word). */
+#define LDA_ABI_VERSION 7
 const char* lda_version(void);
 int32_t lda_abi_version(void);
 

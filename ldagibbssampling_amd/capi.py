@@ -118,6 +118,8 @@ SIGNATURES = {
                                       C.POINTER(_vp)]),
     "lda_exchange_unpack": (C.c_int32, [_vp, C.c_int32, C.c_int32, C.c_int64, _vp]),
     "lda_exchange_unpack_lists": (C.c_int32, [_vp, C.c_int32, C.c_int32, C.c_int64, _vp, C.c_int32]),
+    "lda_set_exchange_cells": (C.c_int32, [_vp, C.c_int32]),
+    "lda_get_exchange_cells": (C.c_int32, [_vp, C.POINTER(C.c_int32)]),
     "lda_counts_checksum": (C.c_int32, [_vp, C.POINTER(C.c_uint64)]),
     "lda_set_sequential_sweeps": (C.c_int32, [_vp, C.c_int32, _vp, C.c_int64, C.c_int64]),
     "lda_get_sequential_sweeps": (C.c_int32, [_vp, C.POINTER(C.c_int32), _vp]),

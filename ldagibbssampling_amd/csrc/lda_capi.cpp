@@ -347,6 +347,7 @@ struct lda_ctx {
   int32_t* exch_packed[LDA_MAX_EXCHANGE_PARTS] = {};
   int32_t* exch_esc[LDA_MAX_EXCHANGE_PARTS] = {};
   size_t exch_esc_cap[LDA_MAX_EXCHANGE_PARTS] = {};
+  int32_t exch_cells = 2;          // cells per packed word: 2 (16-bit fields) or 4 (8-bit)
   int32_t* delta_part[LDA_MAX_EXCHANGE_PARTS] = {};
   std::vector<int64_t> part_range{0, 0};
   double* alpha_d = nullptr;
@@ -1239,14 +1240,19 @@ lda_status lda_delta_buffer_part(lda_ctx* c, int32_t part, void** dev_ptr, size_
 static lda_status exchange_dims(lda_ctx* c, int32_t world, int64_t max_tokens, size_t* packed_count,
                                 size_t* escape_count, int32_t* cap) {
   // world 1: the sum is the identity (a one-rank run with the exchange forced on, to exercise it)
-  if (world < 1 || world > 16384) return fail(LDA_ERR_INVALID_ARG, "world must be in [1, 16384]");
+  const int per = c->exch_cells;
+  const int max_world = per == 4 ? 64 : 16384;
+  if (world < 1 || world > max_world)
+    return fail(LDA_ERR_INVALID_ARG, per == 4 ? "world must be in [1, 64] with 4 cells per word"
+                                              : "world must be in [1, 16384]");
   if (max_tokens < c->N) return fail(LDA_ERR_INVALID_ARG, "max_shard_tokens below this shard's tokens");
   // sum |cell| of one rank's buffer <= 2 x its tokens, so at most that over
-  // the smaller bias can escape
-  const int64_t k = 2 * max_tokens / lda::exch_bias1(world) + 1;
+  // the smallest bias can escape
+  const int64_t bmin = per == 4 ? lda::exch_bias4_top(world) : lda::exch_bias1(world);
+  const int64_t k = 2 * max_tokens / bmin + 1;
   if (k > (int64_t)INT32_MAX / 3 - 1) return fail(LDA_ERR_UNSUPPORTED, "escape list beyond int32 indexing");
   *cap = (int32_t)k;
-  *packed_count = (size_t)c->V * c->Kp / 2 + c->Kp;
+  *packed_count = (size_t)c->V * c->Kp / per + c->Kp;
   *escape_count = 1 + 3 * (size_t)k;
   return LDA_OK;
 }
@@ -1255,6 +1261,32 @@ static lda_status exchange_dims(lda_ctx* c, int32_t world, int64_t max_tokens, s
 static int exchange_slot(lda_ctx* c, int32_t part) {
   const bool seq = c->next_part != 0 || c->pending ? c->sweep_seq : next_sweep_sequential(c);
   return seq ? 0 : part;
+}
+
+lda_status lda_set_exchange_cells(lda_ctx* c, int32_t cells_per_word) {
+  return lda_abi::guarded([&]() -> lda_status {
+  if (!c) return fail(LDA_ERR_INVALID_ARG, "null ctx");
+  if (cells_per_word != 2 && cells_per_word != 4) return fail(LDA_ERR_INVALID_ARG, "cells_per_word must be 2 or 4");
+  if (c->exch_cells != cells_per_word) {
+    // the packed words of a pending exchange have the old layout
+    for (int i = 0; i < LDA_MAX_EXCHANGE_PARTS; ++i)
+      if (c->exch_packed[i]) {
+        HIP_TRY(hipSetDevice(c->device));
+        HIP_TRY(hipFree(c->exch_packed[i]));
+        c->exch_packed[i] = nullptr;
+      }
+    c->exch_cells = cells_per_word;
+  }
+  return LDA_OK;
+  });
+}
+
+lda_status lda_get_exchange_cells(lda_ctx* c, int32_t* cells_per_word) {
+  return lda_abi::guarded([&]() -> lda_status {
+  if (!c || !cells_per_word) return fail(LDA_ERR_INVALID_ARG, "null argument");
+  *cells_per_word = c->exch_cells;
+  return LDA_OK;
+  });
 }
 
 lda_status lda_exchange_sizes(lda_ctx* c, int32_t world, int64_t max_shard_tokens, size_t* packed_count,
@@ -1290,8 +1322,9 @@ lda_status lda_exchange_pack(lda_ctx* c, int32_t part, int32_t world, int64_t ma
   int32_t* pk = c->exch_packed[slot];
   int32_t* es = c->exch_esc[slot];
   HIP_TRY(hipMemsetAsync(es, 0, sizeof(int32_t), c->stream));
-  HIP_TRY(lda::launch_exch_pack(buf, cells, pk, world, es, cap, c->stream));
-  HIP_TRY(hipMemcpyAsync(pk + cells / 2, buf + cells, sizeof(int32_t) * c->Kp, hipMemcpyDeviceToDevice, c->stream));
+  HIP_TRY(lda::launch_exch_pack(buf, cells, pk, world, es, cap, c->stream, c->exch_cells));
+  HIP_TRY(hipMemcpyAsync(pk + cells / c->exch_cells, buf + cells, sizeof(int32_t) * c->Kp,
+                         hipMemcpyDeviceToDevice, c->stream));
   *packed = pk;
   *escapes = es;
   return LDA_OK;
@@ -1328,10 +1361,11 @@ lda_status lda_exchange_unpack_lists(lda_ctx* c, int32_t part, int32_t world, in
   const int64_t cells = (int64_t)c->V * c->Kp;
   int32_t* buf = c->delta_part[slot];
   const int32_t* pk = c->exch_packed[slot];
-  HIP_TRY(hipMemcpyAsync(buf + cells, pk + cells / 2, sizeof(int32_t) * c->Kp, hipMemcpyDeviceToDevice, c->stream));
+  HIP_TRY(hipMemcpyAsync(buf + cells, pk + cells / c->exch_cells, sizeof(int32_t) * c->Kp,
+                         hipMemcpyDeviceToDevice, c->stream));
   HIP_TRY(lda::launch_exch_unpack(pk, cells, buf, world,
                                   list_cap > 0 ? static_cast<const int32_t*>(escapes_all) : nullptr, cap,
-                                  c->stream));
+                                  c->stream, c->exch_cells));
   return LDA_OK;
   });
 }

@@ -196,13 +196,18 @@ hipError_t launch_apply_cols(int32_t* nw, int32_t* delta, int64_t V, int32_t Kp,
 // biases b0 = 2^15 / world (bits 0..15) and b1 = 2^14 / world (bits 16..30)
 inline int32_t exch_bias0(int32_t world) { return 32768 / world; }
 inline int32_t exch_bias1(int32_t world) { return 16384 / world; }
-// cells: a multiple of 4; packed: cells / 2 words; esc: [1 + 3 cap] with esc[0] zeroed
+// ... or 4 cells per word (lda_set_exchange_cells 4, round 6): cells 4i..4i+2
+// biased by 2^7 / world in bits 0..7, 8..15, 16..23, cell 4i+3 by 2^6 / world
+// in bits 24..30 (world <= 64)
+inline int32_t exch_bias4(int32_t world) { return 128 / world; }
+inline int32_t exch_bias4_top(int32_t world) { return 64 / world; }
+// cells: a multiple of 4; packed: cells / per_word words; esc: [1 + 3 cap] with esc[0] zeroed
 hipError_t launch_exch_pack(const int32_t* buf, int64_t cells, int32_t* packed, int32_t world,
-                            int32_t* esc, int32_t cap, hipStream_t st);
+                            int32_t* esc, int32_t cap, hipStream_t st, int32_t per_word = 2);
 // buf[cells] = the unpacked sum, then + every rank's escapes (esc_all: world x
 // [1 + 3 cap]; nullptr: none)
 hipError_t launch_exch_unpack(const int32_t* packed, int64_t cells, int32_t* buf, int32_t world,
-                              const int32_t* esc_all, int32_t cap, hipStream_t st);
+                              const int32_t* esc_all, int32_t cap, hipStream_t st, int32_t per_word = 2);
 // one uint64 partial per block of the nw / nwsum hash (lda_counts_checksum)
 hipError_t launch_counts_checksum(const int32_t* nw, const int32_t* nwsum, int32_t K, int32_t Kp, int64_t V,
                                   uint64_t* partial, int blocks, hipStream_t st);

@@ -3065,6 +3065,29 @@ __global__ __launch_bounds__(256) void k_exch_pack(const int4* __restrict__ buf,
   }
 }
 
+// four cells per word (lda_set_exchange_cells 4): cells 0..2 of an int4 in
+// bytes 0..2 biased by b, cell 3 in bits 24..30 biased by bt (the sum over
+// `world` ranks of values below 2 b stays below 2^8 in each low byte and below
+// 2^7 in the top one: no carry between cells, no int32 overflow)
+__global__ __launch_bounds__(256) void k_exch_pack4(const int4* __restrict__ buf, int64_t n4,
+                                                    uint32_t* __restrict__ packed, int32_t b, int32_t bt,
+                                                    int32_t* __restrict__ esc, int32_t cap) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += (int64_t)gridDim.x * 256) {
+    const int4 d = buf[i];
+    const int64_t c = 4 * i;
+    packed[i] = exch_field(d.x, b, c, esc, cap) | (exch_field(d.y, b, c + 1, esc, cap) << 8) |
+                (exch_field(d.z, b, c + 2, esc, cap) << 16) | (exch_field(d.w, bt, c + 3, esc, cap) << 24);
+  }
+}
+__global__ __launch_bounds__(256) void k_exch_unpack4(const uint32_t* __restrict__ packed, int64_t n4,
+                                                      int4* __restrict__ buf, int32_t wb, int32_t wbt) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += (int64_t)gridDim.x * 256) {
+    const uint32_t p = packed[i];
+    buf[i] = make_int4((int32_t)(p & 0xFFu) - wb, (int32_t)((p >> 8) & 0xFFu) - wb,
+                       (int32_t)((p >> 16) & 0xFFu) - wb, (int32_t)(p >> 24) - wbt);
+  }
+}
+
 // the summed words back into int32 cells (every cell written: the buffer
 // held this rank's own changes before the exchange)
 __global__ __launch_bounds__(256) void k_exch_unpack(const uint2* __restrict__ packed, int64_t n4,
@@ -3980,22 +4003,31 @@ hipError_t launch_apply_build(int32_t* nw, int32_t* delta, int64_t V, int32_t Kp
 }
 
 hipError_t launch_exch_pack(const int32_t* buf, int64_t cells, int32_t* packed, int32_t world,
-                            int32_t* esc, int32_t cap, hipStream_t st) {
+                            int32_t* esc, int32_t cap, hipStream_t st, int32_t per_word) {
   const int64_t n4 = cells / 4;
   if (n4 <= 0) return hipSuccess;
   const int blocks = (int)std::min<int64_t>((n4 + 255) / 256, 8192);
-  hipLaunchKernelGGL(k_exch_pack, dim3(blocks), dim3(256), 0, st, reinterpret_cast<const int4*>(buf), n4,
-                     reinterpret_cast<uint2*>(packed), exch_bias0(world), exch_bias1(world), esc, cap);
+  if (per_word == 4)
+    hipLaunchKernelGGL(k_exch_pack4, dim3(blocks), dim3(256), 0, st, reinterpret_cast<const int4*>(buf), n4,
+                       reinterpret_cast<uint32_t*>(packed), exch_bias4(world), exch_bias4_top(world), esc, cap);
+  else
+    hipLaunchKernelGGL(k_exch_pack, dim3(blocks), dim3(256), 0, st, reinterpret_cast<const int4*>(buf), n4,
+                       reinterpret_cast<uint2*>(packed), exch_bias0(world), exch_bias1(world), esc, cap);
   return hipGetLastError();
 }
 
 hipError_t launch_exch_unpack(const int32_t* packed, int64_t cells, int32_t* buf, int32_t world,
-                              const int32_t* esc_all, int32_t cap, hipStream_t st) {
+                              const int32_t* esc_all, int32_t cap, hipStream_t st, int32_t per_word) {
   const int64_t n4 = cells / 4;
   if (n4 > 0) {
     const int blocks = (int)std::min<int64_t>((n4 + 255) / 256, 8192);
-    hipLaunchKernelGGL(k_exch_unpack, dim3(blocks), dim3(256), 0, st, reinterpret_cast<const uint2*>(packed),
-                       n4, reinterpret_cast<int4*>(buf), world * exch_bias0(world), world * exch_bias1(world));
+    if (per_word == 4)
+      hipLaunchKernelGGL(k_exch_unpack4, dim3(blocks), dim3(256), 0, st, reinterpret_cast<const uint32_t*>(packed),
+                         n4, reinterpret_cast<int4*>(buf), world * exch_bias4(world),
+                         world * exch_bias4_top(world));
+    else
+      hipLaunchKernelGGL(k_exch_unpack, dim3(blocks), dim3(256), 0, st, reinterpret_cast<const uint2*>(packed),
+                         n4, reinterpret_cast<int4*>(buf), world * exch_bias0(world), world * exch_bias1(world));
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
   }

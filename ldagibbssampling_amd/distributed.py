@@ -180,8 +180,11 @@ class ADLDATrainer:
         import torch
         n = esc.numel() if n is None else n
         buf = self._esc_all.get(part)
-        if buf is None or buf.numel() < self.world * esc.numel() or buf.device != esc.device:
-            buf = torch.empty(self.world * esc.numel(), dtype=esc.dtype, device=esc.device)
+        # sized by what is gathered, not by the lists' capacity (with four
+        # cells per word a C5 rank's capacity is 750 MB: world copies of it
+        # would be 6 GB for lists that are normally short)
+        if buf is None or buf.numel() < self.world * n or buf.device != esc.device:
+            buf = torch.empty(self.world * n, dtype=esc.dtype, device=esc.device)
             self._esc_all[part] = buf
         return buf[:self.world * n]
 

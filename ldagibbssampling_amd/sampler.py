@@ -140,6 +140,17 @@ class GibbsSampler:
                                               C.byref(b)), "lda_exchange_sizes")
         return int(a.value), int(b.value)
 
+    def set_exchange_cells(self, cells_per_word: int):
+        """lda_set_exchange_cells: 2 (default) or 4 cells per packed exchange
+        word (half the bytes, narrower fields, more escapes)."""
+        capi.check(self._L.lda_set_exchange_cells(self._h, int(cells_per_word)), "lda_set_exchange_cells")
+
+    @property
+    def exchange_cells(self) -> int:
+        n = C.c_int32()
+        capi.check(self._L.lda_get_exchange_cells(self._h, C.byref(n)), "lda_get_exchange_cells")
+        return int(n.value)
+
     def exchange_pack(self, part: int, world: int, max_tokens: int):
         """Pack part `part`'s exchange buffer (lda_exchange_pack, on this
         context's stream): zero-copy torch int32 views (packed words to

@@ -490,35 +490,43 @@ def doc_completion_loglik(K, V, nw, nwsum, beta, theta, doc_off, words) -> float
 
 
 # ------------------------------------------------ compact exchange (checker)
-def exchange_biases(world: int):
-    """lda_kernels.h exch_bias0 / exch_bias1."""
+def exchange_biases(world: int, cells: int = 2):
+    """Per-field biases of the packed word: lda_kernels.h exch_bias0 /
+    exch_bias1 (2 cells per word), or exch_bias4 x 3 + exch_bias4_top
+    (4 cells per word, lda_set_exchange_cells)."""
+    if cells == 4:
+        return (128 // world,) * 3 + (64 // world,)
     return 32768 // world, 16384 // world
 
 
-def exchange_cap(world: int, max_tokens: int) -> int:
-    """lda_capi.cpp exchange_dims: escapes per rank <= 2 N / b1 (+1)."""
-    return 2 * int(max_tokens) // exchange_biases(world)[1] + 1
+def _field_shifts(cells: int):
+    return (0, 8, 16, 24) if cells == 4 else (0, 16)
 
 
-def exchange_pack(buf, world: int, Kp: int, max_tokens: int):
-    """Numpy restatement of lda_exchange_pack (k_exch_pack): buf int32
-    [cells | Kp] -> (packed int32 [cells/2 | Kp], escapes int32 [1 + 3 cap]).
-    Escapes are listed in cell order here (the GPU's order is scheduling-
-    dependent; the sum they produce is not)."""
-    b0, b1 = exchange_biases(world)
-    cap = exchange_cap(world, max_tokens)
+def exchange_cap(world: int, max_tokens: int, cells: int = 2) -> int:
+    """lda_capi.cpp exchange_dims: escapes per rank <= 2 N / (smallest bias) (+1)."""
+    return 2 * int(max_tokens) // min(exchange_biases(world, cells)) + 1
+
+
+def exchange_pack(buf, world: int, Kp: int, max_tokens: int, cells: int = 2):
+    """Numpy restatement of lda_exchange_pack (k_exch_pack, k_exch_pack4):
+    buf int32 [V Kp | Kp] -> (packed int32 [V Kp / cells | Kp], escapes
+    int32 [1 + 3 cap]).  Escapes are listed in cell order here (the GPU's
+    order is scheduling-dependent; the sum they produce is not)."""
+    bs = exchange_biases(world, cells)
+    cap = exchange_cap(world, max_tokens, cells)
     buf = np.asarray(buf, dtype=np.int64)
-    cells = buf.size - Kp
-    d = buf[:cells].reshape(-1, 2)
-    lo, hi = d[:, 0], d[:, 1]
-    esc_lo = (lo < -b0) | (lo >= b0)
-    esc_hi = (hi < -b1) | (hi >= b1)
-    f0 = np.where(esc_lo, b0, lo + b0)
-    f1 = np.where(esc_hi, b1, hi + b1)
-    packed = np.empty(cells // 2 + Kp, dtype=np.int64)
-    packed[:cells // 2] = f0 + (f1 << 16)
-    packed[cells // 2:] = buf[cells:]
-    idx = np.flatnonzero(np.stack([esc_lo, esc_hi], axis=1).reshape(-1))
+    n = buf.size - Kp
+    d = buf[:n].reshape(-1, cells)
+    packed = np.zeros(n // cells + Kp, dtype=np.int64)
+    escs = []
+    for j, (b, sh) in enumerate(zip(bs, _field_shifts(cells))):
+        x = d[:, j]
+        e = (x < -b) | (x >= b)
+        packed[:n // cells] += np.where(e, b, x + b) << sh
+        escs.append(e)
+    packed[n // cells:] = buf[n:]
+    idx = np.flatnonzero(np.stack(escs, axis=1).reshape(-1))
     assert len(idx) <= cap, "escape bound violated"
     esc = np.zeros(1 + 3 * cap, dtype=np.int64)
     esc[0] = len(idx)
@@ -529,14 +537,15 @@ def exchange_pack(buf, world: int, Kp: int, max_tokens: int):
     return packed.astype(np.int32), esc.astype(np.int32)
 
 
-def exchange_unpack(packed_sum, escapes_all, world: int, Kp: int, max_tokens: int, list_cap=None):
-    """lda_exchange_unpack: the summed packed words (int32 [cells/2 | Kp]) and
-    every rank's escape list (world x [1 + 3 cap], rank order) -> the int32
-    sum of the ranks' buffers [cells | Kp].  list_cap: the lists were sent at
-    1 + 3 list_cap int32 each (lda_exchange_unpack_lists; 0 and escapes_all
-    None: no rank had an escape)."""
-    b0, b1 = exchange_biases(world)
-    cap = exchange_cap(world, max_tokens)
+def exchange_unpack(packed_sum, escapes_all, world: int, Kp: int, max_tokens: int, list_cap=None,
+                    cells: int = 2):
+    """lda_exchange_unpack: the summed packed words (int32 [V Kp / cells |
+    Kp]) and every rank's escape list (world x [1 + 3 cap], rank order) ->
+    the int32 sum of the ranks' buffers [V Kp | Kp].  list_cap: the lists were
+    sent at 1 + 3 list_cap int32 each (lda_exchange_unpack_lists; 0 and
+    escapes_all None: no rank had an escape)."""
+    bs = exchange_biases(world, cells)
+    cap = exchange_cap(world, max_tokens, cells)
     if list_cap is not None:
         assert 0 <= list_cap <= cap
         cap = int(list_cap)
@@ -544,11 +553,12 @@ def exchange_unpack(packed_sum, escapes_all, world: int, Kp: int, max_tokens: in
             assert cap == 0
             escapes_all = np.zeros(world, dtype=np.int32)
     p = np.asarray(packed_sum, dtype=np.int64) & 0xFFFFFFFF
-    half = p.size - Kp
-    out = np.empty(2 * half + Kp, dtype=np.int64)
-    out[0:2 * half:2] = (p[:half] & 0xFFFF) - world * b0
-    out[1:2 * half:2] = (p[:half] >> 16) - world * b1
-    out[2 * half:] = np.asarray(packed_sum[half:], dtype=np.int64)
+    words = p.size - Kp
+    out = np.empty(cells * words + Kp, dtype=np.int64)
+    width = 32 // cells
+    for j, (b, sh) in enumerate(zip(bs, _field_shifts(cells))):
+        out[j:cells * words:cells] = ((p[:words] >> sh) & ((1 << width) - 1)) - world * b
+    out[cells * words:] = np.asarray(packed_sum[words:], dtype=np.int64)
     ea = np.asarray(escapes_all, dtype=np.int64).reshape(world, 1 + 3 * cap)
     for r in range(world):
         n = min(int(ea[r, 0]), cap)

@@ -37,7 +37,10 @@ class OracleEngine:
     def log_likelihood_parts(self):
         return self.s.log_likelihood_parts()
 
-    # the compact exchange (lda_exchange_pack / _unpack) restated in numpy
+    # the compact exchange (lda_exchange_pack / _unpack) restated in numpy;
+    # cells: lda_set_exchange_cells (2 or 4 cells per packed word)
+    cells = 2
+
     @property
     def N(self):
         return self.s.N
@@ -47,11 +50,12 @@ class OracleEngine:
 
     def exchange_sizes(self, world, max_tokens):
         from oracle import oracle as O
-        return self.s.V * self.s.Kp // 2 + self.s.Kp, 1 + 3 * O.exchange_cap(world, max_tokens)
+        return (self.s.V * self.s.Kp // self.cells + self.s.Kp,
+                1 + 3 * O.exchange_cap(world, max_tokens, self.cells))
 
     def exchange_pack(self, part, world, max_tokens):
         from oracle import oracle as O
-        pk, es = O.exchange_pack(self._buf(part), world, self.s.Kp, max_tokens)
+        pk, es = O.exchange_pack(self._buf(part), world, self.s.Kp, max_tokens, cells=self.cells)
         self._packed = getattr(self, "_packed", {})
         self._packed[part] = torch.from_numpy(pk)
         return self._packed[part], torch.from_numpy(es)
@@ -61,7 +65,7 @@ class OracleEngine:
         self.unpacked_lists = getattr(self, "unpacked_lists", []) + [list_cap]
         self._buf(part)[:] = O.exchange_unpack(self._packed[part].numpy(),
                                                None if escapes_all is None else escapes_all.numpy(), world,
-                                               self.s.Kp, max_tokens, list_cap=list_cap)
+                                               self.s.Kp, max_tokens, list_cap=list_cap, cells=self.cells)
 
     def counts_checksum(self):
         from oracle import oracle as O
@@ -154,7 +158,7 @@ def _hot_corpus():
     return np.arange(D + 1, dtype=np.int64) * L, words, z0, 200
 
 
-def _worker(rank, world, port, outdir, parts=1, compact=True, escape_lists="used", corpus="plain"):
+def _worker(rank, world, port, outdir, parts=1, compact=True, escape_lists="used", corpus="plain", cells=2):
     sys.path.insert(0, ROOT)
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -175,6 +179,7 @@ def _worker(rank, world, port, outdir, parts=1, compact=True, escape_lists="used
         eng = WarmOracleEngine(o)
     else:
         eng = OracleEngine(o) if parts == 1 else SplitOracleEngine(o, parts)
+    eng.cells = cells
     if corpus == "corrupt" and rank == world - 1:
         eng.counts_checksum = lambda: 12345             # a replica that differs
     tr = ADLDATrainer(eng, compact=compact, escape_lists=escape_lists)
@@ -240,23 +245,30 @@ def test_gloo_adlda_matches_single(oracle, world, parts, compact):
         np.testing.assert_array_equal(r["secs"], 0.5 + np.arange(world))
 
 
-def _run(world, parts=1, compact=True, escape_lists="used", corpus="plain"):
+def _run(world, parts=1, compact=True, escape_lists="used", corpus="plain", cells=2):
     with tempfile.TemporaryDirectory() as d:
-        mp.start_processes(_worker, args=(world, _free_port(), d, parts, compact, escape_lists, corpus),
+        mp.start_processes(_worker, args=(world, _free_port(), d, parts, compact, escape_lists, corpus, cells),
                            nprocs=world, start_method="spawn")
         return [dict(np.load(os.path.join(d, f"r{r}.npz"))) for r in range(world)]
 
 
-@pytest.mark.parametrize("world,parts,escape_lists", [(2, 1, "used"), (3, 1, "used"), (3, 2, "used"),
-                                                      (2, 1, "capacity")])
-def test_gloo_escape_lists(oracle, world, parts, escape_lists):
+@pytest.mark.parametrize("world,parts,escape_lists,cells", [(2, 1, "used", 2), (3, 1, "used", 2),
+                                                            (3, 2, "used", 2), (2, 1, "capacity", 2),
+                                                            (2, 1, "used", 4), (3, 2, "used", 4),
+                                                            (3, "steady", "used", 4)])
+def test_gloo_escape_lists(oracle, world, parts, escape_lists, cells):
     """A corpus whose first exchange has escapes (cells beyond 2^14/world):
     "used" all-gathers the lists at the MAX-reduced count (lda_exchange_
     unpack_lists; list_cap 0 without escapes, when nothing is gathered),
-    "capacity" the whole lists; both give the single-process run."""
-    res = _run(world, parts, True, escape_lists, "hot")
+    "capacity" the whole lists; both give the single-process run.  cells 4:
+    four 8-bit cells per packed word (lda_set_exchange_cells), whose narrow
+    fields send escapes in later sweeps too."""
+    res = _run(world, parts, True, escape_lists, "hot", cells)
     doc_off, words, z0, V = _hot_corpus()
     single = oracle.ExactSampler(K, V, doc_off, words, 0.1, 0.01, SEED, z_init=z0)
+    if parts == "steady":
+        single.set_warm_start(*WARM)
+        single.set_sequential_sweeps(*oracle.staleness_schedule(4))
     single.sweep(SWEEPS)
     np.testing.assert_array_equal(np.concatenate([r["z"] for r in res]), single.z())
     nw, nwsum, _, _ = single.counts()
@@ -265,9 +277,12 @@ def test_gloo_escape_lists(oracle, world, parts, escape_lists):
         np.testing.assert_array_equal(r["nwsum"], nwsum)
         assert bool(r["agree"])
         lists = r["lists"]
-        if escape_lists == "used":
+        if escape_lists == "used" and cells == 2:
             assert lists[0] >= 1                     # the initial counts' escapes, at their count
             assert (lists[1:] == 0).all()            # later deltas: none, nothing gathered
+            assert "'escape_lists': 'used'" in str(r["xb"])
+        elif escape_lists == "used":
+            assert lists[0] >= 1 and (lists[1:] >= 0).all()
             assert "'escape_lists': 'used'" in str(r["xb"])
         else:
             assert (lists == -1).all()

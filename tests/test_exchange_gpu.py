@@ -84,9 +84,11 @@ def test_split_sweep_ordering_rules(oracle):
     np.testing.assert_array_equal(g.z(), o.z())
 
 
-@pytest.mark.parametrize("world,kind,K", [(2, "dense", 4), (4, "dense", 20), (8, "dense", 4),
-                                          (3, "sparse", 1500), (8, "sparse", 4096)])
-def test_compact_exchange_bit_exact(oracle, world, kind, K):
+@pytest.mark.parametrize("world,kind,K,cells", [(2, "dense", 4, 2), (4, "dense", 20, 2), (8, "dense", 4, 2),
+                                                (3, "sparse", 1500, 2), (8, "sparse", 4096, 2),
+                                                (2, "dense", 4, 4), (8, "dense", 20, 4),
+                                                (3, "sparse", 1500, 4), (8, "sparse", 4096, 4)])
+def test_compact_exchange_bit_exact(oracle, world, kind, K, cells):
     """lda_exchange_pack / lda_exchange_unpack on `world`
     shards held in one process on one GPU: the packed words summed across the
     shards (torch, in place of RCCL) plus every shard's all-gathered escape
@@ -97,7 +99,8 @@ def test_compact_exchange_bit_exact(oracle, world, kind, K):
     2^14/world, so escapes occur in both halves of a word.
     The packed words and escape lists match the numpy restatement
     (oracle.exchange_pack) up to the escapes' order, which the GPU's atomic
-    appends leave open."""
+    appends leave open.  cells 4: four 8-bit cells per word
+    (lda_set_exchange_cells; biases 2^7/world and 2^6/world)."""
     import torch
     from ldagibbssampling_amd.distributed import shard_corpus
     from ldagibbssampling_amd.sampler import GibbsSampler
@@ -113,6 +116,9 @@ def test_compact_exchange_bit_exact(oracle, world, kind, K):
     gs = [GibbsSampler(K, 500, sh.doc_off, sh.words, np.full(K, 0.1), 0.01, seed=5,
                        token_base=sh.token_base, sampler=kind,
                        z_init=z0[sh.token_base:sh.token_base + len(sh.words)]) for sh in shards]
+    for g in gs:
+        g.set_exchange_cells(cells)
+        assert g.exchange_cells == cells
     N = max(g.N for g in gs)
     before = [g.delta_tensor().clone() for g in gs]
     want = torch.stack([b.to(torch.int64) for b in before]).sum(0).to(torch.int32)
@@ -122,7 +128,7 @@ def test_compact_exchange_bit_exact(oracle, world, kind, K):
     assert min(n_esc) >= 2          # topic 0 (low half) and topic 1 (high half) of the hot word
     Kp = gs[0].Kp
     for (pk, es), b in zip(packs, before):
-        opk, oes = oracle.exchange_pack(b.cpu().numpy(), world, Kp, N)
+        opk, oes = oracle.exchange_pack(b.cpu().numpy(), world, Kp, N, cells=cells)
         np.testing.assert_array_equal(pk.cpu().numpy(), opk)
         n = int(oes[0])
         assert int(es[0]) == n
@@ -131,6 +137,7 @@ def test_compact_exchange_bit_exact(oracle, world, kind, K):
         np.testing.assert_array_equal(got[np.lexsort(got.T[::-1])], ref[np.lexsort(ref.T[::-1])])
     total = torch.stack([pk.to(torch.int64) for pk, _ in packs]).sum(0)
     assert int(total.max()) < 2 ** 31
+    assert pk.numel() == gs[0].V * Kp // cells + Kp
     esc_all = torch.cat([es for _, es in packs])
     # odd shards unpack the lists sent at their used length (lda_exchange_
     # unpack_lists, what ADLDATrainer's escape_lists="used" all-gathers)
