@@ -467,9 +467,10 @@ def main():
     ap.add_argument("--exchange-parts", type=int, default=None,
                     help="N > 1: split every sweep into P parts whose all-reduces overlap the "
                          "next part's sampling (default 1: DESIGN.md §5)")
-    ap.add_argument("--exchange-cells", type=int, default=2, choices=[2, 4],
+    ap.add_argument("--exchange-cells", type=int, default=None, choices=[2, 4],
                     help="N > 1: cells per packed exchange word (lda_set_exchange_cells: 4 halves "
-                         "the bytes, more escapes; DESIGN.md §5)")
+                         "the bytes, more escapes; default: ADLDATrainer's choice, 4 for K > 1024; "
+                         "DESIGN.md §5)")
     ap.add_argument("--int32-exchange", action="store_true",
                     help="N > 1: all-reduce the int32 exchange buffer instead of the compact "
                          "packed form (A/B)")
@@ -583,11 +584,10 @@ def main():
         args.exchange_parts = 1
     if args.exchange_parts > 1:
         sampler.set_exchange_parts(args.exchange_parts, args.reserve_cus)
-    if args.exchange_cells != 2:
-        sampler.set_exchange_cells(args.exchange_cells)
     trainer = ADLDATrainer(sampler, sync_before_reduce=False, time_reduce=True,
                            compact=not args.int32_exchange,
-                           exchange=True if args.force_exchange else None)
+                           exchange=True if args.force_exchange else None,
+                           cells_per_word=args.exchange_cells)
     trainer.init_counts()
 
     def step():

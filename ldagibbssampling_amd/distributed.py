@@ -47,6 +47,11 @@ from dataclasses import dataclass
 import numpy as np
 
 
+# the compact exchange's four-cells-per-word default starts at this padded K
+# (the large-K sampler's C >= 32 tables)
+LARGE_K_CELLS4 = 2048
+
+
 @dataclass
 class Shard:
     rank: int
@@ -85,7 +90,7 @@ class ADLDATrainer:
 
     def __init__(self, engine, group=None, sync_before_reduce: bool = True,
                  time_reduce: bool = False, compact: bool = True, exchange=None,
-                 escape_lists: str = "used"):
+                 escape_lists: str = "used", cells_per_word=None):
         """sync_before_reduce=False when the engine already launches on the
         stream the collective runs behind (GibbsSampler.set_stream(torch's
         current stream)): then no host synchronisation per sweep is needed.
@@ -98,7 +103,14 @@ class ADLDATrainer:
         identity (tests/test_distributed_gpu.py).
         escape_lists: "used" (all-gather the escape lists at their used
         length, after a MAX all-reduce of the counts) or "capacity" (the
-        whole fixed-capacity lists)."""
+        whole fixed-capacity lists).
+        cells_per_word: cells per packed word of the compact exchange
+        (lda_set_exchange_cells): 2 or 4; None picks 4 for the large-K
+        sampler's tables (Kp >= LARGE_K_CELLS4, C5: 1.07 GB instead of 2.15 GB
+        per exchange, ~1e5 escapes per rank per sweep at 8 ranks,
+        profiles/r06/exchange/) when the lists travel at their used length,
+        else 2 (C4: the narrower fields escape about as many bytes as they
+        save)."""
         import torch.distributed as dist
 
         if escape_lists not in ("used", "capacity"):
@@ -123,6 +135,11 @@ class ADLDATrainer:
         # the compact exchange needs engine.exchange_pack / exchange_unpack and
         # the largest shard's tokens (every rank sizes its escape list alike)
         self.compact = bool(compact and self.exchange and hasattr(engine, "exchange_pack"))
+        if self.compact and hasattr(engine, "set_exchange_cells"):
+            if cells_per_word is None:
+                cells_per_word = 4 if (escape_lists == "used" and self.world <= 64 and
+                                       int(getattr(engine, "Kp", 0)) >= LARGE_K_CELLS4) else 2
+            engine.set_exchange_cells(int(cells_per_word))
         self._esc_all = {}
         self.max_tokens = self._max_tokens() if self.compact else 0
         if self.exchange and not sync_before_reduce:

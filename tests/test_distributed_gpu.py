@@ -174,7 +174,7 @@ def test_default_mode_waits_for_async_collective(compact):
     assert int(g.delta_tensor().abs().sum()) == 0      # nothing landed after the apply
 
 
-def _rccl_worker(rank, port, outdir, stream_ordered, parts, compact):
+def _rccl_worker(rank, port, outdir, stream_ordered, parts, compact, k=None, kind="dense"):
     sys.path.insert(0, ROOT)
     import torch
     import torch.distributed as dist
@@ -184,7 +184,7 @@ def _rccl_worker(rank, port, outdir, stream_ordered, parts, compact):
     from ldagibbssampling_amd.distributed import ADLDATrainer
     from ldagibbssampling_amd.sampler import GibbsSampler
     c = _corpus()
-    g = GibbsSampler(K, c.num_types, c.doc_off, c.words, 0.1, 0.01, seed=SEED)
+    g = GibbsSampler(k or K, c.num_types, c.doc_off, c.words, 0.1, 0.01, seed=SEED, sampler=kind)
     if parts > 1:
         g.set_exchange_parts(parts, reserve_cus=8)
     if stream_ordered:
@@ -202,14 +202,15 @@ def _rccl_worker(rank, port, outdir, stream_ordered, parts, compact):
     assert chk["replicas_agree"] and chk["ranks_counted"] == 1 and chk["rank_seconds"] == [0.25]
     nw, nwsum, _, _ = g.counts()
     np.savez(os.path.join(outdir, "r0.npz"), z=g.z(), nw=nw, nwsum=nwsum, ll=ll,
-             bytes=tr.exchange_bytes()["allreduce_bytes"])
+             bytes=tr.exchange_bytes()["allreduce_bytes"], cells=g.exchange_cells, kp=g.Kp)
     g.close()
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("stream_ordered,parts,compact", [(True, 1, True), (False, 1, True), (True, 2, True),
-                                                          (True, 1, False)])
-def test_rccl_exchange_one_rank(oracle, stream_ordered, parts, compact):
+@pytest.mark.parametrize("stream_ordered,parts,compact,k,kind", [
+    (True, 1, True, None, "dense"), (False, 1, True, None, "dense"), (True, 2, True, None, "dense"),
+    (True, 1, False, None, "dense"), (True, 1, True, 2048, "sparse"), (True, 2, True, 2048, "sparse")])
+def test_rccl_exchange_one_rank(oracle, stream_ordered, parts, compact, k, kind):
     """The RCCL path bench.py takes at N > 1 (torch.distributed "nccl"),
     exercised on the one-GPU box with one rank and the exchange forced on:
     process-group init on the device, the in-place SUM all-reduce of the
@@ -217,25 +218,30 @@ def test_rccl_exchange_one_rank(oracle, stream_ordered, parts, compact):
     the pack / unpack kernels, stream-ordered and host-synchronised, split
     sweeps.  One rank's sum is the identity, so the chain must equal the
     oracle bit for bit -- a wrong stream order, size or dtype at the RCCL
-    boundary shows up as a difference."""
+    boundary shows up as a difference.  k = 2048 (the large-K sampler): the
+    trainer's default exchange packs four cells per word."""
     import socket
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
     port = s.getsockname()[1]
     s.close()
     with tempfile.TemporaryDirectory() as d:
-        mp.start_processes(_rccl_worker, args=(port, d, stream_ordered, parts, compact), nprocs=1,
+        mp.start_processes(_rccl_worker, args=(port, d, stream_ordered, parts, compact, k, kind), nprocs=1,
                            start_method="spawn")
         r = np.load(os.path.join(d, "r0.npz"))
     c = _corpus()
-    o = oracle.ExactSampler(K, c.num_types, c.doc_off, c.words, 0.1, 0.01, SEED)
+    o = oracle.ExactSampler(k or K, c.num_types, c.doc_off, c.words, 0.1, 0.01, SEED,
+                            kind="sparse" if kind == "sparse" else "dense")
     o.sweep(SWEEPS)
     np.testing.assert_array_equal(r["z"], o.z())
     nw, nwsum, _, _ = o.counts()
     np.testing.assert_array_equal(r["nw"], nw)
     np.testing.assert_array_equal(r["nwsum"], nwsum)
     assert abs(float(r["ll"]) - o.log_likelihood()) < 1e-9 * abs(o.log_likelihood())
-    vk, kp = c.num_types * 128, 128
-    # compact: two nw cells per int32 word, the nwsum part as raw int32, and
-    # the escape count's 4-byte MAX all-reduce
-    assert int(r["bytes"]) == (4 * (vk // 2 + kp) + 4 if compact else 4 * (vk + kp))
+    kp = int(r["kp"])
+    vk = c.num_types * kp
+    cells = int(r["cells"])
+    assert cells == (4 if kp >= 2048 else 2)
+    # compact: two (four) nw cells per int32 word, the nwsum part as raw
+    # int32, and the escape count's 4-byte MAX all-reduce
+    assert int(r["bytes"]) == (4 * (vk // cells + kp) + 4 if compact else 4 * (vk + kp))
