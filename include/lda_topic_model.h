@@ -76,6 +76,17 @@ int32_t ldatm_plan_shards(int32_t num_threads, int32_t num_devices, int64_t num_
 lda_status ldatm_set_devices(ldatm* m, int32_t n, const int32_t* devices);
 /* Shards the next estimate() runs on (creates them if needed). */
 lda_status ldatm_num_shards(ldatm* m, int32_t* shards);
+/* The shards' compact exchange (lda_exchange_pack; creates the shards if
+ * needed): cells per packed word (lda_set_exchange_cells: 4 for K > 1024 up
+ * to 64 shards, else 2; 0 when the shards do not exchange packed words --
+ * one shard, or shards on one device without LDA_LOCAL_COMPACT=1), whether
+ * the escape lists travel at their used length (1, the default: the counts
+ * are read on the host behind each pack, overlapping the packed words'
+ * all-reduce) or whole (0, LDA_ESCAPE_LISTS=capacity), the largest per-shard
+ * escape count gathered so far and the number of count reads.  Any pointer
+ * may be NULL. */
+lda_status ldatm_exchange_info(ldatm* m, int32_t* cells_per_word, int32_t* used_lists, int32_t* escapes_max,
+                               int64_t* list_exchanges);
 /* LDA_SAMPLER_* (default: DENSE for K <= 1024, SPARSE above) */
 lda_status ldatm_set_sampler(ldatm* m, int32_t sampler);
 /* With more than one GPU shard: cut every sweep into `parts` parts

@@ -133,6 +133,21 @@ class ShardGroup {
   size_t packed_count = 0, escape_count = 0;
   std::vector<std::vector<void*>> packed, escapes;        // [part][shard]
   std::vector<std::vector<int32_t*>> escapes_all;         // [part][shard], device buffers
+  // escape lists at their used length (round 6, the torch path's default
+  // since round 5): every shard's count is copied to pinned host memory right
+  // behind its pack, the packed words' all-reduce is issued, and only then
+  // does the host read the counts (the copies, not the sum: the read overlaps
+  // that collective) and all-gather 1 + 3 m int32 per shard, m the largest
+  // count; nothing when m = 0.  false: the whole fixed-capacity lists, no
+  // read (LDA_ESCAPE_LISTS=capacity).
+  bool used_lists = true;
+  int32_t cells = 2;                                      // lda_set_exchange_cells
+  int32_t* host_counts = nullptr;                         // pinned [LDA_MAX_EXCHANGE_PARTS][G]
+  std::vector<std::vector<hipEvent_t>> count_events;      // [part][shard]: count copied
+  std::vector<size_t> gathered_cap;                       // [part]: escapes_all holds G x this
+  std::vector<int32_t> part_m;                            // [part]: the m of the pending exchange
+  int32_t m_max = 0;                                      // largest m gathered (ldatm_exchange_info)
+  int64_t list_exchanges = 0;                             // count reads so far
 
   ~ShardGroup() {
     for (auto c : comms) ncclCommDestroy(c);
@@ -151,6 +166,12 @@ class ShardGroup {
           (void)hipSetDevice(dev[g]);
           (void)hipFree(v[g]);
         }
+    for (auto& v : count_events)
+      for (size_t g = 0; g < v.size(); ++g) {
+        (void)hipSetDevice(dev[g]);
+        (void)hipEventDestroy(v[g]);
+      }
+    if (host_counts) (void)hipHostFree(host_counts);
     for (auto c : ctx) lda_destroy(c);
   }
 
@@ -210,23 +231,60 @@ class ShardGroup {
 
   bool use_compact() const { return compact && (!local_sum || local_compact) && ctx.size() > 1; }
 
-  // local_sum + use_compact(): the packed words summed on streams[0] as
-  // local_reduce sums the int32 buffers, and every shard's escape list copied
-  // into every shard's escapes_all [G x escape_count] in shard order (what
-  // ncclAllReduce + ncclAllGather leave on distinct devices)
-  void local_reduce_compact(int part, const std::vector<hipStream_t>& streams) {
+  // local_sum + use_compact(): every shard's first n int32 of its escape
+  // list copied into every shard's escapes_all [G x n] in shard order (what
+  // ncclAllGather leaves on distinct devices)
+  void local_gather(int part, size_t n, const std::vector<hipStream_t>& streams) {
     const size_t G = ctx.size();
-    const auto& pk = packed[(size_t)part];
-    local_reduce(pk, packed_count, streams);      // packed_count: V Kp / 2 + Kp, a multiple of 4
     for (size_t g = 0; g < G; ++g)
       for (size_t r = 0; r < G; ++r)
-        hip_check(hipMemcpyAsync(escapes_all[(size_t)part][g] + r * escape_count, escapes[(size_t)part][r],
-                                 sizeof(int32_t) * escape_count, hipMemcpyDeviceToDevice, streams[g]),
+        hip_check(hipMemcpyAsync(escapes_all[(size_t)part][g] + r * n, escapes[(size_t)part][r],
+                                 sizeof(int32_t) * n, hipMemcpyDeviceToDevice, streams[g]),
                   "hipMemcpyAsync");
+  }
+
+  // the compact exchange's cells per packed word and list mode, once the
+  // shards exist: four 8-bit cells for the large-K sampler's tables (Kp >=
+  // 2048, at most 64 shards) when the lists travel at their used length --
+  // C5 at 8 GPUs: 1.07 GB instead of 2.15 GB per exchange, ~1e5 escapes per
+  // shard per sweep -- else two (C4: the narrower fields
+  // escape about as many bytes as they save).  LDA_ESCAPE_LISTS=capacity
+  // and LDA_EXCHANGE_CELLS=2|4 override (A/B and tests).
+  void init_cells(int32_t kp) {
+    const char* el = std::getenv("LDA_ESCAPE_LISTS");
+    used_lists = !(el && std::strcmp(el, "capacity") == 0);
+    cells = (used_lists && ctx.size() <= 64 && kp >= 2048) ? 4 : 2;
+    const char* ec = std::getenv("LDA_EXCHANGE_CELLS");
+    if (ec && (ec[0] == '2' || ec[0] == '4') && ec[1] == 0) cells = ec[0] - '0';
+    if (cells == 4 && !used_lists)
+      raise(LDA_ERR_UNSUPPORTED, "four cells per word need used-length escape lists (their capacity is "
+                                 "three times the two-cell lists')");
+    for (auto c : ctx) check(lda_set_exchange_cells(c, cells), "lda_set_exchange_cells");
   }
 
   // the compact exchange's first step, on every shard's own stream: part
   // `part`'s buffer packed (lda_exchange_pack)
+  // escapes_all[part][g] able to hold G x n int32 (grown on demand: with
+  // four cells a C5 shard's list capacity is 750 MB, and G copies of it per
+  // device would be 6 GB for lists that are normally ~1 MB)
+  void reserve_gathered(int part, size_t n) {
+    const size_t G = ctx.size();
+    if (gathered_cap[(size_t)part] >= n) return;
+    const size_t want = std::min(escape_count, std::max(n + n / 2, (size_t)4096));
+    for (size_t g = 0; g < G; ++g) {
+      hip_check(hipSetDevice(dev[g]), "hipSetDevice");
+      if (escapes_all[(size_t)part][g]) {
+        // an unpack of an earlier exchange may still read the old lists
+        hip_check(hipDeviceSynchronize(), "hipDeviceSynchronize");
+        hip_check(hipFree(escapes_all[(size_t)part][g]), "hipFree");
+      }
+      escapes_all[(size_t)part][g] = nullptr;
+      hip_check(hipMalloc(reinterpret_cast<void**>(&escapes_all[(size_t)part][g]), sizeof(int32_t) * want * G),
+                "hipMalloc");
+    }
+    gathered_cap[(size_t)part] = want;
+  }
+
   void pack_part(int part) {
     if (!use_compact()) return;
     const size_t G = ctx.size();
@@ -234,34 +292,95 @@ class ShardGroup {
       packed.resize((size_t)part + 1, std::vector<void*>(G));
       escapes.resize((size_t)part + 1, std::vector<void*>(G));
       escapes_all.resize((size_t)part + 1, std::vector<int32_t*>(G, nullptr));
+      gathered_cap.resize((size_t)part + 1, 0);
+      part_m.resize((size_t)part + 1, 0);
     }
     check(lda_exchange_sizes(ctx[0], (int32_t)G, max_tokens, &packed_count, &escape_count), "lda_exchange_sizes");
+    if (used_lists && !host_counts) {
+      hip_check(hipHostMalloc(reinterpret_cast<void**>(&host_counts), sizeof(int32_t) * G * LDA_MAX_EXCHANGE_PARTS,
+                              hipHostMallocPortable),
+                "hipHostMalloc");
+      count_events.assign(LDA_MAX_EXCHANGE_PARTS, std::vector<hipEvent_t>(G, nullptr));
+      for (auto& v : count_events)
+        for (size_t g = 0; g < G; ++g) {
+          hip_check(hipSetDevice(dev[g]), "hipSetDevice");
+          hip_check(hipEventCreateWithFlags(&v[g], hipEventDisableTiming), "hipEventCreate");
+        }
+    }
     for (size_t g = 0; g < G; ++g) {
       check(lda_exchange_pack(ctx[g], part, (int32_t)G, max_tokens, &packed[(size_t)part][g],
                               &escapes[(size_t)part][g]),
             "lda_exchange_pack");
-      if (!escapes_all[(size_t)part][g]) {
+      if (used_lists) {
+        // the list's count word to pinned memory behind the pack, on the
+        // shard's stream: the host reads it in gather_part
         hip_check(hipSetDevice(dev[g]), "hipSetDevice");
-        hip_check(hipMalloc(reinterpret_cast<void**>(&escapes_all[(size_t)part][g]),
-                            sizeof(int32_t) * escape_count * G),
-                  "hipMalloc");
+        hip_check(hipMemcpyAsync(host_counts + (size_t)part * G + g, escapes[(size_t)part][g], sizeof(int32_t),
+                                 hipMemcpyDeviceToHost, stream(g)),
+                  "hipMemcpyAsync");
+        hip_check(hipEventRecord(count_events[(size_t)part][g], stream(g)), "hipEventRecord");
       }
     }
+    if (!used_lists) reserve_gathered(part, escape_count);
+  }
+
+  // the escape lists' all-gather, on streams[g] behind the packed words'
+  // sum: the whole lists, or (used_lists) the host reads the counts the pack
+  // staged and gathers 1 + 3 m int32 per shard
+  void gather_part(int part, const std::vector<hipStream_t>& streams) {
+    if (!use_compact()) return;
+    const size_t G = ctx.size();
+    size_t n = escape_count;
+    if (used_lists) {
+      int32_t m = 0;
+      for (size_t g = 0; g < G; ++g) {
+        hip_check(hipEventSynchronize(count_events[(size_t)part][g]), "hipEventSynchronize");
+        m = std::max(m, host_counts[(size_t)part * G + g]);
+      }
+      const int32_t cap = (int32_t)((escape_count - 1) / 3);
+      if (m < 0 || m > cap)
+        raise(LDA_ERR_STATE, "escape list overflow: " + std::to_string(m) + " escapes, capacity " +
+                                 std::to_string(cap));
+      part_m[(size_t)part] = m;
+      m_max = std::max(m_max, m);
+      ++list_exchanges;
+      if (m == 0) return;
+      n = 1 + 3 * (size_t)m;
+      reserve_gathered(part, n);
+    }
+    if (local_sum) {
+      local_gather(part, n, streams);
+      return;
+    }
+    ncclResult_t r = ncclGroupStart();
+    for (size_t g = 0; g < G && r == ncclSuccess; ++g)
+      r = ncclAllGather(escapes[(size_t)part][g], escapes_all[(size_t)part][g], n, ncclInt32, comms[g], streams[g]);
+    const ncclResult_t r2 = ncclGroupEnd();
+    if (r != ncclSuccess || r2 != ncclSuccess)
+      raise(LDA_ERR_DEVICE, std::string("ncclAllGather: ") + ncclGetErrorString(r != ncclSuccess ? r : r2));
   }
 
   // ... and its last, on every shard's own stream: the part's buffer = the sum
   void unpack_part(int part) {
     if (!use_compact()) return;
-    for (size_t g = 0; g < ctx.size(); ++g)
-      check(lda_exchange_unpack(ctx[g], part, (int32_t)ctx.size(), max_tokens, escapes_all[(size_t)part][g]),
-            "lda_exchange_unpack");
+    const int32_t G = (int32_t)ctx.size();
+    for (size_t g = 0; g < ctx.size(); ++g) {
+      if (used_lists) {
+        const int32_t m = part_m[(size_t)part];
+        check(lda_exchange_unpack_lists(ctx[g], part, G, max_tokens, m ? escapes_all[(size_t)part][g] : nullptr, m),
+              "lda_exchange_unpack_lists");
+      } else {
+        check(lda_exchange_unpack(ctx[g], part, G, max_tokens, escapes_all[(size_t)part][g]),
+              "lda_exchange_unpack");
+      }
+    }
   }
 
   // the sum of part `part`'s buffers across the shards, each shard's on
   // streams[g] (its own stream, or its collective stream): compact, one
-  // grouped SUM all-reduce of the packed words and an all-gather of the
-  // escape lists (pack_part before, unpack_part after); or the int32
-  // buffers themselves (all-reduce / the device-side sum)
+  // grouped SUM all-reduce of the packed words (pack_part before,
+  // gather_part and unpack_part after); or the int32 buffers themselves
+  // (all-reduce / the device-side sum)
   void reduce_part(int part, const std::vector<hipStream_t>& streams) {
     std::vector<void*> ptr(ctx.size());
     size_t count = 0;
@@ -270,7 +389,7 @@ class ShardGroup {
     const bool cmp = use_compact();
     if (local_sum) {
       if (cmp)
-        local_reduce_compact(part, streams);
+        local_reduce(packed[(size_t)part], packed_count, streams);   // a multiple of 4 int32
       else
         local_reduce(ptr, count, streams);
       return;
@@ -280,17 +399,13 @@ class ShardGroup {
       if (cmp) {
         void* pk = packed[(size_t)part][g];
         r = ncclAllReduce(pk, pk, packed_count, ncclInt32, ncclSum, comms[g], streams[g]);
-        if (r == ncclSuccess)
-          r = ncclAllGather(escapes[(size_t)part][g], escapes_all[(size_t)part][g], escape_count, ncclInt32,
-                            comms[g], streams[g]);
       } else {
         r = ncclAllReduce(ptr[g], ptr[g], count, ncclInt32, ncclSum, comms[g], streams[g]);
       }
     }
     const ncclResult_t r2 = ncclGroupEnd();
     if (r != ncclSuccess || r2 != ncclSuccess)
-      raise(LDA_ERR_DEVICE, std::string(cmp ? "ncclAllReduce / ncclAllGather: " : "ncclAllReduce: ") +
-                                ncclGetErrorString(r != ncclSuccess ? r : r2));
+      raise(LDA_ERR_DEVICE, std::string("ncclAllReduce: ") + ncclGetErrorString(r != ncclSuccess ? r : r2));
   }
 
   void reduce() {
@@ -299,6 +414,7 @@ class ShardGroup {
     for (size_t g = 0; g < ctx.size(); ++g) st[g] = stream(g);
     pack_part(0);
     reduce_part(0, st);
+    gather_part(0, st);
     unpack_part(0);
   }
 
@@ -352,6 +468,9 @@ class ShardGroup {
       }
       reduce_part(i, comm_streams);
     }
+    // every part's escape lists once every sampler part is enqueued: the
+    // count reads wait for the parts' packs, not for the packed sums
+    for (int i = 0; i < parts; ++i) gather_part(i, comm_streams);
     for (size_t g = 0; g < ctx.size(); ++g) {
       hip(hipSetDevice(dev[g]), "hipSetDevice");
       hip(hipEventRecord(events[g], comm_streams[g]), "hipEventRecord");   // every sum landed
@@ -476,6 +595,17 @@ int32_t ParallelTopicModel::numShards() {
   return (int32_t)shards_->ctx.size();
 }
 
+void ParallelTopicModel::exchangeInfo(int32_t* cells, int32_t* used_lists, int32_t* escapes_max,
+                                      int64_t* list_exchanges) {
+  ensureShards();
+  const ShardGroup& s = *shards_;
+  const bool cmp = s.use_compact();
+  if (cells) *cells = cmp ? s.cells : 0;
+  if (used_lists) *used_lists = cmp && s.used_lists ? 1 : 0;
+  if (escapes_max) *escapes_max = s.m_max;
+  if (list_exchanges) *list_exchanges = s.list_exchanges;
+}
+
 void ParallelTopicModel::setExchangeParts(int32_t parts) {
   if (parts < 1 || parts > LDA_MAX_EXCHANGE_PARTS) raise(LDA_ERR_INVALID_ARG, "parts out of range");
   exchange_parts_ = parts;
@@ -588,6 +718,7 @@ void ParallelTopicModel::ensureShards() {
     sg->compact = compact_exchange_ && !(e && e[0] == '1');
     const char* lc = std::getenv("LDA_LOCAL_COMPACT");
     sg->local_compact = lc && lc[0] == '1';
+    if (sg->use_compact()) sg->init_cells(lda_padded_topics(K_));
   }
   if (G > 1) {
     // shards recount (or keep a delta) in the same sweeps: the smallest
@@ -1195,6 +1326,12 @@ lda_status ldatm_set_devices(ldatm* m, int32_t n, const int32_t* devices) {
 lda_status ldatm_num_shards(ldatm* m, int32_t* shards) {
   TM_CHECK(m && shards);
   return guard([&] { *shards = m->model.numShards(); });
+}
+
+lda_status ldatm_exchange_info(ldatm* m, int32_t* cells_per_word, int32_t* used_lists, int32_t* escapes_max,
+                               int64_t* list_exchanges) {
+  TM_CHECK(m);
+  return guard([&] { m->model.exchangeInfo(cells_per_word, used_lists, escapes_max, list_exchanges); });
 }
 
 int32_t ldatm_plan_shards(int32_t num_threads, int32_t num_devices, int64_t num_tokens,

@@ -67,6 +67,10 @@ class ParallelTopicModel {
   // T < 0 -> plain snapshot sweeps
   void setStalenessThreads(int32_t threads);
   int32_t numShards();
+  // the shards' compact exchange: cells per packed word (0: not compact),
+  // escape lists at their used length (1) or whole, the largest per-shard
+  // escape count gathered and the count reads so far (ldatm_exchange_info)
+  void exchangeInfo(int32_t* cells, int32_t* used_lists, int32_t* escapes_max, int64_t* list_exchanges);
   void setVerbosity(int32_t v) { verbosity_ = v; }
   // state a Java-side ParallelTopicModel already holds (GpuParallelTopicModel:
   // Mallet's own addInstances topics, alpha/beta optimised in an earlier

@@ -55,6 +55,7 @@ TM_SIGNATURES = {
     "ldatm_set_warm_start": (_i32, [_vp, _i32, _i32]),
     "ldatm_set_staleness_threads": (_i32, [_vp, _i32]),
     "ldatm_num_shards": (_i32, [_vp, C.POINTER(_i32)]),
+    "ldatm_exchange_info": (_i32, [_vp, C.POINTER(_i32), C.POINTER(_i32), C.POINTER(_i32), C.POINTER(C.c_int64)]),
     "ldatm_plan_shards": (_i32, [_i32, _i32, C.c_int64, _i32, _i32, C.c_int64]),
     "ldatm_set_topics": (_i32, [_vp, C.c_int64, _vp]),
     "ldatm_set_hyper": (_i32, [_vp, _vp, C.c_double, C.c_double]),
@@ -308,6 +309,16 @@ class ParallelTopicModel:
         n = C.c_int32()
         _check(self._L.ldatm_num_shards(self._h, C.byref(n)), "numShards")
         return n.value
+
+    def exchangeInfo(self) -> dict:
+        """The shards' compact exchange (ldatm_exchange_info): cells per
+        packed word (0: none), used-length escape lists, the largest escape
+        count gathered, the count reads so far."""
+        c, u, m, n = C.c_int32(), C.c_int32(), C.c_int32(), C.c_int64()
+        _check(self._L.ldatm_exchange_info(self._h, C.byref(c), C.byref(u), C.byref(m), C.byref(n)),
+               "exchangeInfo")
+        return {"cells_per_word": c.value, "used_lists": bool(u.value), "escapes_max": m.value,
+                "list_exchanges": n.value}
 
     # --------------------------------------------------------- training
     def estimate(self):

@@ -274,10 +274,13 @@ def test_shard_group_on_one_device(oracle, shards, parts, kind):
     np.testing.assert_allclose([v for _, v in m.llTrace()], [v for _, v in single.llTrace()], rtol=1e-12)
 
 
-@pytest.mark.parametrize("shards,parts,sequential", [(2, 1, False), (3, 2, False), (3, 1, True)])
-def test_shard_group_compact_exchange_on_one_device(monkeypatch, shards, parts, sequential):
+@pytest.mark.parametrize("shards,parts,sequential,lists", [(2, 1, False, "used"), (3, 2, False, "used"),
+                                                           (3, 1, True, "used"), (2, 1, False, "capacity"),
+                                                           (3, 2, False, "capacity")])
+def test_shard_group_compact_exchange_on_one_device(monkeypatch, shards, parts, sequential, lists):
     """The multi-GPU ShardGroup's compact exchange (pack_part, the packed
-    words' sum and the escape lists' all-gather, unpack_part) with the two
+    words' sum, the escape lists' all-gather -- at their used length after
+    the host reads the counts, or whole -- and unpack_part) with the two
     collectives replaced by device-side stand-ins (LDA_LOCAL_COMPACT=1), so
     its ordering runs on the one-GPU box: plain snapshot sweeps (split into
     `parts`, the exchange on the collective streams) or the default
@@ -285,6 +288,7 @@ def test_shard_group_compact_exchange_on_one_device(monkeypatch, shards, parts, 
     cells beyond both biases, so escape lists travel; bit-exact against one
     context."""
     monkeypatch.setenv("LDA_LOCAL_COMPACT", "1")
+    monkeypatch.setenv("LDA_ESCAPE_LISTS", lists)
     from ldagibbssampling_amd.corpus import Corpus
     rng = np.random.default_rng(shards * 10 + parts)
     D, L, V, K = 1000, 150, 300, 2
@@ -306,6 +310,49 @@ def test_shard_group_compact_exchange_on_one_device(monkeypatch, shards, parts, 
     m = run([0] * shards)
     single = run(None)
     assert m.numShards() == shards and single.numShards() == 1
+    info = m.exchangeInfo()
+    assert info["cells_per_word"] == 2 and info["used_lists"] == (lists == "used")
+    if lists == "used":
+        assert info["escapes_max"] > 0 and info["list_exchanges"] >= 6
+    np.testing.assert_array_equal(m.topicAssignments(), single.topicAssignments())
+    for a, b in zip(m.typeTopicCounts(), single.typeTopicCounts()):
+        np.testing.assert_array_equal(a, b)
+
+
+@pytest.mark.parametrize("shards,parts,sequential", [(2, 1, False), (3, 2, False), (2, 1, True)])
+def test_shard_group_four_cells_large_k_on_one_device(monkeypatch, shards, parts, sequential):
+    """K = 2048 (the large-K sampler): the ShardGroup packs four 8-bit cells
+    per word and sends its escape lists at their used length by default
+    (ldatm_exchange_info), with the collectives' device-side stand-ins.  One
+    word holding most tokens puts (word, topic) changes beyond the four-cell
+    bias (2^7 / shards), so escapes travel in the first exchanges; bit-exact
+    against one context."""
+    monkeypatch.setenv("LDA_LOCAL_COMPACT", "1")
+    monkeypatch.delenv("LDA_ESCAPE_LISTS", raising=False)
+    from ldagibbssampling_amd.corpus import Corpus
+    rng = np.random.default_rng(100 + shards * 10 + parts)
+    D, L, V, K = 1200, 500, 400, 2048
+    words = rng.integers(1, V, size=D * L).astype(np.int32)
+    words[rng.random(D * L) < 0.9] = 0
+    c = Corpus(np.arange(D + 1, dtype=np.int64) * L, words, V)
+
+    def run(devices):
+        m, _ = _model(c, K, 20.0, 0.05, 11, setNumIterations=4, setOptimizeInterval=0)
+        if not sequential:
+            m.setWarmStart(1, 0)
+            m.setStalenessThreads(-1)
+        if devices:
+            m.setDevices(devices)
+            m.setExchangeParts(parts)
+        m.estimate()
+        return m
+
+    m = run([0] * shards)
+    single = run(None)
+    assert m.numShards() == shards and single.numShards() == 1
+    info = m.exchangeInfo()
+    assert info["cells_per_word"] == 4 and info["used_lists"]
+    assert info["escapes_max"] > 0
     np.testing.assert_array_equal(m.topicAssignments(), single.topicAssignments())
     for a, b in zip(m.typeTopicCounts(), single.typeTopicCounts()):
         np.testing.assert_array_equal(a, b)
