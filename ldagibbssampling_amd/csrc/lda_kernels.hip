@@ -112,6 +112,7 @@ __device__ __forceinline__ float dpp_mov(float v) {
 // s_waitcnt vmcnt(0) / vmcnt(1) (gfx9 encoding: expcnt and lgkmcnt left at their maxima)
 constexpr int kVmcnt0 = 0x0F70;
 constexpr int kVmcnt1 = 0x0F71;
+constexpr int kLgkmcnt0 = 0xC07F;   // lgkmcnt(0), vmcnt and expcnt left at their maxima
 // (a != b) ? m : 0 as s_cmp + s_cselect_b64
 __device__ __forceinline__ uint64_t select_mask_ne(int a, int b, uint64_t m) {
   uint64_t r;
@@ -1938,6 +1939,32 @@ __global__ __launch_bounds__(256) void k_sample_sparse(SampleParams p) {
 #ifndef SB_APICK_LDS
 #define SB_APICK_LDS 1
 #endif
+// > 0 (default 4 since late round 6): the LDS reads (tab + document count)
+// of the first SB_LDS_BATCH register rounds are all issued, with the doc
+// part's, before the first is used -- one LDS round trip for those rounds
+// instead of one per round (the compiler had serialised them: one pair of
+// reads, wait, fma, the next pair); the sums are the same fma for fma.
+// SB_LDS_BATCH2 > 0: the next SB_LDS_BATCH2 rounds the same way, when the
+// row has them.  C5 with SB_TOKEN_LGKM0 (below), one session, both orders
+// (profiles/r06/ldsbatch/): near init 2.250 -> 2.294e9, after 30 sweeps
+// 2.730 -> 2.828e9; batches of 6 or all 12 rounds gain less.
+#ifndef SB_LDS_BATCH
+#define SB_LDS_BATCH 4
+#endif
+#ifndef SB_LDS_BATCH2
+#define SB_LDS_BATCH2 0
+#endif
+#ifndef SB_LDS_BATCH_ADDR
+#define SB_LDS_BATCH_ADDR 0
+#endif
+// 1 (default since late round 6): an lgkmcnt(0) at the end of every token,
+// where every LDS read of the token has been used anyway: without it the
+// waitcnt pass carried a rare path's pending LDS write across the loop's
+// join into the next token, as an lgkmcnt(0) between the batch's first reads
+// and the rest
+#ifndef SB_TOKEN_LGKM0
+#define SB_TOKEN_LGKM0 1
+#endif
 // gfx9 buffer resource word 3 (raw 32-bit loads, bounds checked)
 constexpr int kBufWord3 = 0x00020000;
 #ifndef SB_WAVES
@@ -2472,6 +2499,71 @@ __global__ __launch_bounds__(64 * sb_waves<C>()) SB_ATTR void k_sample_big(Sampl
           // above the branch, their wait and conversions went with them)
           if (!row_sat) {
             asm volatile("" ::: "memory");
+#if SB_LDS_BATCH > 0
+            constexpr int BQ = SB_LDS_BATCH < RB ? SB_LDS_BATCH : RB;
+#if SB_LDS_BATCH_ADDR
+            // the rounds' topics first, so that every read below issues back
+            // to back (no address arithmetic between them to reuse a register
+            // still awaited)
+            int tq[BQ];
+#pragma unroll
+            for (int q = 0; q < BQ; ++q) tq[q] = (int)(ring[s][q] & ENT_TOPIC_MASK);
+            __builtin_amdgcn_sched_barrier(0);
+#endif
+            const DocReads dr = doc_reads();
+            // every batched round's reads (a round past the row reads topic
+            // 0's entries: harmless, its count is 0 and it is skipped below)
+            float2 tbq[BQ];
+            int ndq[BQ];
+#pragma unroll
+            for (int q = 0; q < BQ; ++q) {
+#if SB_LDS_BATCH_ADDR
+              const int t_ = tq[q];
+#else
+              const int t_ = (int)(ring[s][q] & ENT_TOPIC_MASK);
+#endif
+              tbq[q] = tab[t_];
+              ndq[q] = nd16_get(nd2, t_);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int q = 0; q < BQ; ++q) {
+              if (q < SB_RU || q < nr_all) {
+                const float coef = __builtin_fmaf((float)ndq[q], tbq[q].x, tbq[q].y);
+                acc = __builtin_fmaf((float)(ring[s][q] >> ENT_TOPIC_BITS), coef, acc);
+              }
+              accq[q] = acc;
+            }
+            doc_part(dr);
+#if SB_LDS_BATCH2 > 0
+            constexpr int BQ2 = (BQ + SB_LDS_BATCH2 < RB ? BQ + SB_LDS_BATCH2 : RB);
+            if (BQ2 > BQ && nr_all > BQ) {
+              float2 tb2[BQ2 > BQ ? BQ2 - BQ : 1];
+              int nd2q[BQ2 > BQ ? BQ2 - BQ : 1];
+#pragma unroll
+              for (int q = BQ; q < BQ2; ++q) {
+                const int t_ = (int)(ring[s][q] & ENT_TOPIC_MASK);
+                tb2[q - BQ] = tab[t_];
+                nd2q[q - BQ] = nd16_get(nd2, t_);
+              }
+              __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+              for (int q = BQ; q < BQ2; ++q) {
+                if (q < nr_all) {
+                  const float coef = __builtin_fmaf((float)nd2q[q - BQ], tb2[q - BQ].x, tb2[q - BQ].y);
+                  acc = __builtin_fmaf((float)(ring[s][q] >> ENT_TOPIC_BITS), coef, acc);
+                }
+                accq[q] = acc;
+              }
+            } else {
+#pragma unroll
+              for (int q = BQ; q < BQ2; ++q) accq[q] = acc;
+            }
+            rounds(false, BQ2);
+#else
+            rounds(false, BQ);
+#endif
+#else
             const DocReads dr = doc_reads();
             // the doc reads issue first; nothing moves across (the scheduler
             // had issued them after the rounds' reads had been waited for)
@@ -2483,6 +2575,7 @@ __global__ __launch_bounds__(64 * sb_waves<C>()) SB_ATTR void k_sample_big(Sampl
             }
             doc_part(dr);
             rounds(false, SB_RU);
+#endif
           } else {
             asm volatile("" ::: "memory");
             doc_part(doc_reads());
@@ -2802,6 +2895,12 @@ __global__ __launch_bounds__(64 * sb_waves<C>()) SB_ATTR void k_sample_big(Sampl
 #endif
           pk = kn;
           cn = (lane == idx) ? kn : cn;
+#if SB_TOKEN_LGKM0
+          // every LDS read of this token has been used by now: say so, so the
+          // waitcnt pass does not carry a rare path's pending LDS write into
+          // the next token's first reads as an lgkmcnt(0)
+          __builtin_amdgcn_s_waitcnt(kLgkmcnt0);
+#endif
         }
       }
     }
