@@ -116,11 +116,11 @@ def test_bench_traffic_record_matches_its_sweep_window():
     rec, src = bench.pmc_record(250_000_000, "k_sample_big<", 4096, 0, C=64)
     if rec is None:
         pytest.skip("no C5 profile of the kernel sources in the tree")
-    assert src.endswith("traffic_c5.json")
+    assert "traffic_c5" in src and "_b30" not in src
     assert rec.get("burnin", 0) == 0
     rec30, src30 = bench.pmc_record(250_000_000, "k_sample_big<", 4096, 30, C=64)
     if rec30 is not None:
-        assert src30.endswith("traffic_c5_b30.json") and rec30["burnin"] == 30
+        assert "traffic_c5" in src30 and src30.endswith("_b30.json") and rec30["burnin"] == 30
         assert rec30["bytes_per_token"] < rec["bytes_per_token"]
     assert bench.pmc_record(250_000_000, "k_sample_big<", 4096, 7, C=64) == (None, None)
 
