@@ -1965,6 +1965,11 @@ __global__ __launch_bounds__(256) void k_sample_sparse(SampleParams p) {
 #ifndef SB_TOKEN_LGKM0
 #define SB_TOKEN_LGKM0 1
 #endif
+// 1 (A/B builds): the long rows' batches past the register rounds issue each
+// batch's LDS reads together as well
+#ifndef SB_LDS_BATCH_LONG
+#define SB_LDS_BATCH_LONG 0
+#endif
 // gfx9 buffer resource word 3 (raw 32-bit loads, bounds checked)
 constexpr int kBufWord3 = 0x00020000;
 #ifndef SB_WAVES
@@ -2615,8 +2620,32 @@ __global__ __launch_bounds__(64 * sb_waves<C>()) SB_ATTR void k_sample_big(Sampl
 #pragma unroll
                 for (int b = 0; b < SB_BATCH; ++b) en[b] = 0u;
               }
+#if SB_LDS_BATCH_LONG
+              if (!sat) {
+                // the batch's LDS reads issued together (one round trip per
+                // batch instead of one per round), then its fma in order
+                float2 tbb[SB_BATCH];
+                int ndb[SB_BATCH];
+#pragma unroll
+                for (int b = 0; b < SB_BATCH; ++b) {
+                  const int t_ = (int)(ea[b] & ENT_TOPIC_MASK);
+                  tbb[b] = tab[t_];
+                  ndb[b] = nd16_get(nd2, t_);
+                }
+                __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                for (int b = 0; b < SB_BATCH; ++b) {
+                  const float coef = __builtin_fmaf((float)ndb[b], tbb[b].x, tbb[b].y);
+                  acc = __builtin_fmaf((float)(ea[b] >> ENT_TOPIC_BITS), coef, acc);
+                }
+              } else {
+#pragma unroll
+                for (int b = 0; b < SB_BATCH; ++b) acc = term_acc(ea[b], w, sat, acc);
+              }
+#else
 #pragma unroll
               for (int b = 0; b < SB_BATCH; ++b) acc = term_acc(ea[b], w, sat, acc);
+#endif
 #pragma unroll
               for (int i = 0; i < SB_NB; ++i) accb[i] = (mb == i) ? acc : accb[i];
 #pragma unroll
