@@ -2176,9 +2176,56 @@ __device__ __forceinline__ int nd16_get(const uint32_t* nd2, int k) {
   do {              \
   } while (0)
 #endif
+// SB_GLOBAL_AS: the pointers a KARG read yields are used as global (address
+// space 1) pointers (KGLOBAL), so the count atomics are global_atomic, not
+// FLAT.  A FLAT operation still in flight (the no-return delta atomics of a
+// chunk switch) makes the waitcnt pass order every later vector memory wait
+// as vmcnt(0); merged into the loop's join, that had drained the ring of
+// prefetched rows at every token's first round (now vmcnt(14..19)).  2 (the
+// default since late round 6): the field itself still read as a FLAT load,
+// waited for where it is used.  1 (A/B): the field read through the kernarg
+// segment's address space -- scalar loads, 7% slower on C5.  0: round 5's
+// FLAT atomics.  C5, four sessions: +0.2-0.5% near init, +0.4-0.7% after
+// burn-in (profiles/r06/ldsbatch/r6v, r6w).
+#ifndef SB_GLOBAL_AS
+#define SB_GLOBAL_AS 2
+#endif
+// 1: the chunk switch waits vmcnt(1) for its chunk registers (round 4: with
+// FLAT atomics in flight the waitcnt pass had turned every later wait into
+// vmcnt(0)); 0 (A/B) leaves the waits to the compiler
+#ifndef SB_CHUNK_WAIT
+#define SB_CHUNK_WAIT 1
+#endif
+#if SB_GLOBAL_AS
+#if SB_GLOBAL_AS == 1
+#define KARG(field)                                                                                   \
+  (*(const volatile __attribute__((address_space(4))) decltype(SampleParams::field)*)(                 \
+      (const __attribute__((address_space(4))) char*)(__builtin_amdgcn_kernarg_segment_ptr()) +        \
+      offsetof(SampleParams, field)))
+#else
+// 2: the field read as before (a FLAT load, waited for where it is used),
+// only the pointers' own accesses global
 #define KARG(field)                                                                                   \
   (*reinterpret_cast<const volatile decltype(SampleParams::field)*>(                                  \
       (const char*)(__builtin_amdgcn_kernarg_segment_ptr()) + offsetof(SampleParams, field)))
+#endif
+template <typename T>
+__device__ __forceinline__ __attribute__((address_space(1))) T* kglobal(T* p) {
+  return (__attribute__((address_space(1))) T*)p;
+}
+template <typename T>
+__device__ __forceinline__ const __attribute__((address_space(1))) T* kglobal(const T* p) {
+  return (const __attribute__((address_space(1))) T*)p;
+}
+#define KGLOBAL(field) kglobal(KARG(field))
+#define KATOMIC_ADD(ptr, v) __hip_atomic_fetch_add((ptr), (v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+#else
+#define KARG(field)                                                                                   \
+  (*reinterpret_cast<const volatile decltype(SampleParams::field)*>(                                  \
+      (const char*)(__builtin_amdgcn_kernarg_segment_ptr()) + offsetof(SampleParams, field)))
+#define KGLOBAL(field) KARG(field)
+#define KATOMIC_ADD(ptr, v) atomicAdd((ptr), (v))
+#endif
 template <int C, int NS, int RB, bool FROZEN>
 #if SB_WPE
 #define SB_ATTR __attribute__((amdgpu_waves_per_eu(SB_WPE, SB_WPE)))
@@ -2217,7 +2264,7 @@ __global__ __launch_bounds__(64 * sb_waves<C>()) SB_ATTR void k_sample_big(Sampl
   auto term_acc = [&](uint32_t e, int w, bool sat, float acc) -> float {
     const int t = (int)(e & ENT_TOPIC_MASK);
     uint32_t c = e >> ENT_TOPIC_BITS;
-    if (sat && c == ENT_COUNT_SAT) c = (uint32_t)KARG(nw)[(int64_t)w * KP + t];
+    if (sat && c == ENT_COUNT_SAT) c = (uint32_t)KGLOBAL(nw)[(int64_t)w * KP + t];
     const float2 tb = tab[t];
     const float coef = __builtin_fmaf((float)nd16_get(nd2, t), tb.x, tb.y);
     return __builtin_fmaf((float)c, coef, acc);
@@ -2226,7 +2273,7 @@ __global__ __launch_bounds__(64 * sb_waves<C>()) SB_ATTR void k_sample_big(Sampl
   auto term_parts = [&](uint32_t e, int w, bool sat, float& cf, float& coef) {
     const int t = (int)(e & ENT_TOPIC_MASK);
     uint32_t c = e >> ENT_TOPIC_BITS;
-    if (sat && c == ENT_COUNT_SAT) c = (uint32_t)KARG(nw)[(int64_t)w * KP + t];
+    if (sat && c == ENT_COUNT_SAT) c = (uint32_t)KGLOBAL(nw)[(int64_t)w * KP + t];
     const float2 tb = tab[t];
     coef = __builtin_fmaf((float)nd16_get(nd2, t), tb.x, tb.y);
     cf = (float)c;
@@ -2282,8 +2329,8 @@ __global__ __launch_bounds__(64 * sb_waves<C>()) SB_ATTR void k_sample_big(Sampl
     auto flush_chunk = [&]() {
       if (kDelta && cn != cz) {
         const uint64_t rb = (uint64_t)(uint32_t)cw * (uint64_t)KP;
-        atomicAdd(KARG(delta) + (rb + (uint32_t)cz), -1);
-        atomicAdd(KARG(delta) + (rb + (uint32_t)cn), 1);
+        KATOMIC_ADD(KGLOBAL(delta) + (rb + (uint32_t)cz), -1);
+        KATOMIC_ADD(KGLOBAL(delta) + (rb + (uint32_t)cn), 1);
       }
     };
 
@@ -2387,18 +2434,20 @@ __global__ __launch_bounds__(64 * sb_waves<C>()) SB_ATTR void k_sample_big(Sampl
             // but the z store just issued): a chunk register the compiler
             // believes in flight makes it wait vmcnt(0) where a token reads
             // it, i.e. drain the row ring
+#if SB_CHUNK_WAIT
             __builtin_amdgcn_s_waitcnt(kVmcnt1);
+#endif
             if (kDelta && on != oz) {
               const uint64_t rb = (uint64_t)(uint32_t)ow * (uint64_t)KP;
-              atomicAdd(KARG(delta) + (rb + (uint32_t)oz), -1);
-              atomicAdd(KARG(delta) + (rb + (uint32_t)on), 1);
+              KATOMIC_ADD(KGLOBAL(delta) + (rb + (uint32_t)oz), -1);
+              KATOMIC_ADD(KGLOBAL(delta) + (rb + (uint32_t)on), 1);
             }
             philox_x01(gbase + (uint64_t)(cbase + lane), p.c2, p.c3, p.k0, p.k1, cx0, cx1);
           }
           if (t == doc_end) {
             clear_doc();
             ++doc;
-            const int64_t* dof = KARG(doc_off);
+            const auto dof = KGLOBAL(doc_off);
             while (dof[doc + 1] - t0 <= t) ++doc;
             doc_end = uniform_i((int)(dof[doc + 1] - t0));
             build_doc(t, doc_end);
@@ -2713,7 +2762,7 @@ __global__ __launch_bounds__(64 * sb_waves<C>()) SB_ATTR void k_sample_big(Sampl
               // (+ dG at zo) split in 16-bit halves, each scanned in 32-bit
               // lanes (< 2^22), so no second global round trip
               const int kc = C * lane + C - 1;
-              const uint64_t pc = KARG(big.pfx)[kc];
+              const uint64_t pc = KGLOBAL(big.pfx)[kc];
               const int64_t vc = (int64_t)pc + ((!FROZEN && kc >= zo) ? dG : 0);
               const uint64_t mc = __ballot((uint64_t)vc > tfx);
               const int L = mc ? (int)__builtin_ctzll(mc) : 63;
@@ -2732,11 +2781,11 @@ __global__ __launch_bounds__(64 * sb_waves<C>()) SB_ATTR void k_sample_big(Sampl
               const int k = mf ? C * L + (int)__builtin_ctzll(mf) : last_topic;
 #else
               const int kc = C * lane + C - 1;
-              const int64_t vc = (int64_t)KARG(big.pfx)[kc] + ((!FROZEN && kc >= zo) ? dG : 0);
+              const int64_t vc = (int64_t)KGLOBAL(big.pfx)[kc] + ((!FROZEN && kc >= zo) ? dG : 0);
               const uint64_t mc = __ballot((uint64_t)vc > tfx);
               const int L = mc ? (int)__builtin_ctzll(mc) : 63;
               const int kf = C * L + (lane < C ? lane : C - 1);
-              const int64_t vf = (int64_t)KARG(big.pfx)[kf] + ((!FROZEN && kf >= zo) ? dG : 0);
+              const int64_t vf = (int64_t)KGLOBAL(big.pfx)[kf] + ((!FROZEN && kf >= zo) ? dG : 0);
               const uint64_t mf = __ballot(lane < C && (uint64_t)vf > tfx);
               const int k = mf ? C * L + (int)__builtin_ctzll(mf) : last_topic;
 #endif
@@ -2801,7 +2850,7 @@ __global__ __launch_bounds__(64 * sb_waves<C>()) SB_ATTR void k_sample_big(Sampl
 #if SB_APICK_LDS
             const uint32_t ff = (!FROZEN && kf == zo) ? Fm1z : fixp(tab[kf].x);
 #else
-            const uint32_t ff = (!FROZEN && kf == zo) ? Fm1z : KARG(big.F)[kf];
+            const uint32_t ff = (!FROZEN && kf == zo) ? Fm1z : KGLOBAL(big.F)[kf];
 #endif
             const uint64_t wf = lane < C ? (uint64_t)nd16_get(nd2, kf) * ff : 0ull;
             const uint64_t i2 = wave_incl_scan_u64(wf);
@@ -2883,7 +2932,7 @@ __global__ __launch_bounds__(64 * sb_waves<C>()) SB_ATTR void k_sample_big(Sampl
               wk.lo = qsel > 0 ? readlane_f(accq[qsel > 0 ? qsel - 1 : 0], lstar) : 0.0f;
             }
             uint32_t c = wk.e >> ENT_TOPIC_BITS;
-            if (row_sat && c == ENT_COUNT_SAT) c = (uint32_t)KARG(nw)[(int64_t)w * KP + zo];
+            if (row_sat && c == ENT_COUNT_SAT) c = (uint32_t)KGLOBAL(nw)[(int64_t)w * KP + zo];
             const float wo = wk.hi - wk.lo;
             const float4 m1 = rm1[s];
             const float O = (float)(c > 0 ? c - 1 : 0u) * __builtin_fmaf((float)ndz, m1.x, m1.y);
