@@ -2193,6 +2193,19 @@ __device__ __forceinline__ int nd16_get(const uint32_t* nd2, int k) {
 // 1: the chunk switch waits vmcnt(1) for its chunk registers (round 4: with
 // FLAT atomics in flight the waitcnt pass had turned every later wait into
 // vmcnt(0)); 0 (A/B) leaves the waits to the compiler
+// 1 (default since late round 6): the alpha part's 64 block-end prefixes
+// (fixed for the sweep) in a register pair per lane for the whole launch
+// instead of one global round trip per A-alpha draw (8.7% of the draws).  Two
+// VGPRs spill in the 4 x 6 ring; still C5 +1.1-1.3% near init, +0.9% after
+// burn-in, two sessions (profiles/r06/ldsbatch/r6y)
+#ifndef SB_PFX_REG
+#define SB_PFX_REG 1
+#endif
+// 1 (A/B): the A search's document part sums only the nonzero count words
+// of each lane's block (a mask first), not all C topics
+#ifndef SB_ADOC_SPARSE
+#define SB_ADOC_SPARSE 0
+#endif
 #ifndef SB_CHUNK_WAIT
 #define SB_CHUNK_WAIT 1
 #endif
@@ -2257,6 +2270,11 @@ __global__ __launch_bounds__(64 * sb_waves<C>()) SB_ATTR void k_sample_big(Sampl
   auto row_ptr = [&](uint32_t o) -> const uint32_t* { return ent + ((uint64_t)o << 6); };
   const int32_t* __restrict__ row_nnz = p.row_nnz;
   const float4* __restrict__ tab_m1 = p.big.tab_m1;
+#if SB_PFX_REG
+  // the alpha part's block-end prefixes (fixed for the sweep) held per lane:
+  // the A search's block choice without a global round trip
+  const uint64_t pfx_r = p.big.pfx[C * lane + C - 1];
+#endif
 
   auto fixp = [&](float x) -> uint32_t { return big_fix(x, S); };
   // one B term into the lane's running sum (SAT: the row holds a saturated
@@ -2762,7 +2780,11 @@ __global__ __launch_bounds__(64 * sb_waves<C>()) SB_ATTR void k_sample_big(Sampl
               // (+ dG at zo) split in 16-bit halves, each scanned in 32-bit
               // lanes (< 2^22), so no second global round trip
               const int kc = C * lane + C - 1;
+#if SB_PFX_REG
+              const uint64_t pc = pfx_r;
+#else
               const uint64_t pc = KGLOBAL(big.pfx)[kc];
+#endif
               const int64_t vc = (int64_t)pc + ((!FROZEN && kc >= zo) ? dG : 0);
               const uint64_t mc = __ballot((uint64_t)vc > tfx);
               const int L = mc ? (int)__builtin_ctzll(mc) : 63;
@@ -2803,6 +2825,35 @@ __global__ __launch_bounds__(64 * sb_waves<C>()) SB_ATTR void k_sample_big(Sampl
             // time); the own topic's F' = Fm1 added as a correction on its lane
             uint64_t ps = 0;
             {
+#if SB_ADOC_SPARSE && !SB_ND8
+              // only the lane's nonzero count words: a mask from C / 8
+              // 16-byte reads (starting at a lane-rotated chunk), then one
+              // count word and one 16-byte tab read per nonzero word (a
+              // document holds at most a few hundred topics of 4096); the
+              // same integer sum, in another order
+              const uint4* ndv = reinterpret_cast<const uint4*>(nd2) + lane * (C / 8);
+              uint32_t nzm = 0;
+#pragma unroll 2
+              for (int j8 = 0; j8 < C / 8; ++j8) {
+                const int o8 = (j8 + lane) & (C / 8 - 1);
+                const uint4 v = ndv[o8];
+                const uint32_t b = (uint32_t)(v.x != 0u) | ((uint32_t)(v.y != 0u) << 1) |
+                                   ((uint32_t)(v.z != 0u) << 2) | ((uint32_t)(v.w != 0u) << 3);
+                nzm |= b << (4 * o8);
+              }
+              const float2* tl = tab + C * lane;
+              const uint32_t* ndw = nd2 + lane * (C / 2);
+              // a wave-uniform loop (a lane out of words adds 0): a divergent
+              // one made the allocator spill ~90 VGPRs
+              while (__ballot(nzm != 0u)) {
+                const bool has = nzm != 0u;
+                const int i = has ? __builtin_ctz(nzm) : 0;
+                nzm &= nzm - 1u;
+                const uint32_t wv = has ? ndw[i] : 0u;
+                const float4 t2 = *reinterpret_cast<const float4*>(tl + 2 * i);
+                ps += (uint64_t)(wv & 0xFFFFu) * fixp(t2.x) + (uint64_t)(wv >> 16) * fixp(t2.z);
+              }
+#else
 #if SB_ND8
               const uint8_t* ndh = reinterpret_cast<const uint8_t*>(nd2) + C * lane;
 #else
@@ -2814,6 +2865,7 @@ __global__ __launch_bounds__(64 * sb_waves<C>()) SB_ATTR void k_sample_big(Sampl
                 const int o = (j + lane) & (C - 1);
                 ps += (uint64_t)ndh[o] * fixp(tl[o].x);
               }
+#endif
               if (!FROZEN && lane == (int)((uint32_t)zo / (uint32_t)C))
                 ps += (uint64_t)((int64_t)ndz * ((int64_t)Fm1z - (int64_t)Fz));
             }

@@ -1,0 +1,14 @@
+# Round 6, GPU call Y: the alpha part's block-end prefixes held in registers
+# (variants/pfx, -DSB_PFX_REG=1): parity, then C5 near init / after 30 sweeps
+# against the tree, both orders.
+set -o pipefail
+cd "$GRAFT_REPO_ROOT"
+O=gpurun_out/r6y; mkdir -p $O
+for v in pfx; do
+  LDA_MI355X_LIB=variants/$v/liblda_mi355x.so timeout -k 10 400 python -u -m pytest -x -q --timeout 200 \
+    --timeout-method thread -m gpu tests/test_parity_gpu.py tests/test_parity_random_gpu.py -k "large_k or sparse or random" \
+    > $O/parity_$v.log 2>&1 || { tail -20 $O/parity_$v.log; exit 1; }
+  echo "$v $(tail -1 $O/parity_$v.log)"
+done
+bash tools/gpu_r5_c5ab.sh r6y/a 0 tree variants/pfx/liblda_mi355x.so || exit 1
+bash tools/gpu_r5_c5ab.sh r6y/b 0 variants/pfx/liblda_mi355x.so tree || exit 1
