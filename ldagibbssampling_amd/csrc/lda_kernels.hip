@@ -2201,10 +2201,12 @@ __device__ __forceinline__ int nd16_get(const uint32_t* nd2, int k) {
 #ifndef SB_PFX_REG
 #define SB_PFX_REG 1
 #endif
-// 1 (A/B): the A search's document part sums only the nonzero count words
-// of each lane's block (a mask first), not all C topics
+// 1 (default since late round 6): the A search's document part sums only the
+// nonzero count words of each lane's block (a mask first), not all C topics:
+// the same integers; C5 +0.5-0.7% near init, flat after burn-in
+// (profiles/r06/ldsbatch/r6z)
 #ifndef SB_ADOC_SPARSE
-#define SB_ADOC_SPARSE 0
+#define SB_ADOC_SPARSE 1
 #endif
 #ifndef SB_CHUNK_WAIT
 #define SB_CHUNK_WAIT 1
