@@ -2208,6 +2208,14 @@ __device__ __forceinline__ int nd16_get(const uint32_t* nd2, int k) {
 #ifndef SB_ADOC_SPARSE
 #define SB_ADOC_SPARSE 1
 #endif
+// 1 (default since late round 6): a long row's first batch past the register
+// rounds loaded at the token's start instead of after the rounds, so its
+// memory latency overlaps them; C5 +2.7% near init, +1.5% after burn-in, two
+// sessions (profiles/r06/ldsbatch/r6ac, r6ad).  2 (the second batch too)
+// spills 6 VGPRs and loses.
+#ifndef SB_EARLY_BATCH
+#define SB_EARLY_BATCH 1
+#endif
 #ifndef SB_CHUNK_WAIT
 #define SB_CHUNK_WAIT 1
 #endif
@@ -2571,6 +2579,29 @@ __global__ __launch_bounds__(64 * sb_waves<C>()) SB_ATTR void k_sample_big(Sampl
           };
           // (the memory barriers keep the doc reads in the branches: hoisted
           // above the branch, their wait and conversions went with them)
+#if SB_EARLY_BATCH
+          // a long row's first batch past the register rounds issued now, so
+          // its latency overlaps the rounds (zeros when the row has none)
+          uint32_t ea0[SB_BATCH];
+#if SB_EARLY_BATCH >= 2
+          uint32_t eb0[SB_BATCH];
+#endif
+          {
+            const __amdgpu_buffer_rsrc_t rb0 = __builtin_amdgcn_make_buffer_rsrc(
+                (void*)erow, (short)0, nr_all > RB ? n * 4 : 0, kBufWord3);
+            int lo4 = lane * 4;
+            asm volatile("" : "+v"(lo4));
+#pragma unroll
+            for (int b = 0; b < SB_BATCH; ++b) ea0[b] = __builtin_amdgcn_raw_buffer_load_b32(rb0, lo4 + (RB + b) * 256, 0, 0);
+#if SB_EARLY_BATCH >= 2
+            // and the second (a row shorter than it reads zeros: the bound
+            // is the row's own length)
+#pragma unroll
+            for (int b = 0; b < SB_BATCH; ++b)
+              eb0[b] = __builtin_amdgcn_raw_buffer_load_b32(rb0, lo4 + (RB + SB_BATCH + b) * 256, 0, 0);
+#endif
+          }
+#endif
           if (!row_sat) {
             asm volatile("" ::: "memory");
 #if SB_LDS_BATCH > 0
@@ -2673,14 +2704,25 @@ __global__ __launch_bounds__(64 * sb_waves<C>()) SB_ATTR void k_sample_big(Sampl
             uint32_t ea[SB_BATCH];
             int lo4 = lane * 4;
             asm volatile("" : "+v"(lo4));
+#if SB_EARLY_BATCH
+#pragma unroll
+            for (int b = 0; b < SB_BATCH; ++b) ea[b] = ea0[b];
+#else
 #pragma unroll
             for (int b = 0; b < SB_BATCH; ++b)
               ea[b] = __builtin_amdgcn_raw_buffer_load_b32(rb, lo4 + (RB + b) * 256, 0, 0);
+#endif
             int mb = 0;
             for (int q0 = RB; q0 < nr_all; q0 += SB_BATCH, ++mb) {
               // the next batch's loads only when it exists: a load left
               // unconsumed keeps its registers "in flight" into the next token
               uint32_t en[SB_BATCH];
+#if SB_EARLY_BATCH >= 2
+              if (q0 == RB) {
+#pragma unroll
+                for (int b = 0; b < SB_BATCH; ++b) en[b] = eb0[b];
+              } else
+#endif
               if (q0 + SB_BATCH < nr_all) {
                 const int vo = lo4 + (q0 + SB_BATCH) * 256;
 #pragma unroll
