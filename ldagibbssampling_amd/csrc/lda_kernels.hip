@@ -2216,6 +2216,11 @@ __device__ __forceinline__ int nd16_get(const uint32_t* nd2, int k) {
 #ifndef SB_EARLY_BATCH
 #define SB_EARLY_BATCH 1
 #endif
+// 1 (A/B): the ring slot of token t-1 refilled at token t's start rather
+// than after t's register rounds
+#ifndef SB_REFILL_FIRST
+#define SB_REFILL_FIRST 0
+#endif
 #ifndef SB_CHUNK_WAIT
 #define SB_CHUNK_WAIT 1
 #endif
@@ -2482,6 +2487,16 @@ __global__ __launch_bounds__(64 * sb_waves<C>()) SB_ATTR void k_sample_big(Sampl
             pk = -1;
           }
 
+#if SB_REFILL_FIRST
+          {
+            // the slot of token t-1 refilled first thing (its registers were
+            // used up by token t-1): with no FLAT operation in flight the
+            // waits for this token's own slot count past these loads
+            // (vmcnt(N)), and the next rows get a fuller token of lead
+            const int sp = (s + NS - 1) % NS;
+            prefetch(ring[sp], rm1[sp], t + NS - 1);
+          }
+#endif
           const int w = readlane_i(cw, idx);
           const int zo = readlane_i(cz, idx);
           const float u = u01((uint32_t)readlane_i((int)cx0, idx));
@@ -2776,7 +2791,11 @@ __global__ __launch_bounds__(64 * sb_waves<C>()) SB_ATTR void k_sample_big(Sampl
             else batches(true);
           }
 #else
+#if !SB_REFILL_FIRST
           refill();
+#else
+          (void)refill;
+#endif
           if (nr_all > RB) {
             if (!row_sat) batches(false);
             else batches(true);
