@@ -2216,10 +2216,12 @@ __device__ __forceinline__ int nd16_get(const uint32_t* nd2, int k) {
 #ifndef SB_EARLY_BATCH
 #define SB_EARLY_BATCH 1
 #endif
-// 1 (A/B): the ring slot of token t-1 refilled at token t's start rather
-// than after t's register rounds
+// 1 (default since late round 6): the ring slot of token t-1 refilled at
+// token t's start rather than after t's register rounds -- possible once no
+// FLAT operation forces vmcnt(0) (SB_GLOBAL_AS): C5 after 30 sweeps +1.3%,
+// near init within noise, two sessions (profiles/r06/ldsbatch/r6af)
 #ifndef SB_REFILL_FIRST
-#define SB_REFILL_FIRST 0
+#define SB_REFILL_FIRST 1
 #endif
 #ifndef SB_CHUNK_WAIT
 #define SB_CHUNK_WAIT 1
