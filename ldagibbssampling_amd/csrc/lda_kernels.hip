@@ -2223,6 +2223,11 @@ __device__ __forceinline__ int nd16_get(const uint32_t* nd2, int k) {
 #ifndef SB_REFILL_FIRST
 #define SB_REFILL_FIRST 1
 #endif
+// 1 (A/B): Philox x1 (the own-entry accept test) computed on the own-entry
+// path instead of held per lane for the chunk (one VGPR)
+#ifndef SB_X1_LAZY
+#define SB_X1_LAZY 0
+#endif
 #ifndef SB_CHUNK_WAIT
 #define SB_CHUNK_WAIT 1
 #endif
@@ -3053,16 +3058,28 @@ __global__ __launch_bounds__(64 * sb_waves<C>()) SB_ATTR void k_sample_big(Sampl
             const float wo = wk.hi - wk.lo;
             const float4 m1 = rm1[s];
             const float O = (float)(c > 0 ? c - 1 : 0u) * __builtin_fmaf((float)ndz, m1.x, m1.y);
+#if SB_X1_LAZY
+            // x1 of the token's Philox block computed here, on the own-entry
+            // path only, instead of held per lane for the whole chunk
+            uint32_t gt = (uint32_t)t;
+            asm volatile("" : "+s"(gt));
+            uint32_t y0, y1, y2;
+            philox_x012(gbase + (uint64_t)gt, p.c2, p.c3, p.k0, p.k1, y0, y1, y2);
+            const float u1 = u01(y1);
+#else
             const float u1 = u01((uint32_t)readlane_i((int)cx1, idx));
+#endif
             if (!(u1 * wo < O)) {
               // the re-draw (rare): x2 of the token's Philox block, computed
               // here (the token index passes an opaque register, so the block
               // is not hoisted into every token)
               SB_COUNT(4);
+#if !SB_X1_LAZY
               uint32_t gt = (uint32_t)t;
               asm volatile("" : "+s"(gt));
               uint32_t y0, y1, y2;
               philox_x012(gbase + (uint64_t)gt, p.c2, p.c3, p.k0, p.k1, y0, y1, y2);
+#endif
               const float s_lo = (lstar > 0 ? readlane_f(TB, lstar - 1) : 0.0f) + wk.lo;
               const float Tp = ((sumB - wo) + O) + A_f;
               const float thr2 = uniform_f(u01(y2) * Tp);
