@@ -2228,6 +2228,11 @@ __device__ __forceinline__ int nd16_get(const uint32_t* nd2, int k) {
 #ifndef SB_X1_LAZY
 #define SB_X1_LAZY 0
 #endif
+// 1 (A/B): a new document's counts built from the chunk registers instead of
+// a memory read of its topics
+#ifndef SB_DOC_REGS
+#define SB_DOC_REGS 0
+#endif
 #ifndef SB_CHUNK_WAIT
 #define SB_CHUNK_WAIT 1
 #endif
@@ -2378,15 +2383,29 @@ __global__ __launch_bounds__(64 * sb_waves<C>()) SB_ATTR void k_sample_big(Sampl
     uint64_t R = 0;
     auto build_doc = [&](int ts, int te) {
       uint64_t rl = 0;
-      for (int i = ts + lane; i < te; i += 64) {
-        const int k = zr[i];
+      auto add_topic = [&](int k) {
 #if SB_ND8
         atomicAdd(&nd2[k >> 2], 1u << (8 * (k & 3)));
 #else
         atomicAdd(&nd2[k >> 1], (k & 1) ? 0x10000u : 1u);
 #endif
         rl += fixp(tab[k].x);
+      };
+#if SB_DOC_REGS
+      // the document's topics from the chunk registers (tokens cbase ..
+      // cbase + 191, not yet sampled: their old topics, as z in memory
+      // holds them), memory only past them -- no load on a document switch
+      // of a document that fits
+      {
+        const int i0 = cbase + lane;
+        if (i0 >= ts && i0 < te) add_topic(cz);
+        if (i0 + 64 >= ts && i0 + 64 < te) add_topic(z1);
+        if (i0 + 128 >= ts && i0 + 128 < te) add_topic(z2);
       }
+      for (int i = (ts > cbase + 192 ? ts : cbase + 192) + lane; i < te; i += 64) add_topic(zr[i]);
+#else
+      for (int i = ts + lane; i < te; i += 64) add_topic(zr[i]);
+#endif
       R = uniform_u64(wave_sum_u64(rl));
       wave_lds_fence();
     };
