@@ -2228,10 +2228,11 @@ __device__ __forceinline__ int nd16_get(const uint32_t* nd2, int k) {
 #ifndef SB_X1_LAZY
 #define SB_X1_LAZY 0
 #endif
-// 1 (A/B): a new document's counts built from the chunk registers instead of
-// a memory read of its topics
+// 1 (default at the end of round 6): a new document's counts built from the
+// chunk registers instead of a memory read of its topics; the same counts,
+// C5 +0.3% after burn-in, flat near init (profiles/r06/ldsbatch/r6am)
 #ifndef SB_DOC_REGS
-#define SB_DOC_REGS 0
+#define SB_DOC_REGS 1
 #endif
 #ifndef SB_CHUNK_WAIT
 #define SB_CHUNK_WAIT 1
